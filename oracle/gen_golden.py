@@ -1,0 +1,118 @@
+"""Generate the golden fixtures under tests/golden/ from the reference's own CPU path (oracle/_ref).
+
+TEST INFRASTRUCTURE ONLY. Run in the build container, where /root/reference exists:
+    make -C oracle && python oracle/gen_golden.py
+The fixtures are data (inputs + the reference's outputs); they travel with the repo so the parity tests
+run on the GPU box, which has no /root/reference.
+
+Fixtures
+  sedov10.npz    Sedov lattice n=10 (1000 particles): IC, and full state after steps 1..3 (ref_step)
+  noh10.npz      Noh lattice-sphere n=12 (open box): IC and state after steps 1..3
+  kernels.npz    one Sedov n=12 state after 2 steps + the reference neighbor list (CPU layout) and every
+                 per-kernel output computed by the reference *Impl loops on it
+  tree_rand.npz  2000 seeded random points: Hilbert keys, cornerstone leaves (bucket 16), linked octree
+                 arrays, node centers/sizes, neighbor lists + counts with and without h iteration
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import pyoracle as po  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+def snapshot(st, prefix):
+    d = {f"{prefix}{k}": v.copy() for k, v in st.arrays.items()}
+    d[f"{prefix}scalars"] = np.array([st.minDt, st.minDt_m1, st.ttot, st.minDtCourant, st.minDtRho])
+    return d
+
+
+def box_arr(box):
+    return np.array(list(box.lim) + list(box.bnd), dtype=np.float64)
+
+
+def run_steps(ref, st, box, nsteps, name):
+    out = {"box": box_arr(box)}
+    out.update(snapshot(st, "s0_"))
+    for s in range(1, nsteps + 1):
+        ref.step(st, box)
+        out.update(snapshot(st, f"s{s}_"))
+    np.savez_compressed(os.path.join(OUT, name), **out)
+
+
+def main():
+    ref = po.load_ref()
+    if ref is None:
+        raise SystemExit("oracle/_ref/libsphexa_ref.so missing: run `make -C oracle` where /root/reference exists")
+    os.makedirs(OUT, exist_ok=True)
+
+    st, box = po.sedov_state(10)
+    run_steps(ref, st, box, 3, "sedov10.npz")
+
+    st, box = po.noh_state(12)
+    run_steps(ref, st, box, 3, "noh10.npz")
+
+    # per-kernel fixture: state after two steps, then each kernel on the reference's own neighbor list
+    st, box = po.sedov_state(12)
+    ref.step(st, box)
+    ref.step(st, box)
+    ref.sfc_keys(st, box)
+    order = np.argsort(st.keys, kind="stable")
+    for k in po.CONSERVED + ["keys"]:
+        st.arrays[k][:] = st.arrays[k][order]
+    pre = st.copy()
+    nbr, nc = ref.find_neighbors(st, box, iterate_h=True)
+    st.nc[:] = nc
+    out = {"box": box_arr(box), "nbr": nbr, "nc": nc, "h_after_iter": st.h.copy()}
+    out.update(snapshot(pre, "in_"))
+    ref.xmass(st, box, nbr)
+    out["xm"] = st.xm.copy()
+    ref.ve_def_gradh(st, box, nbr)
+    out["kx"], out["gradh"] = st.kx.copy(), st.gradh.copy()
+    ref.eos(st)
+    out["prho"], out["c"] = st.prho.copy(), st.c.copy()
+    ref.iad_divv_curlv(st, box, nbr)
+    for k in ["c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv"]:
+        out[k] = st.arrays[k].copy()
+    ref.av_switches(st, box, nbr)
+    out["alpha"] = st.alpha.copy()
+    out["minDtCourant"] = np.array([ref.momentum_energy(st, box, nbr)])
+    for k in ["du", "ax", "ay", "az"]:
+        out[k] = st.arrays[k].copy()
+    np.savez_compressed(os.path.join(OUT, "kernels.npz"), **out)
+
+    # tree + neighbor search on seeded random points (cstone findneighbors test style, random.hpp seed 42)
+    rng = np.random.default_rng(42)
+    n = 2000
+    st = po.HostState(n)
+    st.x[:] = rng.uniform(-0.5, 0.5, n)
+    st.y[:] = rng.uniform(-0.5, 0.5, n)
+    st.z[:] = np.clip(rng.normal(0.0, 0.15, n), -0.5, 0.4999)
+    box = po.make_box(-0.5, 0.5, True)
+    keys = ref.sfc_keys(st, box).copy()
+    order = np.argsort(keys, kind="stable")
+    for k in ["x", "y", "z"]:
+        st.arrays[k][:] = st.arrays[k][order]
+    st.keys[:] = keys[order]
+    tree = ref.octree(st.keys, 16)
+    cen, siz = ref.node_centers(tree["prefixes"], box)
+    st.h[:] = np.float32(0.06)
+    out = {"x": st.x.copy(), "y": st.y.copy(), "z": st.z.copy(), "keys_unsorted": keys, "order": order,
+           "box": box_arr(box), "centers": cen, "sizes": siz}
+    out.update({f"tree_{k}": v for k, v in tree.items()})
+    nbr, nc = ref.find_neighbors(st, box, bucket=16, iterate_h=False)
+    out["nbr_noiter"], out["nc_noiter"] = nbr, nc
+    h0 = st.h.copy()
+    nbr, nc = ref.find_neighbors(st, box, bucket=16, iterate_h=True)
+    out["nbr_iter"], out["nc_iter"], out["h_iter"], out["h0"] = nbr, nc, st.h.copy(), h0
+    np.savez_compressed(os.path.join(OUT, "tree_rand.npz"), **out)
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,342 @@
+"""Python side of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Loads oracle/libsphexa_oracle.so (the plain-C restatement, oracle/sph_oracle.c) and, when it was built
+in this container, oracle/_ref/libsphexa_ref.so (the reference's own CPU path compiled from
+/root/reference by oracle/Makefile).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg import this module, and only as the checker; the product library never links or calls it.
+
+Also holds the numpy restatement of the Sedov / Noh initial conditions used to feed both sides:
+  Sedov: main/src/init/sedov_init.hpp:48-96, sedov_constants.hpp:11-21, grid.hpp:102-132
+  Noh:   main/src/init/noh_init.hpp:46-100 (lattice-cut-sphere substitute)
+"""
+
+import ctypes as C
+import math
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "libsphexa_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libsphexa_ref.so")
+
+KTABLE = 20000
+
+
+class OxBox(C.Structure):
+    _fields_ = [("lim", C.c_double * 6), ("bnd", C.c_int32 * 3)]
+
+
+class OxParams(C.Structure):
+    _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
+                ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
+                ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double)]
+
+
+STATE_FIELDS = [
+    ("x", np.float64), ("y", np.float64), ("z", np.float64),
+    ("x_m1", np.float32), ("y_m1", np.float32), ("z_m1", np.float32),
+    ("vx", np.float32), ("vy", np.float32), ("vz", np.float32),
+    ("temp", np.float64), ("h", np.float32), ("m", np.float32), ("alpha", np.float32),
+    ("du_m1", np.float32), ("id", np.uint64),
+    ("du", np.float64),
+    ("ax", np.float32), ("ay", np.float32), ("az", np.float32), ("prho", np.float32), ("c", np.float32),
+    ("xm", np.float32), ("kx", np.float32), ("gradh", np.float32), ("divv", np.float32), ("curlv", np.float32),
+    ("c11", np.float32), ("c12", np.float32), ("c13", np.float32), ("c22", np.float32), ("c23", np.float32),
+    ("c33", np.float32), ("nc", np.uint32), ("keys", np.uint64),
+]
+CONSERVED = ["x", "y", "z", "x_m1", "y_m1", "z_m1", "vx", "vy", "vz", "temp", "h", "m", "alpha", "du_m1", "id"]
+
+_CT = {np.float64: C.c_double, np.float32: C.c_float, np.uint64: C.c_uint64, np.uint32: C.c_uint32}
+
+
+class OxState(C.Structure):
+    _fields_ = [("n", C.c_size_t)] + [(name, C.POINTER(_CT[t])) for name, t in STATE_FIELDS] + [
+        ("minDt", C.c_double), ("minDt_m1", C.c_double), ("ttot", C.c_double), ("minDtCourant", C.c_double),
+        ("minDtRho", C.c_double)]
+
+
+def default_params(K):
+    """ParticlesData defaults (particles_data.hpp:86-138)."""
+    return OxParams(K=K, ng0=100, ngmax=150, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0,
+                    alphamin=0.05, alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
+                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1)
+
+
+def make_box(lo=-0.5, hi=0.5, periodic=True):
+    b = OxBox()
+    for k, v in enumerate([lo, hi, lo, hi, lo, hi]):
+        b.lim[k] = v
+    for k in range(3):
+        b.bnd[k] = 1 if periodic else 0
+    return b
+
+
+class HostState:
+    """numpy-owned particle state with an OxState view."""
+
+    def __init__(self, n):
+        self.n = n
+        self.arrays = {name: np.zeros(n, dtype=t) for name, t in STATE_FIELDS}
+        self.minDt = 1e-6
+        self.minDt_m1 = 1e-6
+        self.ttot = 0.0
+        self.minDtCourant = math.inf
+        self.minDtRho = math.inf
+
+    def __getattr__(self, item):
+        arrays = self.__dict__.get("arrays")
+        if arrays is not None and item in arrays:
+            return arrays[item]
+        raise AttributeError(item)
+
+    def struct(self):
+        s = OxState()
+        s.n = self.n
+        for name, t in STATE_FIELDS:
+            a = self.arrays[name]
+            assert a.flags["C_CONTIGUOUS"] and a.dtype == t
+            setattr(s, name, a.ctypes.data_as(C.POINTER(_CT[t])))
+        s.minDt, s.minDt_m1, s.ttot = self.minDt, self.minDt_m1, self.ttot
+        s.minDtCourant, s.minDtRho = self.minDtCourant, self.minDtRho
+        self._s = s
+        return s
+
+    def pull(self, s):
+        self.minDt, self.minDt_m1, self.ttot = s.minDt, s.minDt_m1, s.ttot
+        self.minDtCourant, self.minDtRho = s.minDtCourant, s.minDtRho
+
+    def copy(self):
+        o = HostState(self.n)
+        for k, v in self.arrays.items():
+            o.arrays[k][:] = v
+        o.minDt, o.minDt_m1, o.ttot = self.minDt, self.minDt_m1, self.ttot
+        o.minDtCourant, o.minDtRho = self.minDtCourant, self.minDtRho
+        return o
+
+
+def ideal_gas_cv(mui=np.float32(10.0), gamma=5.0 / 3.0):
+    """idealGasCv<float,double> (sph/eos.hpp:13-18): R is a float constant, result float."""
+    R = np.float32(8.317e7)
+    return np.float32(np.float64(R / np.float32(mui)) / (gamma - 1.0))
+
+
+def sedov_state(side):
+    """Sedov lattice IC (sedov_init.hpp:48-96, 106-130; grid.hpp:102-132); box [-0.5,0.5]^3 periodic."""
+    r = 0.5
+    n = side ** 3
+    st = HostState(n)
+    step = (2.0 * r) / side
+    r_ini = -r + 0.5 * step
+    idx = np.arange(side, dtype=np.float64)
+    coord = r_ini + idx * step
+    zz, yy, xx = np.meshgrid(coord, coord, coord, indexing="ij")
+    st.x[:] = xx.ravel()
+    st.y[:] = yy.ravel()
+    st.z[:] = zz.ravel()
+    ng0 = 100
+    total_volume = (2 * r) ** 3
+    h_init = np.cbrt(3.0 / (4 * math.pi) * ng0 * total_volume / n) * 0.5
+    st.m[:] = np.float32(1.0 / n)
+    st.h[:] = np.float32(h_init)
+    st.alpha[:] = np.float32(0.05)
+    width = 0.1
+    ener0 = 1.0 / math.pi ** 1.5 / 1.0 / width ** 3.0
+    u0 = 1e-8
+    cv = ideal_gas_cv()
+    r2 = st.x * st.x + st.y * st.y + st.z * st.z
+    ui = ener0 * np.exp(-(r2 / (width * width))) + u0
+    st.temp[:] = ui / np.float64(cv)
+    st.id[:] = np.arange(n, dtype=np.uint64)
+    st.minDt = 1e-6
+    st.minDt_m1 = 1e-6
+    return st, make_box(-r, r, True)
+
+
+def noh_state(side):
+    """Noh substitute: side^3 lattice in [-0.5,0.5]^3 cut to r<=0.5, open box,
+    v = -r_hat, T = 1e-20/cv, dt0 = 1e-4 (noh_init.hpp:46-100 field values)."""
+    r = 0.5
+    step = (2.0 * r) / side
+    r_ini = -r + 0.5 * step
+    idx = np.arange(side, dtype=np.float64)
+    coord = r_ini + idx * step
+    zz, yy, xx = np.meshgrid(coord, coord, coord, indexing="ij")
+    x, y, z = xx.ravel(), yy.ravel(), zz.ravel()
+    rad = np.sqrt(x * x + y * y + z * z)
+    keep = rad <= r
+    x, y, z, rad = x[keep], y[keep], z[keep], rad[keep]
+    n = x.size
+    st = HostState(n)
+    st.x[:], st.y[:], st.z[:] = x, y, z
+    vol = 4.0 / 3.0 * math.pi * r ** 3
+    ng0 = 100
+    h_init = np.cbrt(3.0 / (4 * math.pi) * ng0 * vol / n) * 0.5
+    st.m[:] = np.float32(1.0 / n)
+    st.h[:] = np.float32(h_init)
+    st.alpha[:] = np.float32(0.05)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = np.where(rad > 0, 1.0 / rad, 0.0)
+    st.vx[:] = (-x * inv).astype(np.float32)
+    st.vy[:] = (-y * inv).astype(np.float32)
+    st.vz[:] = (-z * inv).astype(np.float32)
+    st.temp[:] = 1e-20 / np.float64(ideal_gas_cv())
+    st.id[:] = np.arange(n, dtype=np.uint64)
+    st.minDt = 1e-4
+    st.minDt_m1 = 1e-4
+    lo, hi = -0.5 - 1e-3, 0.5 + 1e-3
+    return st, make_box(lo, hi, False)
+
+
+def _bind(lib):
+    P = C.c_void_p
+    u32p = C.POINTER(C.c_uint32)
+    for name, res, args in [
+        ("kernel_tables", None, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_double)]),
+        ("sfc_keys", None, [P, P, P, C.c_size_t, C.POINTER(OxBox), P]),
+        ("compute_octree", C.c_int, [P, C.c_size_t, C.c_uint, P, P, C.c_int]),
+        ("build_octree", None, [P, C.c_int, P, P, P, P, P, P]),
+        ("node_centers", None, [P, C.c_int, C.POINTER(OxBox), P, P]),
+        ("find_neighbors", None, [P, P, P, P, P, C.c_size_t, C.c_uint, C.c_uint, C.POINTER(OxBox), C.c_uint,
+                                  C.c_uint, C.c_uint, C.c_int, u32p, u32p]),
+        ("xmass", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint, C.c_uint]),
+        ("ve_def_gradh", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint,
+                                C.c_uint]),
+        ("eos", None, [C.POINTER(OxState), C.POINTER(OxParams), C.c_uint, C.c_uint]),
+        ("iad_divv_curlv", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint,
+                                  C.c_uint]),
+        ("av_switches", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint,
+                               C.c_uint]),
+        ("momentum_energy", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p,
+                                          C.c_uint, C.c_uint]),
+        ("positions", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint, C.c_uint]),
+        ("update_h_range", None, [C.POINTER(OxState), C.c_uint, C.c_uint, C.c_uint]),
+        ("step", C.c_int, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint]),
+        ("update_h", C.c_float, [C.c_uint, C.c_uint, C.c_float]),
+    ]:
+        for prefix in ("ref_", "ox_"):
+            if hasattr(lib, prefix + name):
+                f = getattr(lib, prefix + name)
+                f.restype = res
+                f.argtypes = args
+                setattr(lib, name, f)
+    return lib
+
+
+class Lib:
+    """Thin wrapper that offers the same python API for both the reference and the restatement."""
+
+    def __init__(self, path):
+        self.path = path
+        self.lib = _bind(C.CDLL(path))
+        wh = np.zeros(KTABLE, np.float32)
+        whd = np.zeros(KTABLE, np.float32)
+        K = C.c_double()
+        self.lib.kernel_tables(wh.ctypes.data_as(C.POINTER(C.c_float)), whd.ctypes.data_as(C.POINTER(C.c_float)),
+                               C.byref(K))
+        self.wh, self.whd, self.K = wh, whd, K.value
+
+    def params(self):
+        return default_params(self.K)
+
+    def sfc_keys(self, st, box):
+        self.lib.sfc_keys(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.n, C.byref(box),
+                          st.keys.ctypes.data)
+        return st.keys
+
+    def octree(self, keys, bucket):
+        n = keys.size
+        nleaf = self.lib.compute_octree(keys.ctypes.data, n, bucket, None, None, 0)
+        leaves = np.zeros(nleaf + 1, np.uint64)
+        counts = np.zeros(nleaf, np.uint32)
+        self.lib.compute_octree(keys.ctypes.data, n, bucket, leaves.ctypes.data, counts.ctypes.data, nleaf)
+        nint = (nleaf - 1) // 7
+        ntot = nleaf + nint
+        out = dict(leaves=leaves, counts=counts, prefixes=np.zeros(ntot, np.uint64),
+                   childOffsets=np.zeros(ntot + 1, np.int32), parents=np.zeros(max(1, (ntot - 1) // 8), np.int32),
+                   levelRange=np.zeros(23, np.int32), internalToLeaf=np.zeros(ntot, np.int32),
+                   leafToInternal=np.zeros(ntot, np.int32))
+        self.lib.build_octree(leaves.ctypes.data, nleaf, out["prefixes"].ctypes.data, out["childOffsets"].ctypes.data,
+                              out["parents"].ctypes.data, out["levelRange"].ctypes.data,
+                              out["internalToLeaf"].ctypes.data, out["leafToInternal"].ctypes.data)
+        return out
+
+    def node_centers(self, prefixes, box):
+        nn = prefixes.size
+        c = np.zeros((nn, 3), np.float64)
+        s = np.zeros((nn, 3), np.float64)
+        self.lib.node_centers(prefixes.ctypes.data, nn, C.byref(box), c.ctypes.data, s.ctypes.data)
+        return c, s
+
+    def find_neighbors(self, st, box, first=0, last=None, bucket=64, iterate_h=True, ngmax=150, ng0=100):
+        last = st.n if last is None else last
+        nbr = np.zeros((last - first) * ngmax, np.uint32)
+        nc = np.zeros(last - first, np.uint32)
+        self.lib.find_neighbors(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.h.ctypes.data,
+                                st.keys.ctypes.data, st.n, first, last, C.byref(box), bucket, ng0, ngmax,
+                                int(iterate_h), nbr.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                nc.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return nbr, nc
+
+    def _kern(self, name, st, box, nbr, first, last, params=None):
+        p = params or self.params()
+        s = st.struct()
+        f = getattr(self.lib, name)
+        ptr = nbr.ctypes.data_as(C.POINTER(C.c_uint32))
+        r = f(C.byref(s), C.byref(p), C.byref(box), ptr, first, last)
+        st.pull(s)
+        return r
+
+    def xmass(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("xmass", st, box, nbr, first, st.n if last is None else last, params)
+
+    def ve_def_gradh(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("ve_def_gradh", st, box, nbr, first, st.n if last is None else last, params)
+
+    def iad_divv_curlv(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("iad_divv_curlv", st, box, nbr, first, st.n if last is None else last, params)
+
+    def av_switches(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("av_switches", st, box, nbr, first, st.n if last is None else last, params)
+
+    def momentum_energy(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("momentum_energy", st, box, nbr, first, st.n if last is None else last, params)
+
+    def eos(self, st, first=0, last=None, params=None):
+        p = params or self.params()
+        s = st.struct()
+        self.lib.eos(C.byref(s), C.byref(p), first, st.n if last is None else last)
+
+    def positions(self, st, box, first=0, last=None, params=None):
+        p = params or self.params()
+        s = st.struct()
+        self.lib.positions(C.byref(s), C.byref(p), C.byref(box), first, st.n if last is None else last)
+
+    def step(self, st, box, bucket=64, params=None):
+        p = params or self.params()
+        s = st.struct()
+        r = self.lib.step(C.byref(s), C.byref(p), C.byref(box), bucket)
+        st.pull(s)
+        return r
+
+
+def load_ref():
+    """The reference's own CPU path, or None when it was not built (e.g. on the GPU box without the .so)."""
+    if not os.path.exists(REF_SO):
+        return None
+    return Lib(REF_SO)
+
+
+def load_oracle():
+    if not os.path.exists(ORACLE_SO):
+        raise FileNotFoundError(ORACLE_SO + " not built: run `make -C oracle`")
+    return Lib(ORACLE_SO)
+
+
+def total_energy(st):
+    """kinetic + internal energy (conserved_quantities.hpp:49-93 restated; u = cv*T)."""
+    cv = np.float64(ideal_gas_cv())
+    v2 = st.vx.astype(np.float64) ** 2 + st.vy.astype(np.float64) ** 2 + st.vz.astype(np.float64) ** 2
+    m = st.m.astype(np.float64)
+    return float(np.sum(0.5 * m * v2) + np.sum(m * cv * st.temp))

@@ -1,0 +1,1265 @@
+/* sph_oracle.c -- CPU restatement of the SPH-EXA VE hot path, in plain C11 + OpenMP.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the checker: tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load it (via oracle/pyoracle.py); the product library (sph-exa_amd/) never links or
+ * calls anything here.  Parity status: PINNED -- tests/test_oracle_vs_ref.py checks every function below
+ * bit-for-bit against the reference's own CPU path compiled from /root/reference (oracle/_ref), and
+ * tests/test_oracle_golden.py against the committed fixtures under tests/golden/ (generated from _ref by
+ * oracle/gen_golden.py) and the reference's known-answer test data (sph/test/ve.cpp:112-233).
+ *
+ * Every function restates one reference function; citations are /root/reference paths.  Expressions
+ * keep the reference's operand order *and* its implicit float/double promotions (e.g. `K` is double,
+ * so `rho0 * K * h3Inv` is evaluated in double), so that with identical neighbor order the results are
+ * bitwise identical to the reference compiled with the same flags (no FMA contraction).
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "sx_host_types.h"
+
+#define KTABLE 20000
+#define MAXLEVEL 21 /* maxTreeLevel<uint64_t> (sfc/sfc.hpp:119-127) */
+#define UNUSED_BITS 1
+
+typedef uint64_t key_t_;
+
+/* ------------------------------------------------------------------------------------------------
+ * kernel tables (sph_kernel_tables.hpp, kernels.hpp:35-59)
+ * ------------------------------------------------------------------------------------------------ */
+
+static double wharmonic_std(double v) /* kernels.hpp:35-42 */
+{
+    if (v == 0.0) return 1.0;
+    const double Pv = M_PI_2 * v;
+    return sin(Pv) / Pv;
+}
+
+static double wharmonic_derivative_std(double v) /* kernels.hpp:48-57 */
+{
+    if (v == 0.0) return 0.0;
+    const double piHalf = M_PI_2;
+    const double Pv     = piHalf * v;
+    const double sincv  = sin(Pv) / (Pv);
+    return sincv * piHalf * ((cos(Pv) / sin(Pv)) - 1.0 / Pv);
+}
+
+static double sinc6(double x) { return pow(wharmonic_std(x), 6.0); } /* getSphKernel sinc_n, :143-147 */
+
+static double sinc6_derivative(double x) /* powSincDerivative, :104-108 */
+{
+    return 6.0 * pow(wharmonic_std(x), 6.0 - 1) * wharmonic_derivative_std(x);
+}
+
+static int cmp_double(const void* a, const void* b)
+{
+    double x = *(const double*)a, y = *(const double*)b;
+    return (x > y) - (x < y);
+}
+
+static double kernel_vol(double x) { return 4.0 * M_PI * x * x * sinc6(x); }
+
+/* util::simpson (sph_kernel_tables.hpp:27-56), samples sorted before accumulation */
+static double simpson(double a, double b, uint64_t n)
+{
+    uint64_t numOdd  = n / 2;
+    uint64_t numEven = (numOdd >= 1) ? numOdd - 1 : 0;
+    double   h       = (b - a) / (double)n;
+    double*  odd     = (double*)malloc(sizeof(double) * (numOdd ? numOdd : 1));
+    double*  even    = (double*)malloc(sizeof(double) * (numEven ? numEven : 1));
+    for (uint64_t i = 0; i < numOdd; ++i)
+        odd[i] = kernel_vol(a + (double)(2 * (i + 1) - 1) * h);
+    for (uint64_t i = 0; i < numEven; ++i)
+        even[i] = kernel_vol(a + (double)(2 * (i + 1)) * h);
+    qsort(odd, numOdd, sizeof(double), cmp_double);
+    qsort(even, numEven, sizeof(double), cmp_double);
+    double so = 0.0, se = 0.0;
+    for (uint64_t i = 0; i < numOdd; ++i)
+        so += odd[i];
+    for (uint64_t i = 0; i < numEven; ++i)
+        se += even[i];
+    free(odd);
+    free(even);
+    return h / 3.0 * (kernel_vol(a) + kernel_vol(b) + 4.0 * so + 2.0 * se);
+}
+
+/* kernel_3D_k (:78-85) and tabulateFunction<float, 20000> (:88-101) */
+void ox_kernel_tables(float* wh, float* whd, double* K)
+{
+    *K                 = 1.0 / simpson(0, 2.0, 2000);
+    const float dx     = (float)((2.0 - 0.0) / (KTABLE - 1));
+    for (size_t i = 0; i < KTABLE; ++i)
+    {
+        float nv = (float)(0.0 + (float)i * dx);
+        wh[i]    = (float)sinc6((double)nv);
+        whd[i]   = (float)sinc6_derivative((double)nv);
+    }
+}
+
+/* lt::lookup<float> (table_lookup.hpp:14-26) */
+static inline float lookup(const float* table, float v)
+{
+    const int   numIntervals = KTABLE - 1;
+    const float support      = 2.0f;
+    const float dx           = support / numIntervals;
+    const float invDx        = 1.0f / dx;
+    int         idx          = (int)(v * invDx);
+    float derivative = (idx >= numIntervals) ? 0.0f : (table[idx + 1] - table[idx]) * invDx;
+    return (idx >= numIntervals) ? 0.0f : table[idx] + derivative * (v - (float)idx * dx);
+}
+
+float ox_lookup(const float* table, float v) { return lookup(table, v); }
+
+/* updateH<float> (kernels.hpp:26-32) */
+float ox_update_h(unsigned ng0, unsigned nc, float h)
+{
+    const float c0 = 1023.0f;
+    const float ex = (float)(1.0 / 10.0);
+    return h * 0.5f * powf(1.0f + c0 * ng0 / (float)nc, ex);
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * box helpers (cstone/sfc/box.hpp:193-267)
+ * ------------------------------------------------------------------------------------------------ */
+
+static inline double box_l(const ox_box* b, int d) { return b->lim[2 * d + 1] - b->lim[2 * d]; }
+static inline double box_il(const ox_box* b, int d) { return 1.0 / (b->lim[2 * d + 1] - b->lim[2 * d]); }
+static inline int    box_pbc(const ox_box* b, int d) { return b->bnd[d] == 1; }
+
+/* legacy applyPBC<double,float> (:233-255): xx -= lx is evaluated in double, then rounded */
+static inline void applyPBC(const ox_box* b, float r, float* xx, float* yy, float* zz)
+{
+    if (box_pbc(b, 0) && *xx > r) *xx = (float)((double)*xx - box_l(b, 0));
+    else if (box_pbc(b, 0) && *xx < -r) *xx = (float)((double)*xx + box_l(b, 0));
+    if (box_pbc(b, 1) && *yy > r) *yy = (float)((double)*yy - box_l(b, 1));
+    else if (box_pbc(b, 1) && *yy < -r) *yy = (float)((double)*yy + box_l(b, 1));
+    if (box_pbc(b, 2) && *zz > r) *zz = (float)((double)*zz - box_l(b, 2));
+    else if (box_pbc(b, 2) && *zz < -r) *zz = (float)((double)*zz + box_l(b, 2));
+}
+
+/* distancePBC<double,float> (:257-267) */
+static inline float distancePBC(const ox_box* b, float hi, double x1, double y1, double z1, double x2, double y2,
+                                double z2)
+{
+    float xx = (float)(x1 - x2);
+    float yy = (float)(y1 - y2);
+    float zz = (float)(z1 - z2);
+    applyPBC(b, 2.0f * hi, &xx, &yy, &zz);
+    return sqrtf(xx * xx + yy * yy + zz * zz);
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Hilbert SFC (sfc/hilbert.hpp:60-105, 145-190; sfc/sfc.hpp:157-194)
+ * ------------------------------------------------------------------------------------------------ */
+
+static key_t_ iHilbert(unsigned px, unsigned py, unsigned pz)
+{
+    static const unsigned mortonToHilbert[8] = {0, 1, 3, 2, 7, 6, 4, 5};
+    key_t_ key = 0;
+    for (int level = MAXLEVEL - 1; level >= 0; --level)
+    {
+        unsigned xi     = (px >> level) & 1u;
+        unsigned yi     = (py >> level) & 1u;
+        unsigned zi     = (pz >> level) & 1u;
+        unsigned octant = (xi << 2) | (yi << 1) | zi;
+        key             = (key << 3) + mortonToHilbert[octant];
+        px ^= -(xi & ((!yi) | zi));
+        py ^= -((xi & (yi | zi)) | (yi & (!zi)));
+        pz ^= -((xi & (!yi) & (!zi)) | (yi & (!zi)));
+        if (zi)
+        {
+            unsigned pt = px;
+            px          = py;
+            py          = pz;
+            pz          = pt;
+        }
+        else if (!yi)
+        {
+            unsigned pt = px;
+            px          = pz;
+            pz          = pt;
+        }
+    }
+    return key;
+}
+
+static void decodeHilbert(key_t_ key, unsigned* ox, unsigned* oy, unsigned* oz)
+{
+    unsigned px = 0, py = 0, pz = 0;
+    for (unsigned level = 0; level < MAXLEVEL; ++level)
+    {
+        unsigned       octant = (key >> (3 * level)) & 7u;
+        const unsigned xi     = octant >> 2u;
+        const unsigned yi     = (octant >> 1u) & 1u;
+        const unsigned zi     = octant & 1u;
+        if (yi ^ zi)
+        {
+            unsigned pt = px;
+            px          = pz;
+            pz          = py;
+            py          = pt;
+        }
+        else if ((!xi & !yi & !zi) || (xi & yi & zi))
+        {
+            unsigned pt = px;
+            px          = pz;
+            pz          = pt;
+        }
+        unsigned mask = (1u << level) - 1;
+        px ^= mask & (-(xi & (yi | zi)));
+        py ^= mask & (-((xi & ((!yi) | (!zi))) | ((!xi) & yi & zi)));
+        pz ^= mask & (-((xi & (!yi) & (!zi)) | (yi & zi)));
+        px |= (xi << level);
+        py |= ((xi ^ yi) << level);
+        pz |= ((yi ^ zi) << level);
+    }
+    *ox = px;
+    *oy = py;
+    *oz = pz;
+}
+
+/* sfc3D<HilbertKey<uint64_t>, double> (sfc.hpp:157-194) */
+static key_t_ sfc3D(double x, double y, double z, const ox_box* b)
+{
+    const unsigned cubeLength = 1u << MAXLEVEL;
+    const int      mcoord     = (1 << MAXLEVEL) - 1;
+    double mx = cubeLength * box_il(b, 0), my = cubeLength * box_il(b, 1), mz = cubeLength * box_il(b, 2);
+    int    ix = (int)(floor(x * mx) - b->lim[0] * mx);
+    int    iy = (int)(floor(y * my) - b->lim[2] * my);
+    int    iz = (int)(floor(z * mz) - b->lim[4] * mz);
+    ix        = ix < mcoord ? ix : mcoord;
+    iy        = iy < mcoord ? iy : mcoord;
+    iz        = iz < mcoord ? iz : mcoord;
+    return iHilbert((unsigned)ix, (unsigned)iy, (unsigned)iz);
+}
+
+void ox_sfc_keys(const double* x, const double* y, const double* z, size_t n, const ox_box* b, uint64_t* keys)
+{
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; ++i)
+        keys[i] = sfc3D(x[i], y[i], z[i], b);
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * cornerstone octree (tree/csarray.hpp:290-467, tree/octree.hpp:95-213, sfc/common.hpp)
+ * ------------------------------------------------------------------------------------------------ */
+
+static inline int      clz64(key_t_ v) { return v ? __builtin_clzll(v) : 64; }
+static inline key_t_   nodeRange(unsigned level) { return (key_t_)1 << (3u * (MAXLEVEL - level)); }
+static inline unsigned treeLevel(key_t_ range) { return (unsigned)(clz64(range - 1) - UNUSED_BITS) / 3; }
+static inline int      commonPrefix(key_t_ a, key_t_ b) { return clz64(a ^ b) - UNUSED_BITS; }
+static inline key_t_   encodePlaceholderBit(key_t_ code, int prefixLength)
+{
+    int nShifts = 3 * MAXLEVEL - prefixLength;
+    return ((key_t_)1 << prefixLength) | (code >> nShifts);
+}
+static inline unsigned decodePrefixLength(key_t_ code) { return 8 * sizeof(key_t_) - 1 - clz64(code); }
+static inline key_t_   decodePlaceholderBit(key_t_ code)
+{
+    int prefixLength = (int)decodePrefixLength(code);
+    return (code ^ ((key_t_)1 << prefixLength)) << (3 * MAXLEVEL - prefixLength);
+}
+static inline unsigned octalDigit(key_t_ code, unsigned position)
+{
+    return (unsigned)(code >> (3u * (MAXLEVEL - position))) & 7u;
+}
+static inline int digitWeight(int digit)
+{
+    int fourGeqMask = -(int)(digit >= 4);
+    return ((7 - digit) & fourGeqMask) - (digit & ~fourGeqMask);
+}
+
+static size_t lower_bound_u64(const key_t_* a, size_t n, key_t_ v)
+{
+    size_t lo = 0, hi = n;
+    while (lo < hi)
+    {
+        size_t mid = (lo + hi) / 2;
+        if (a[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+typedef struct
+{
+    key_t_*   leaves;
+    unsigned* counts;
+    size_t    n, cap;
+} leafbuf;
+
+static void push_leaf(leafbuf* lb, key_t_ k, unsigned c)
+{
+    if (lb->n == lb->cap)
+    {
+        lb->cap    = lb->cap ? 2 * lb->cap : 1024;
+        lb->leaves = (key_t_*)realloc(lb->leaves, lb->cap * sizeof(key_t_));
+        lb->counts = (unsigned*)realloc(lb->counts, lb->cap * sizeof(unsigned));
+    }
+    lb->leaves[lb->n] = k;
+    lb->counts[lb->n] = c;
+    lb->n++;
+}
+
+/* The converged cornerstone tree of computeOctree (csarray.hpp:456-467) is the unique tree in which a
+ * node is split iff its particle count exceeds the bucket size and it is above the maximum level
+ * (calculateNodeOp, :233-255): restated here as a depth-first split in key order. */
+static void split_node(const key_t_* keys, size_t n, key_t_ start, unsigned level, unsigned bucket, leafbuf* lb)
+{
+    key_t_ end   = start + nodeRange(level);
+    size_t lo    = lower_bound_u64(keys, n, start);
+    size_t hi    = lower_bound_u64(keys, n, end);
+    size_t count = hi - lo;
+    if (count > bucket && level < MAXLEVEL)
+    {
+        for (int s = 0; s < 8; ++s)
+            split_node(keys + lo, count, start + (key_t_)s * nodeRange(level + 1), level + 1, bucket, lb);
+    }
+    else { push_leaf(lb, start, (unsigned)count); }
+}
+
+int ox_compute_octree(const uint64_t* keys, size_t n, unsigned bucket, uint64_t* leaves, unsigned* counts, int cap)
+{
+    leafbuf lb = {0, 0, 0, 0};
+    split_node(keys, n, 0, 0, bucket, &lb);
+    int nLeaf = (int)lb.n;
+    if (cap >= nLeaf)
+    {
+        memcpy(leaves, lb.leaves, nLeaf * sizeof(key_t_));
+        leaves[nLeaf] = nodeRange(0);
+        memcpy(counts, lb.counts, nLeaf * sizeof(unsigned));
+    }
+    free(lb.leaves);
+    free(lb.counts);
+    return nLeaf;
+}
+
+static int binaryKeyWeight(key_t_ key, unsigned level) /* octree.hpp:58-68 */
+{
+    int ret = 0;
+    for (unsigned l = 1; l <= level + 1; ++l)
+        ret += digitWeight((int)octalDigit(key, l));
+    return ret;
+}
+
+typedef struct
+{
+    key_t_ prefix;
+    int    idx;
+} prefix_pair;
+
+static int cmp_prefix(const void* a, const void* b)
+{
+    key_t_ x = ((const prefix_pair*)a)->prefix, y = ((const prefix_pair*)b)->prefix;
+    return (x > y) - (x < y);
+}
+
+/* buildOctreeCpu (octree.hpp:185-213) with createUnsortedLayoutCpu (:79-107), linkTreeCpu (:124-158),
+ * getLevelRangeCpu (:161-172) */
+void ox_build_octree(const uint64_t* leaves, int numLeaves, uint64_t* prefixes, int* childOffsets, int* parents,
+                     int* levelRange, int* internalToLeaf, int* leafToInternal)
+{
+    int          nInt = (numLeaves - 1) / 7;
+    int          nTot = numLeaves + nInt;
+    prefix_pair* pp   = (prefix_pair*)malloc(sizeof(prefix_pair) * nTot);
+    for (int tid = 0; tid < numLeaves; ++tid)
+    {
+        key_t_   key         = leaves[tid];
+        unsigned level       = treeLevel(leaves[tid + 1] - key);
+        pp[tid + nInt].prefix = encodePlaceholderBit(key, 3 * (int)level);
+        pp[tid + nInt].idx    = tid + nInt;
+        int prefixLength     = commonPrefix(key, leaves[tid + 1]);
+        if (prefixLength % 3 == 0 && tid < numLeaves - 1)
+        {
+            int octIndex         = (tid + binaryKeyWeight(key, (unsigned)prefixLength / 3)) / 7;
+            pp[octIndex].prefix  = encodePlaceholderBit(key, prefixLength);
+            pp[octIndex].idx     = octIndex;
+        }
+    }
+    qsort(pp, nTot, sizeof(prefix_pair), cmp_prefix); /* prefixes are unique: stable not needed */
+    for (int i = 0; i < nTot; ++i)
+    {
+        prefixes[i]       = pp[i].prefix;
+        internalToLeaf[i] = pp[i].idx;
+    }
+    free(pp);
+    for (int i = 0; i < nTot; ++i)
+        leafToInternal[internalToLeaf[i]] = i;
+    for (int i = 0; i < nTot; ++i)
+        internalToLeaf[i] -= nInt;
+    for (unsigned level = 0; level <= MAXLEVEL; ++level)
+        levelRange[level] = (int)lower_bound_u64(prefixes, nTot, encodePlaceholderBit(0, 3 * (int)level));
+    levelRange[MAXLEVEL + 1] = nTot;
+    for (int i = 0; i < nTot; ++i)
+        childOffsets[i] = 0;
+    for (int i = 0; i < nInt; ++i)
+    {
+        int      idxA         = leafToInternal[i];
+        key_t_   prefix       = prefixes[idxA];
+        key_t_   nodeKey      = decodePlaceholderBit(prefix);
+        unsigned prefixLength = decodePrefixLength(prefix);
+        unsigned level        = prefixLength / 3;
+        key_t_   childPrefix  = encodePlaceholderBit(nodeKey, (int)prefixLength + 3);
+        int      s0 = levelRange[level + 1], s1 = levelRange[level + 2];
+        int      childIdx = s0 + (int)lower_bound_u64(prefixes + s0, (size_t)(s1 - s0), childPrefix);
+        if (childIdx != s1 && childPrefix == prefixes[childIdx])
+        {
+            childOffsets[idxA]          = childIdx;
+            parents[(childIdx - 1) / 8] = idxA;
+        }
+    }
+}
+
+/* nodeFpCenters (focus/source_center.hpp:146-157) with hilbertIBox (hilbert.hpp:274-290) and
+ * centerAndSize (sfc/box.hpp:333-348) */
+void ox_node_centers(const uint64_t* prefixes, int numNodes, const ox_box* b, double* centers, double* sizes)
+{
+    const int    maxCoord = 1 << MAXLEVEL;
+    const double uL       = 1.0 / maxCoord;
+    double       hx = 0.5 * uL * box_l(b, 0), hy = 0.5 * uL * box_l(b, 1), hz = 0.5 * uL * box_l(b, 2);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < numNodes; ++i)
+    {
+        key_t_   prefix     = prefixes[i];
+        key_t_   startKey   = decodePlaceholderBit(prefix);
+        unsigned level      = decodePrefixLength(prefix) / 3;
+        unsigned cubeLength = (unsigned)maxCoord >> level;
+        unsigned mask       = ~(cubeLength - 1);
+        unsigned ix, iy, iz;
+        decodeHilbert(startKey, &ix, &iy, &iz);
+        ix &= mask;
+        iy &= mask;
+        iz &= mask;
+        int xmin = (int)ix, xmax = (int)(ix + cubeLength), ymin = (int)iy, ymax = (int)(iy + cubeLength);
+        int zmin = (int)iz, zmax = (int)(iz + cubeLength);
+        centers[3 * i + 0] = b->lim[0] + (xmax + xmin) * hx;
+        centers[3 * i + 1] = b->lim[2] + (ymax + ymin) * hy;
+        centers[3 * i + 2] = b->lim[4] + (zmax + zmin) * hz;
+        sizes[3 * i + 0]   = (xmax - xmin) * hx;
+        sizes[3 * i + 1]   = (ymax - ymin) * hy;
+        sizes[3 * i + 2]   = (zmax - zmin) * hz;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * neighbor search (cstone/findneighbors.hpp:95-188, traversal/traversal.hpp:69-110,
+ * traversal/boxoverlap.hpp:186-216, sph/find_neighbors.hpp:10-44)
+ * ------------------------------------------------------------------------------------------------ */
+
+typedef struct
+{
+    int             numLeafNodes;
+    const key_t_*   prefixes;
+    const int*      childOffsets;
+    const int*      internalToLeaf;
+    const uint32_t* layout;
+    const double*   centers;
+    const double*   sizes;
+    float           searchExtFactor;
+} ns_view;
+
+static inline double rint_pbc(double dx, const ox_box* b, int d)
+{
+    return dx - box_pbc(b, d) * box_l(b, d) * rint(dx * box_il(b, d));
+}
+
+/* norm2(minDistance(...)) with and without PBC (boxoverlap.hpp:197-216); dot = right fold */
+static inline double minDist2(const double* p, const double* c, const double* s, const ox_box* b, int pbc)
+{
+    double d[3];
+    for (int k = 0; k < 3; ++k)
+    {
+        double dx = c[k] - p[k];
+        if (pbc) dx = rint_pbc(dx, b, k);
+        dx = fabs(dx);
+        dx -= s[k];
+        dx += fabs(dx);
+        dx *= 0.5;
+        d[k] = dx;
+    }
+    return d[0] * d[0] + (d[1] * d[1] + d[2] * d[2]);
+}
+
+static unsigned findNeighbors1(uint32_t i, const double* x, const double* y, const double* z, const float* h,
+                               const ns_view* t, const ox_box* b, unsigned ngmax, uint32_t* neighbors)
+{
+    double xi = x[i], yi = y[i], zi = z[i];
+    float  hi = h[i];
+
+    float  radiusSq     = 4.0f * hi * hi;
+    float  cellRadiusSq = radiusSq * t->searchExtFactor * t->searchExtFactor;
+    double particle[3]  = {xi, yi, zi};
+    unsigned numNeighbors = 0;
+
+    int anyPbc = box_pbc(b, 0) || box_pbc(b, 1) || box_pbc(b, 2);
+    /* insideBox(particle, {2h,2h,2h}, box) */
+    double tw     = 2.0 * (double)hi;
+    int    inside = (xi - tw >= b->lim[0]) && (yi - tw >= b->lim[2]) && (zi - tw >= b->lim[4]) &&
+                 (xi + tw <= b->lim[1]) && (yi + tw <= b->lim[3]) && (zi + tw <= b->lim[5]);
+    int usePbc = anyPbc && !inside;
+
+#define OVERLAPS(idx) (minDist2(particle, t->centers + 3 * (idx), t->sizes + 3 * (idx), b, usePbc) < cellRadiusSq)
+#define SEARCH_BOX(idx)                                                                                                \
+    do {                                                                                                               \
+        int      leafIdx = t->internalToLeaf[idx];                                                                     \
+        uint32_t first = t->layout[leafIdx], last = t->layout[leafIdx + 1];                                            \
+        for (uint32_t j = first; j < last; ++j)                                                                        \
+        {                                                                                                              \
+            if (j == i) continue;                                                                                      \
+            double dx = x[j] - particle[0], dy = y[j] - particle[1], dz = z[j] - particle[2];                          \
+            if (usePbc)                                                                                                \
+            {                                                                                                          \
+                dx = rint_pbc(dx, b, 0);                                                                               \
+                dy = rint_pbc(dy, b, 1);                                                                               \
+                dz = rint_pbc(dz, b, 2);                                                                               \
+            }                                                                                                          \
+            if (dx * dx + dy * dy + dz * dz < radiusSq)                                                                \
+            {                                                                                                          \
+                if (numNeighbors < ngmax) neighbors[numNeighbors] = j;                                                 \
+                numNeighbors++;                                                                                        \
+            }                                                                                                          \
+        }                                                                                                              \
+    } while (0)
+
+    /* singleTraversal (traversal.hpp:69-110) */
+    if (!OVERLAPS(0)) return numNeighbors;
+    if (t->childOffsets[0] == 0)
+    {
+        SEARCH_BOX(0);
+        return numNeighbors;
+    }
+    int stack[128];
+    stack[0]     = 0;
+    int stackPos = 1;
+    int node     = 0;
+    do
+    {
+        for (int octant = 0; octant < 8; ++octant)
+        {
+            int child = t->childOffsets[node] + octant;
+            if (OVERLAPS(child))
+            {
+                if (t->childOffsets[child] == 0) { SEARCH_BOX(child); }
+                else { stack[stackPos++] = child; }
+            }
+        }
+        node = stack[--stackPos];
+    } while (node != 0);
+#undef OVERLAPS
+#undef SEARCH_BOX
+    return numNeighbors;
+}
+
+/* Tree for an already sorted key array (same construction as the reference harness). */
+typedef struct
+{
+    key_t_*   leaves;
+    unsigned* counts;
+    key_t_*   prefixes;
+    int *     childOffsets, *parents, *levelRange, *internalToLeaf, *leafToInternal;
+    double *  centers, *sizes;
+    uint32_t* layout;
+    int       nLeaf, nTot;
+} ox_tree;
+
+static void tree_build(ox_tree* t, const uint64_t* keys, size_t n, unsigned bucket, const ox_box* b)
+{
+    int nLeaf        = ox_compute_octree(keys, n, bucket, NULL, NULL, 0);
+    t->nLeaf         = nLeaf;
+    t->leaves        = (key_t_*)malloc(sizeof(key_t_) * (nLeaf + 1));
+    t->counts        = (unsigned*)malloc(sizeof(unsigned) * nLeaf);
+    ox_compute_octree(keys, n, bucket, t->leaves, t->counts, nLeaf);
+    int nInt          = (nLeaf - 1) / 7;
+    int nTot          = nLeaf + nInt;
+    t->nTot           = nTot;
+    t->prefixes       = (key_t_*)malloc(sizeof(key_t_) * nTot);
+    t->childOffsets   = (int*)calloc(nTot + 1, sizeof(int));
+    t->parents        = (int*)calloc((nTot - 1) / 8 > 1 ? (nTot - 1) / 8 : 1, sizeof(int));
+    t->levelRange     = (int*)calloc(MAXLEVEL + 2, sizeof(int));
+    t->internalToLeaf = (int*)calloc(nTot, sizeof(int));
+    t->leafToInternal = (int*)calloc(nTot, sizeof(int));
+    ox_build_octree(t->leaves, nLeaf, t->prefixes, t->childOffsets, t->parents, t->levelRange, t->internalToLeaf,
+                    t->leafToInternal);
+    t->centers = (double*)malloc(sizeof(double) * 3 * nTot);
+    t->sizes   = (double*)malloc(sizeof(double) * 3 * nTot);
+    ox_node_centers(t->prefixes, nTot, b, t->centers, t->sizes);
+    t->layout    = (uint32_t*)malloc(sizeof(uint32_t) * (nLeaf + 1));
+    uint32_t acc = 0;
+    for (int i = 0; i < nLeaf; ++i)
+    {
+        t->layout[i] = acc;
+        acc += t->counts[i];
+    }
+    t->layout[nLeaf] = acc;
+}
+
+static void tree_free(ox_tree* t)
+{
+    free(t->leaves);
+    free(t->counts);
+    free(t->prefixes);
+    free(t->childOffsets);
+    free(t->parents);
+    free(t->levelRange);
+    free(t->internalToLeaf);
+    free(t->leafToInternal);
+    free(t->centers);
+    free(t->sizes);
+    free(t->layout);
+}
+
+static ns_view tree_view(const ox_tree* t)
+{
+    ns_view v = {t->nLeaf, t->prefixes, t->childOffsets, t->internalToLeaf, t->layout, t->centers, t->sizes, 1.0f};
+    return v;
+}
+
+/* findNeighborsSph (sph/find_neighbors.hpp:10-44): nc includes self; returns the number of failures */
+static size_t findNeighborsSph(const double* x, const double* y, const double* z, float* h, uint32_t firstId,
+                               uint32_t lastId, const ox_box* b, const ns_view* t, unsigned ng0, unsigned ngmax,
+                               uint32_t* neighbors, uint32_t* nc)
+{
+    uint32_t numWork  = lastId - firstId;
+    unsigned ngmin    = ng0 / 4;
+    size_t   numFails = 0;
+#pragma omp parallel for reduction(+ : numFails)
+    for (uint32_t i = 0; i < numWork; ++i)
+    {
+        uint32_t id    = i + firstId;
+        unsigned ncSph = 1 + findNeighbors1(id, x, y, z, h, t, b, ngmax, neighbors + (size_t)i * ngmax);
+        int      iteration = 0;
+        while ((ngmin > ncSph || (ncSph - 1) > ngmax) && iteration++ < 10)
+        {
+            h[id] = ox_update_h(ng0, ncSph, h[id]);
+            ncSph = 1 + findNeighbors1(id, x, y, z, h, t, b, ngmax, neighbors + (size_t)i * ngmax);
+        }
+        numFails += (iteration >= 10);
+        nc[i] = ncSph;
+    }
+    return numFails;
+}
+
+void ox_find_neighbors(const double* x, const double* y, const double* z, float* h, const uint64_t* keys, size_t n,
+                       unsigned first, unsigned last, const ox_box* b, unsigned bucket, unsigned ng0, unsigned ngmax,
+                       int iterate_h, uint32_t* neighbors, uint32_t* nc)
+{
+    ox_tree t;
+    tree_build(&t, keys, n, bucket, b);
+    ns_view v = tree_view(&t);
+    if (iterate_h) { findNeighborsSph(x, y, z, h, first, last, b, &v, ng0, ngmax, neighbors, nc); }
+    else
+    {
+        uint32_t numWork = last - first;
+#pragma omp parallel for
+        for (uint32_t i = 0; i < numWork; ++i)
+            nc[i] = findNeighbors1(i + first, x, y, z, h, &v, b, ngmax, neighbors + (size_t)i * ngmax);
+    }
+    tree_free(&t);
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * VE kernels (sph/hydro_ve/<kernel>_kern.hpp), driven like the compute*Impl loops
+ * ------------------------------------------------------------------------------------------------ */
+
+static float g_wh[KTABLE], g_whd[KTABLE];
+static double g_K;
+static int    g_tables = 0;
+
+static void ensure_tables(void)
+{
+    if (!g_tables)
+    {
+#pragma omp critical(ox_tables)
+        {
+            if (!g_tables)
+            {
+                ox_kernel_tables(g_wh, g_whd, &g_K);
+                g_tables = 1;
+            }
+        }
+    }
+}
+
+static inline unsigned nc_capped(const uint32_t* nc, size_t i, unsigned ngmax)
+{
+    unsigned v = nc[i] - 1;
+    return v < ngmax ? v : ngmax;
+}
+
+/* xmassJLoop (xmass_kern.hpp:50-79) */
+static float xmassJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, const ox_state* s)
+{
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  hi = s->h[i], mi = s->m[i];
+    float  hInv  = (float)(1.0 / hi);
+    float  h3Inv = hInv * hInv * hInv;
+    float  rho0i = mi;
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j    = nb[pj];
+        float    dist = distancePBC(b, hi, xi, yi, zi, s->x[j], s->y[j], s->z[j]);
+        float    vloc = dist * hInv;
+        float    w    = lookup(g_wh, vloc);
+        rho0i += w * s->m[j];
+    }
+    /* veDefinition deduces T = double from (rho0i * K * h3Inv) */
+    return (float)((double)mi / ((double)rho0i * K * (double)h3Inv));
+}
+
+void ox_xmass(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+              unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; i++)
+    {
+        size_t ni = i - first;
+        s->xm[i]  = xmassJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s);
+    }
+}
+
+/* veDefGradhJLoop (ve_def_gradh_kern.hpp:43-90) */
+static void veDefGradhJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt,
+                            const ox_state* s, float* kxo, float* gradho)
+{
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  hi = s->h[i], mi = s->m[i], xmassi = s->xm[i];
+    float  hInv     = 1.0f / hi;
+    float  h3Inv    = hInv * hInv * hInv;
+    float  kxi      = xmassi;
+    float  whomegai = -3.0f * xmassi;
+    float  wrho0i   = -3.0f * mi;
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j      = nb[pj];
+        float    dist   = distancePBC(b, hi, xi, yi, zi, s->x[j], s->y[j], s->z[j]);
+        float    vloc   = dist * hInv;
+        float    w      = lookup(g_wh, vloc);
+        float    dw     = lookup(g_whd, vloc);
+        float    dterh  = -(3.0f * w + vloc * dw);
+        float    xmassj = s->xm[j];
+        kxi += w * xmassj;
+        whomegai += dterh * xmassj;
+        wrho0i += dterh * s->m[j];
+    }
+    kxi      = (float)((double)kxi * (K * (double)h3Inv));
+    whomegai = (float)((double)whomegai * (K * (double)h3Inv * (double)hInv));
+    wrho0i   = (float)((double)wrho0i * (K * (double)h3Inv * (double)hInv));
+    whomegai = (float)((double)(whomegai * mi / xmassi) +
+                       ((double)kxi - K * (double)xmassi * (double)h3Inv) * (double)wrho0i);
+    float rhoi   = kxi * mi / xmassi;
+    float dhdrho = -hi / (rhoi * 3.0f);
+    *kxo         = kxi;
+    *gradho      = 1.0f - dhdrho * whomegai;
+}
+
+void ox_ve_def_gradh(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                     unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; i++)
+    {
+        size_t ni = i - first;
+        veDefGradhJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s, &s->kx[i],
+                        &s->gradh[i]);
+    }
+}
+
+/* computeEOS_Impl (hydro_ve/eos.hpp:52-77) with idealGasEOS/idealGasCv (sph/eos.hpp:13-40) */
+static float ideal_gas_cv_f(float mui, double gamma)
+{
+    const float R = 8.317e7f;
+    return (float)((double)(R / mui) / (gamma - 1.0f));
+}
+
+void ox_eos(ox_state* s, const ox_params* p, unsigned first, unsigned last)
+{
+#pragma omp parallel for schedule(static)
+    for (size_t i = first; i < last; ++i)
+    {
+        float  rho = s->kx[i] * s->m[i] / s->xm[i];
+        double tmp = (double)ideal_gas_cv_f(p->muiConst, p->gamma) * s->temp[i] * (p->gamma - 1.0);
+        double pi  = (double)rho * tmp;
+        double ci  = sqrt(tmp);
+        s->prho[i] = (float)(pi / (double)(s->kx[i] * s->m[i] * s->m[i] * s->gradh[i]));
+        s->c[i]    = (float)ci;
+    }
+}
+
+/* IADJLoop (iad_kern.hpp:43-109) */
+static void IADJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s)
+{
+    float  tau11 = 0, tau12 = 0, tau13 = 0, tau22 = 0, tau23 = 0, tau33 = 0;
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  hi    = s->h[i];
+    float  hiInv = 1.0f / hi;
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j  = nb[pj];
+        float    rx = (float)(xi - s->x[j]);
+        float    ry = (float)(yi - s->y[j]);
+        float    rz = (float)(zi - s->z[j]);
+        applyPBC(b, 2.0f * hi, &rx, &ry, &rz);
+        float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
+        float vloc   = dist * hiInv;
+        float w      = lookup(g_wh, vloc);
+        float volj_w = s->xm[j] / s->kx[j] * w;
+        tau11 += rx * rx * volj_w;
+        tau12 += rx * ry * volj_w;
+        tau13 += rx * rz * volj_w;
+        tau22 += ry * ry * volj_w;
+        tau23 += ry * rz * volj_w;
+        tau33 += rz * rz * volj_w;
+    }
+#define GETEXP(v) ((v) == 0.0f ? 0 : ilogbf(v))
+    int tauExpSum = GETEXP(tau11) + GETEXP(tau12) + GETEXP(tau13) + GETEXP(tau22) + GETEXP(tau23) + GETEXP(tau33);
+#undef GETEXP
+    float normalization = ldexpf(1.0f, -tauExpSum / 6);
+    tau11 *= normalization;
+    tau12 *= normalization;
+    tau13 *= normalization;
+    tau22 *= normalization;
+    tau23 *= normalization;
+    tau33 *= normalization;
+    float det = tau11 * tau22 * tau33 + 2.0f * tau12 * tau23 * tau13 - tau11 * tau23 * tau23 -
+                tau22 * tau13 * tau13 - tau33 * tau12 * tau12;
+    float factor = (float)((double)(normalization * (hi * hi * hi)) / ((double)det * K));
+    s->c11[i]    = (tau22 * tau33 - tau23 * tau23) * factor;
+    s->c12[i]    = (tau13 * tau23 - tau33 * tau12) * factor;
+    s->c13[i]    = (tau12 * tau23 - tau22 * tau13) * factor;
+    s->c22[i]    = (tau11 * tau33 - tau13 * tau13) * factor;
+    s->c23[i]    = (tau13 * tau12 - tau11 * tau23) * factor;
+    s->c33[i]    = (tau11 * tau22 - tau12 * tau12) * factor;
+}
+
+/* divV_curlVJLoop (divv_curlv_kern.hpp:43-123), doGradV = false, curlv stored */
+static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s)
+{
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
+    float  hi = s->h[i], kxi = s->kx[i];
+    float  hiInv  = 1.0f / hi;
+    float  hiInv3 = hiInv * hiInv * hiInv;
+    float  dVx[3] = {0, 0, 0}, dVy[3] = {0, 0, 0}, dVz[3] = {0, 0, 0};
+    float  c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i],
+          c33i = s->c33[i];
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j  = nb[pj];
+        float    rx = (float)(xi - s->x[j]);
+        float    ry = (float)(yi - s->y[j]);
+        float    rz = (float)(zi - s->z[j]);
+        applyPBC(b, 2.0f * hi, &rx, &ry, &rz);
+        float r2    = rx * rx + ry * ry + rz * rz;
+        float dist  = sqrtf(r2);
+        float vx_ji = s->vx[j] - vxi;
+        float vy_ji = s->vy[j] - vyi;
+        float vz_ji = s->vz[j] - vzi;
+        float v1    = dist * hiInv;
+        float Wi    = lookup(g_wh, v1);
+        float tA[3];
+        tA[0]        = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
+        tA[1]        = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
+        tA[2]        = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
+        float xmassj = s->xm[j];
+        float fx = vx_ji * xmassj, fy = vy_ji * xmassj, fz = vz_ji * xmassj;
+        for (int k = 0; k < 3; ++k)
+        {
+            dVx[k] = dVx[k] + tA[k] * fx;
+            dVy[k] = dVy[k] + tA[k] * fy;
+            dVz[k] = dVz[k] + tA[k] * fz;
+        }
+    }
+    float norm_kxi = (float)(K * (double)hiInv3 / (double)kxi);
+    s->divv[i]     = norm_kxi * (dVx[0] + dVy[1] + dVz[2]);
+    if (s->curlv)
+    {
+        float cv0 = dVz[1] - dVy[2], cv1 = dVx[2] - dVz[0], cv2 = dVy[0] - dVx[1];
+        s->curlv[i] = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
+    }
+}
+
+void ox_iad_divv_curlv(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                       unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; ++i)
+    {
+        size_t   ni  = i - first;
+        unsigned cnt = nc_capped(s->nc, i, p->ngmax);
+        IADJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s);
+        divVcurlVJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s);
+    }
+}
+
+/* AVswitchesJLoop (av_switches_kern.hpp:43-137) */
+static float AVswitchesJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt,
+                             const ox_state* s, double dt, float alphamin, float alphamax, float decay_constant,
+                             float alpha_i)
+{
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
+    float  hi = s->h[i], ci = s->c[i];
+    float  c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i],
+          c33i = s->c33[i];
+    float vijsignal_i = 1.e-40f * ci;
+    float hiInv       = 1.0f / hi;
+    float hiInv3      = hiInv * hiInv * hiInv;
+    float divv_i      = s->divv[i];
+    float gx = 0, gy = 0, gz = 0;
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j  = nb[pj];
+        float    rx = (float)(xi - s->x[j]);
+        float    ry = (float)(yi - s->y[j]);
+        float    rz = (float)(zi - s->z[j]);
+        applyPBC(b, 2.0f * hi, &rx, &ry, &rz);
+        float r2           = rx * rx + ry * ry + rz * rz;
+        float dist         = sqrtf(r2);
+        float vx_ij        = vxi - s->vx[j];
+        float vy_ij        = vyi - s->vy[j];
+        float vz_ij        = vzi - s->vz[j];
+        float rv           = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+        float vijsignal_ij = 0.0f;
+        if (rv < 0.0f) { vijsignal_ij = ci + s->c[j] - 3.0f * rv / dist; }
+        if (vijsignal_i < vijsignal_ij) vijsignal_i = vijsignal_ij; /* stl::max */
+        float v1     = dist * hiInv;
+        float Wi     = (float)(K * (double)hiInv3 * (double)lookup(g_wh, v1));
+        float termA1 = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
+        float termA2 = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
+        float termA3 = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
+        float volj   = s->xm[j] / s->kx[j];
+        float factor = volj * (divv_i - s->divv[j]);
+        gx += factor * termA1;
+        gy += factor * termA2;
+        gz += factor * termA3;
+    }
+    float graddivv = sqrtf(gx * gx + gy * gy + gz * gz);
+    float alphaloc = 0.0f;
+    if (divv_i < 0.0f)
+    {
+        float a_const = hi * hi * graddivv;
+        alphaloc      = alphamax * a_const / (a_const + hi * fabsf(divv_i) + 0.05f * ci);
+    }
+    if (alphaloc >= alpha_i) { alpha_i = alphaloc; }
+    else
+    {
+        float decay    = hi / (decay_constant * vijsignal_i);
+        float alphadot = 0.0f;
+        if (alphaloc >= alphamin) { alphadot = (alphaloc - alpha_i) / decay; }
+        else { alphadot = (alphamin - alpha_i) / decay; }
+        alpha_i = (float)((double)alpha_i + (double)alphadot * dt);
+    }
+    return alpha_i;
+}
+
+void ox_av_switches(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                    unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; ++i)
+    {
+        size_t ni   = i - first;
+        s->alpha[i] = AVswitchesJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax),
+                                      s, s->minDt, p->alphamin, p->alphamax, p->decay_constant, s->alpha[i]);
+    }
+}
+
+/* momentumAndEnergyJLoop<avClean=false> (momentum_energy_kern.hpp:65-222), tdpdTrho == nullptr.
+ * The Atwood ramp calls unqualified `pow(float, float)` inside namespace sph (momentum_energy_kern.hpp:192-193);
+ * with libstdc++ that resolves to ::pow(double, double) from <math.h>, so each product is formed in double and
+ * rounded once to float -- verified bit-for-bit against oracle/_ref on the Noh IC, where powf() differs. */
+static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
+                          float Atmin, float Atmax, float ramp, float* maxvsignal)
+{
+    double xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float  vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
+    float  hi = s->h[i], mi = s->m[i], ci = s->c[i], kxi = s->kx[i];
+    float  alpha_i = s->alpha[i];
+    float  xmassi  = s->xm[i];
+    float  rhoi    = kxi * mi / xmassi;
+    float  prhoi   = s->prho[i];
+    float  hiInv   = 1.0f / hi;
+    float  hiInv3  = hiInv * hiInv * hiInv;
+    float  maxvsignali = 0.0f;
+    float  mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
+    float  c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i],
+          c33i = s->c33[i];
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j   = nb[pj];
+        float    rx  = (float)(xi - s->x[j]);
+        float    ry  = (float)(yi - s->y[j]);
+        float    rz  = (float)(zi - s->z[j]);
+        float    vxj = s->vx[j], vyj = s->vy[j], vzj = s->vz[j];
+        applyPBC(b, 2.0f * hi, &rx, &ry, &rz);
+        float r2     = rx * rx + ry * ry + rz * rz;
+        float dist   = sqrtf(r2);
+        float vx_ij  = vxi - vxj;
+        float vy_ij  = vyi - vyj;
+        float vz_ij  = vzi - vzj;
+        float hj     = s->h[j];
+        float hjInv  = 1.0f / hj;
+        float v1     = dist * hiInv;
+        float v2     = dist * hjInv;
+        float hjInv3 = hjInv * hjInv * hjInv;
+        float Wi     = hiInv3 * lookup(g_wh, v1);
+        float Wj     = hjInv3 * lookup(g_wh, v2);
+        float tA1i   = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
+        float tA2i   = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
+        float tA3i   = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
+        float c11j = s->c11[j], c12j = s->c12[j], c13j = s->c13[j], c22j = s->c22[j], c23j = s->c23[j],
+              c33j = s->c33[j];
+        float tA1j   = -(c11j * rx + c12j * ry + c13j * rz) * Wj;
+        float tA2j   = -(c12j * rx + c22j * ry + c23j * rz) * Wj;
+        float tA3j   = -(c13j * rx + c23j * ry + c33j * rz) * Wj;
+        float mj     = s->m[j];
+        float cj     = s->c[j];
+        float kxj    = s->kx[j];
+        float xmassj = s->xm[j];
+        float rhoj   = kxj * mj / xmassj;
+        float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+        float wij    = rv / dist;
+        /* artificial_viscosity<float> (kernels.hpp:70-84): (alpha_i + alpha_j) / 4.0 is a double */
+        float viscosity_ij = 0.0f;
+        if (wij < 0.0f)
+        {
+            float vij_signal =
+                (float)((double)(alpha_i + s->alpha[j]) / 4.0 * (double)(ci + cj) - (double)(2.0f * wij));
+            viscosity_ij = -vij_signal * wij;
+        }
+        float vijsignal = 0.5f * (ci + cj) - 2.0f * wij;
+        maxvsignali     = (vijsignal > maxvsignali) ? vijsignal : maxvsignali;
+        float a_mom, b_mom;
+        float Atwood = fabsf(rhoi - rhoj) / (rhoi + rhoj);
+        if (Atwood < Atmin)
+        {
+            a_mom = xmassi * xmassi;
+            b_mom = xmassj * xmassj;
+        }
+        else if (Atwood > Atmax)
+        {
+            a_mom = xmassi * xmassj;
+            b_mom = a_mom;
+        }
+        else
+        {
+            float sigma_ij = ramp * (Atwood - Atmin);
+            a_mom          = (float)(pow(xmassi, 2.0f - sigma_ij) * pow(xmassj, sigma_ij));
+            b_mom          = (float)(pow(xmassj, 2.0f - sigma_ij) * pow(xmassi, sigma_ij));
+        }
+        float a_visc   = mj / rhoi * viscosity_ij;
+        float b_visc   = mj / rhoj * viscosity_ij;
+        float a_visc_x = 0.5f * (a_visc * tA1i + b_visc * tA1j);
+        float a_visc_y = 0.5f * (a_visc * tA2i + b_visc * tA2j);
+        float a_visc_z = 0.5f * (a_visc * tA3i + b_visc * tA3j);
+        a_visc_energy += a_visc_x * vx_ij + a_visc_y * vy_ij + a_visc_z * vz_ij;
+        energy += mj * a_mom * (vx_ij * tA1i + vy_ij * tA2i + vz_ij * tA3i);
+        float momentum_i = mj * prhoi * a_mom;
+        float momentum_j = mj * s->prho[j] * b_mom;
+        mx += momentum_i * tA1i + momentum_j * tA1j + a_visc_x;
+        my += momentum_i * tA2i + momentum_j * tA2j + a_visc_y;
+        mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
+    }
+    if (a_visc_energy < 0.0f) a_visc_energy = 0.0f; /* stl::max(T(0), x) */
+    float eCoeff = prhoi;
+    s->du[i]     = K * (double)(eCoeff * energy + 0.5f * a_visc_energy);
+    s->ax[i]     = (float)(-K * (double)mx);
+    s->ay[i]     = (float)(-K * (double)my);
+    s->az[i]     = (float)(-K * (double)mz);
+    *maxvsignal  = maxvsignali;
+}
+
+/* tsKCourant<float> (kernels.hpp:12-18); Kcour is a float parameter */
+static inline float tsKCourant(float maxvsignal, float h, float c, float Kcour)
+{
+    float v = maxvsignal > 0.0f ? maxvsignal : c;
+    return Kcour * h / v;
+}
+
+double ox_momentum_energy(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors,
+                          unsigned first, unsigned last)
+{
+    ensure_tables();
+    float minDt = INFINITY;
+#pragma omp parallel for schedule(static) reduction(min : minDt)
+    for (size_t i = first; i < last; ++i)
+    {
+        size_t ni         = i - first;
+        float  maxvsignal = 0;
+        momentumJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s, p->Atmin,
+                      p->Atmax, p->ramp, &maxvsignal);
+        float dt_i = tsKCourant(maxvsignal, s->h[i], s->c[i], (float)p->Kcour);
+        minDt      = minDt < dt_i ? minDt : dt_i;
+    }
+    s->minDtCourant = minDt;
+    return minDt;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * integration (sph/positions.hpp:54-139 with the F2 fix, update_h.hpp:12-22, ts_global.hpp:72-112)
+ * ------------------------------------------------------------------------------------------------ */
+
+void ox_positions(ox_state* s, const ox_params* p, const ox_box* b, unsigned first, unsigned last)
+{
+    double dt = s->minDt, dt_m1 = s->minDt_m1;
+    float  constCv = ideal_gas_cv_f(p->muiConst, p->gamma);
+#pragma omp parallel for schedule(static)
+    for (size_t i = first; i < last; i++)
+    {
+        /* positionUpdate<double> (:77-88); fixed-boundary branch (:99-108) applies to bnd == 2 only */
+        int skip = 0;
+        if ((b->bnd[0] == 2 || b->bnd[1] == 2 || b->bnd[2] == 2) && s->vx[i] == 0.0f && s->vy[i] == 0.0f &&
+            s->vz[i] == 0.0f)
+        {
+            double X[3] = {s->x[i], s->y[i], s->z[i]};
+            for (int d = 0; d < 3; ++d)
+            {
+                double top = b->lim[2 * d + 1], bot = b->lim[2 * d];
+                if (b->bnd[d] == 2 &&
+                    (fabs(top - X[d]) < 2.0f * s->h[i] || fabs(bot - X[d]) < 2.0f * s->h[i]))
+                    skip = 1;
+            }
+        }
+        if (!skip)
+        {
+            double A[3]  = {s->ax[i], s->ay[i], s->az[i]};
+            double X[3]  = {s->x[i], s->y[i], s->z[i]};
+            double dX[3] = {s->x_m1[i], s->y_m1[i], s->z_m1[i]};
+            double Xn[3], Vn1[3], dXn1[3];
+            double inv = 1.0 / dt_m1, hdm1 = 0.5 * dt_m1, adt = fabs(dt);
+            for (int k = 0; k < 3; ++k)
+            {
+                double Vnmhalf = dX[k] * inv;
+                double Vn      = Vnmhalf + A[k] * hdm1;
+                Vn1[k]         = Vn + A[k] * dt;
+                dXn1[k]        = (Vn + (A[k] * 0.5) * adt) * dt;
+                Xn[k]          = X[k] + dXn1[k];
+            }
+            /* putInBox (box.hpp:209-230) */
+            for (int d = 0; d < 3; ++d)
+            {
+                int pbc = box_pbc(b, d);
+                if (pbc && Xn[d] > b->lim[2 * d + 1]) Xn[d] -= box_l(b, d);
+                else if (pbc && Xn[d] < b->lim[2 * d]) Xn[d] += box_l(b, d);
+            }
+            s->x[i]    = Xn[0];
+            s->y[i]    = Xn[1];
+            s->z[i]    = Xn[2];
+            s->x_m1[i] = (float)dXn1[0];
+            s->y_m1[i] = (float)dXn1[1];
+            s->z_m1[i] = (float)dXn1[2];
+            s->vx[i]   = (float)Vn1[0];
+            s->vy[i]   = (float)Vn1[1];
+            s->vz[i]   = (float)Vn1[2];
+        }
+        /* updateTempHost with energyUpdate<double,double> (:54-61, :121-139), F2 fixed */
+        double u_old = (double)constCv * s->temp[i];
+        double du = s->du[i], du_m1 = (double)s->du_m1[i];
+        double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;
+        if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
+        s->temp[i]  = u_new / (double)constCv;
+        s->du_m1[i] = (float)s->du[i];
+    }
+}
+
+void ox_update_h_range(ox_state* s, unsigned ng0, unsigned first, unsigned last)
+{
+#pragma omp parallel for schedule(static)
+    for (size_t i = first; i < last; i++)
+        s->h[i] = ox_update_h(ng0, s->nc[i], s->h[i]);
+}
+
+typedef struct
+{
+    uint64_t key;
+    uint64_t idx;
+} kv_pair;
+
+static int cmp_kv(const void* a, const void* b)
+{
+    uint64_t x = ((const kv_pair*)a)->key, y = ((const kv_pair*)b)->key;
+    if (x != y) return (x > y) - (x < y);
+    uint64_t i = ((const kv_pair*)a)->idx, j = ((const kv_pair*)b)->idx;
+    return (i > j) - (i < j);
+}
+
+#define PERMUTE(field, type)                                                                                           \
+    do {                                                                                                               \
+        type* tmp_ = (type*)scratch;                                                                                   \
+        _Pragma("omp parallel for schedule(static)") for (size_t i = 0; i < n; ++i) tmp_[i] = s->field[ord[i].idx];   \
+        memcpy(s->field, tmp_, n * sizeof(type));                                                                      \
+    } while (0)
+
+/* One VE step, single rank: sync (keys, sort, reorder, tree) + computeForces + integrate
+ * (ve_hydro.hpp:132-218). Returns the number of h-nc convergence failures. */
+int ox_step(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket)
+{
+    ensure_tables();
+    size_t n = s->n;
+    ox_sfc_keys(s->x, s->y, s->z, n, b, s->keys);
+    kv_pair* ord = (kv_pair*)malloc(sizeof(kv_pair) * n);
+    for (size_t i = 0; i < n; ++i)
+    {
+        ord[i].key = s->keys[i];
+        ord[i].idx = i;
+    }
+    qsort(ord, n, sizeof(kv_pair), cmp_kv);
+    void* scratch = malloc(n * sizeof(double));
+    for (size_t i = 0; i < n; ++i)
+        s->keys[i] = ord[i].key;
+    PERMUTE(x, double);
+    PERMUTE(y, double);
+    PERMUTE(z, double);
+    PERMUTE(h, float);
+    PERMUTE(m, float);
+    PERMUTE(temp, double);
+    PERMUTE(vx, float);
+    PERMUTE(vy, float);
+    PERMUTE(vz, float);
+    PERMUTE(x_m1, float);
+    PERMUTE(y_m1, float);
+    PERMUTE(z_m1, float);
+    PERMUTE(du_m1, float);
+    PERMUTE(alpha, float);
+    PERMUTE(id, uint64_t);
+    free(scratch);
+    free(ord);
+
+    ox_tree t;
+    tree_build(&t, s->keys, n, bucket, b);
+    ns_view   v   = tree_view(&t);
+    uint32_t* nbr = (uint32_t*)malloc(sizeof(uint32_t) * n * p->ngmax);
+
+    size_t fails = findNeighborsSph(s->x, s->y, s->z, s->h, 0, (uint32_t)n, b, &v, p->ng0, p->ngmax, nbr, s->nc);
+    ox_xmass(s, p, b, nbr, 0, (unsigned)n);
+    ox_ve_def_gradh(s, p, b, nbr, 0, (unsigned)n);
+    ox_eos(s, p, 0, (unsigned)n);
+    ox_iad_divv_curlv(s, p, b, nbr, 0, (unsigned)n);
+    float maxDivv = -INFINITY;
+#pragma omp parallel for reduction(max : maxDivv)
+    for (size_t i = 0; i < n; ++i)
+        maxDivv = s->divv[i] > maxDivv ? s->divv[i] : maxDivv;
+    s->minDtRho = p->Krho / fabs((double)maxDivv);
+    ox_av_switches(s, p, b, nbr, 0, (unsigned)n);
+    ox_momentum_energy(s, p, b, nbr, 0, (unsigned)n);
+
+    double minDtLoc = INFINITY;
+    double cand[3]  = {s->minDtCourant, s->minDtRho, p->maxDtIncrease * s->minDt};
+    for (int k = 0; k < 3; ++k)
+        minDtLoc = cand[k] < minDtLoc ? cand[k] : minDtLoc;
+    s->ttot += minDtLoc;
+    s->minDt_m1 = s->minDt;
+    s->minDt    = minDtLoc;
+    ox_positions(s, p, b, 0, (unsigned)n);
+    ox_update_h_range(s, p->ng0, 0, (unsigned)n);
+
+    free(nbr);
+    tree_free(&t);
+    return (int)fails;
+}
