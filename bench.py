@@ -1,0 +1,162 @@
+"""Benchmark: particle-updates/s of the VE time step (Sedov lattice) on N MI355X, one process per GPU.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--side S] [--no-cpu-baseline]
+
+A step is one full HydroVeProp step (ve_hydro.hpp:132-218): sync (keys, sort, reorder, tree), neighbor search with
+h iteration, XMass, VeDefGradh, EOS, IAD+divv/curlv, AV switches, momentum/energy, time-step, positions, h update.
+Inputs are generated and kept in HBM; nothing leaves the device inside the timed region except the per-step
+4-byte tree-level counts and stats.  Weak scaling: side = round(200 * N^(1/3)) particles^(1/3) in total
+(N=1: Sedov -n 200 = BASELINE config 2; N=8: Sedov -n 400 = config 4).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sph-exa_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MOM_OWN_BYTES = 108    # momentum kernel own record R+W
+MOM_EDGE_BYTES = 4 + 88  # index + neighbor record per edge
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--side", type=int, default=0, help="total lattice side (default weak scaling from 200)")
+    ap.add_argument("--bucket", type=int, default=64)
+    ap.add_argument("--exact", action="store_true", help="use the no-FMA (bit-reproducible) kernels")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Reference CPU path (oracle/_ref, OpenMP) timed on this host on a bounded Sedov sample."""
+    import pyoracle as po
+
+    kind = "reference"
+    path = os.path.join(ROOT, "oracle", "_ref", "libsphexa_ref_fast.so")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "oracle", "_ref", "libsphexa_ref.so")
+    if not os.path.exists(path):
+        path, kind = po.ORACLE_SO, "port"
+    lib = po.Lib(path)
+    side = 50
+    st, box = po.sedov_state(side)
+    lib.step(st, box)  # warm-up (first touch, thread pool)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        lib.step(st, box)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 50:
+            break
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": st.n * steps / el, "unit": "particle-updates/s", "cores": cores, "kind": kind,
+            "sample": f"Sedov lattice -n {side} ({st.n} particles), {steps} VE steps after 1 warm-up, "
+                      f"{os.path.basename(path)}, OMP threads={cores}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(args.gpus, world)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (gloo): rendezvous, barrier, max-reduce of timings
+
+        dist.init_process_group("gloo")
+
+    import numpy as np
+
+    import sphexa_amd as sx
+
+    side = args.side or int(round(200 * n_gpus ** (1.0 / 3.0)))
+    ctx = sx.Context(local, exact=args.exact)
+    box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
+    # interim multi-GPU: each rank runs the side^3/N share as an independent periodic replica
+    rank_side = side if world == 1 else int(round(side / world ** (1.0 / 3.0)))
+    n_local = rank_side ** 3
+    sim = sx.Sim(ctx, n_local, box, bucket=args.bucket)
+    sim.init_sedov(rank_side)
+
+    for _ in range(args.warmup):
+        sim.step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ctx.sync()
+    barrier()
+    stage_sum = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.step()
+        for k, v in sim.stage_times().items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+    ctx.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    stats = sim.stats()
+    n_total = n_local * world
+    ms_step = el / args.steps * 1e3
+    ng = stats["sumNeighbors"] / max(1, n_local)
+    mom_ms = stage_sum.get("MomentumEnergy", float("nan")) / args.steps
+    mom_bytes = n_local * (MOM_OWN_BYTES + ng * MOM_EDGE_BYTES)
+    achieved = mom_bytes / (mom_ms * 1e-3) / 1e9
+    sc = sim.scalars()
+    out = {
+        "metric": "particle-updates/sec (whole node), Sedov -n 400, 1/2/4/8 MI355X + HBM roofline %",
+        "value": n_total * args.steps / el,
+        "unit": "particle-updates/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 hydro / f64 coordinates (sph::SphTypes)",
+        "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint",
+        "config": {"workload": f"Sedov -n {side} ({side ** 3} particles), VE propagator, {args.steps} steps",
+                   "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
+                   "parallelism": "1 GPU" if world == 1 else f"{world} independent replicas (interim)",
+                   "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
+        "roofline": {"bound": "hbm", "kernel": "momentumEnergyKernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": mom_bytes, "avg_launch_ms": mom_ms,
+                     "model": f"edge model: {MOM_OWN_BYTES} B own + {ng:.1f} neighbors x {MOM_EDGE_BYTES} B"},
+        "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
+        "neighbors_per_particle": ng,
+        "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),
+        "minDt": sc["minDt"],
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    sim.close()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

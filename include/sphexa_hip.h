@@ -1,0 +1,253 @@
+/*! @file sphexa_hip.h
+ * @brief C-ABI of libsphexa_hip.so -- the MI355X (gfx950) hot path of SPH-EXA's VE propagator.
+ *
+ * Plain C, POD structs and raw device pointers only.  Each entry point replaces one GPU seam of the
+ * reference (paths relative to the SPH-EXA tree, lks1248/SPH-EXA @ 2024-10-16):
+ *
+ *   sx_sfc_keys            cstone::computeSfcKeysGpu            domain/include/cstone/sfc/sfc_gpu.h, sfc_gpu.cu:47
+ *   sx_sort_keys           cstone::GpuSfcSorter::setMapFromCodes domain/include/cstone/primitives/primitives_gpu.cu:271-283
+ *   sx_gather              cstone::gatherGpu                    primitives/primitives_gpu.cu:86
+ *   sx_compute_octree      cstone::computeOctreeGpu / updateOctreeGpu (converged)  tree/csarray_gpu.cu:100-264
+ *   sx_build_octree        cstone::buildOctreeGpu               tree/octree_gpu.cu:153-170
+ *   sx_node_centers        cstone::computeGeoCentersGpu         focus/source_center_gpu.cu:117-135
+ *   sx_compute_groups      sph::computeSpatialGroups            sph/include/sph/groups.cu:30-47
+ *   sx_find_neighbors      cstone::findNeighbors (+ sph h-nc iteration) findneighbors.hpp:167-188,
+ *                                                               sph/include/sph/find_neighbors.hpp:10-44
+ *   sx_xmass               sph::cuda::computeXMass              sph/include/sph/sph_gpu.hpp:25, hydro_ve/xmass_gpu.cu:103
+ *   sx_ve_def_gradh        sph::cuda::computeVeDefGradh         sph_gpu.hpp:37, hydro_ve/ve_def_gradh_gpu.cu:86
+ *   sx_eos                 sph::cuda::computeEOS (VE)           sph_gpu.hpp:40-43, hydro_ve/eos_gpu.cu:74
+ *   sx_iad_divv_curlv      sph::cuda::computeIadDivvCurlv       sph_gpu.hpp:45, hydro_ve/iad_divv_curlv_gpu.cu:91
+ *   sx_av_switches         sph::cuda::computeAVswitches         sph_gpu.hpp:48, hydro_ve/av_switches_gpu.cu:103
+ *   sx_momentum_energy     sph::cuda::computeMomentumEnergy<avClean=false> sph_gpu.hpp:51-53, momentum_energy_gpu.cu:121
+ *   sx_positions           sph::computePositionsGpu             sph_gpu.hpp:64-72, positions_gpu.cu:167-179
+ *   sx_update_h            sph::updateSmoothingLengthGpu        sph_gpu.hpp:78, update_h_gpu.cu:49-60
+ *   sx_max_divv            cstone::MinMaxGpu (rhoTimestep)      sph/ts_global.hpp:72-94
+ *   sx_sim_*               one HydroVeProp step (sync + computeForces + integrate), main/src/propagator/ve_hydro.hpp:132-218
+ *
+ * Conventions (reference semantics preserved):
+ *  - Field types follow sph::SphTypes (sph/types.hpp:39-46): x,y,z,temp,u,du double; other hydro fields float.
+ *  - Neighbor criterion is the reference CPU one (cstone/findneighbors.hpp:111,133-158):
+ *    |r_ij|^2 (double) < float(4 h_i^2), j != i, periodic folding when the particle is within 2h of the box edge.
+ *  - nc[i] counts neighbors INCLUDING self (sph/find_neighbors.hpp:26); kernels use min(nc-1, ngmax) of them.
+ *  - sx_xmass runs the neighbor search with the coupled h-nc iteration (mutates h, writes nc), exactly like
+ *    sph::cuda::computeXMass.  The neighbor list it builds is cached in the context and reused by the later pair
+ *    kernels of the same step (the reference GPU re-traverses the tree in each kernel; positions and h do not change
+ *    between computeXMass and computeMomentumEnergy in ve_hydro.hpp:132-205).  Call sx_find_neighbors again if x,y,z
+ *    or h change.
+ *  - Every call is asynchronous on the context stream unless it returns a host scalar (sx_momentum_energy,
+ *    sx_max_divv, sx_compute_octree), which synchronises that stream -- like the reference, whose entry points
+ *    synchronise (e.g. xmass_gpu.cu:113).
+ *  - Return value: SX_OK, or an SX_ERR_* code; sx_last_error() has the message.  The reference turns the same
+ *    conditions into std::runtime_error (xmass_gpu.cu:126-127) or exit() (cuda/errorcheck.cuh:30-42).
+ */
+#ifndef SPHEXA_HIP_H
+#define SPHEXA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SX_OK 0
+#define SX_ERR_TRAVERSAL 1   /* neighbor-search candidate buffer exhausted ("GPU traversal stack exhausted") */
+#define SX_ERR_NOT_CONVERGED 2 /* coupled h-nc iteration failed to converge (xmass_gpu.cu:127) */
+#define SX_ERR_HIP 3         /* HIP runtime error */
+#define SX_ERR_ARG 4         /* invalid argument (sizes, missing buffers, no neighbor list) */
+#define SX_ERR_NOMEM 5
+
+/*! cstone::Box<double> (sfc/box.hpp:111-191). bnd[k]: 0 open, 1 periodic, 2 fixed (cstone::BoundaryType). */
+typedef struct sx_box
+{
+    double  lim[6]; /* xmin xmax ymin ymax zmin zmax */
+    int32_t bnd[3];
+} sx_box;
+
+/*! ParticlesData physics members (sph/particles_data.hpp:86-138) used by the VE kernels. */
+typedef struct sx_params
+{
+    double   K;        /* kernel normalisation; sx_kernel_constant() returns the reference value */
+    uint32_t ng0;      /* target neighbor count, 100 */
+    uint32_t ngmax;    /* max stored neighbors, 150 */
+    double   Kcour;    /* 0.2 */
+    double   Krho;     /* 0.06 */
+    double   gamma;    /* 5/3 */
+    float    muiConst; /* 10 */
+    float    alphamin, alphamax, decay_constant; /* 0.05, 1.0, 0.2 */
+    float    Atmin, Atmax, ramp;                 /* 0.1, 0.2, 10 */
+    double   maxDtIncrease;                      /* 1.1 */
+} sx_params;
+
+/*! Device pointers in sphexa::ParticlesData field order (particles_data.hpp:247-251); NULL where unused.
+ *  n = number of particles INCLUDING halos (every array has this length). */
+typedef struct sx_fields
+{
+    size_t    n;
+    double *  x, *y, *z;
+    float *   x_m1, *y_m1, *z_m1;
+    float *   vx, *vy, *vz;
+    float*    rho;
+    double*   u;
+    float *   p, *prho, *tdpdTrho, *h, *m, *c;
+    float *   ax, *ay, *az;
+    double*   du;
+    float*    du_m1;
+    float *   c11, *c12, *c13, *c22, *c23, *c33;
+    float *   mue, *mui;
+    double*   temp;
+    float *   cv, *xm, *kx, *divv, *curlv, *alpha, *gradh;
+    uint64_t* keys;
+    uint32_t* nc;
+    float *   dV11, *dV12, *dV13, *dV22, *dV23, *dV33;
+    float*    markRamp;
+    uint8_t*  rung;
+} sx_fields;
+
+/*! cstone::OctreeNsView<double, uint64_t> (tree/octree.hpp:296-316), device pointers. centers/sizes are
+ *  Vec3<double> arrays (3 doubles per node). */
+typedef struct sx_tree
+{
+    int32_t         numLeafNodes;
+    int32_t         numNodes;
+    const uint64_t* prefixes;
+    const int32_t*  childOffsets;
+    const int32_t*  internalToLeaf;
+    const int32_t*  levelRange;
+    const uint64_t* leaves;
+    const uint32_t* layout; /* leaf -> first particle; numLeafNodes + 1 entries */
+    const double*   centers;
+    const double*   sizes;
+    float           searchExtFactor;
+} sx_tree;
+
+/*! sph::GroupView (cstone/traversal/groups.hpp:19-55). The MI355X path partitions [firstBody, lastBody) into
+ *  fixed 64-particle SFC blocks (one wavefront each); groupStart/groupEnd are accepted for interface parity. */
+typedef struct sx_groups
+{
+    uint32_t        firstBody, lastBody, numGroups;
+    const uint32_t* groupStart;
+    const uint32_t* groupEnd;
+} sx_groups;
+
+/*! Linked octree arrays (cstone::OctreeData, tree/octree.hpp:318-375), device pointers, caller-owned.
+ *  Sizes: numNodes = numLeaves + (numLeaves-1)/7; childOffsets numNodes+1; parents max(1,(numNodes-1)/8);
+ *  levelRange 23; internalToLeaf, leafToInternal numNodes. */
+typedef struct sx_octree
+{
+    uint64_t* prefixes;
+    int32_t*  childOffsets;
+    int32_t*  parents;
+    int32_t*  levelRange;
+    int32_t*  internalToLeaf;
+    int32_t*  leafToInternal;
+} sx_octree;
+
+/*! neighbor-search statistics (cstone::NcStats, traversal/find_neighbors.cuh:346-357) */
+typedef struct sx_nbstats
+{
+    uint64_t sumNeighbors;   /* sum over targets of stored neighbors */
+    uint32_t maxNeighbors;   /* max true count (excluding self) */
+    uint32_t numFailed;      /* h-nc iteration failures */
+    uint64_t sumCandidates;  /* candidate particles tested (per target, summed) */
+} sx_nbstats;
+
+typedef struct sx_ctx sx_ctx;
+
+/* ---- context --------------------------------------------------------------------------------------------- */
+int         sx_create(sx_ctx** ctx, int device);
+void        sx_destroy(sx_ctx* ctx);
+int         sx_set_stream(sx_ctx* ctx, void* hipStream); /* NULL = the context's own stream */
+void*       sx_get_stream(sx_ctx* ctx);
+const char* sx_last_error(sx_ctx* ctx);
+/*! 1: bit-reproducible arithmetic (no FMA contraction; matches the CPU reference bit-for-bit given the same neighbor
+ *  order); 0 (default): FMA-contracted kernels. */
+int    sx_set_exact(sx_ctx* ctx, int exact);
+double sx_kernel_constant(void); /* K of the sinc^6 kernel, particles_data.hpp:366 */
+int    sx_copy_tables(sx_ctx* ctx, float* wh_host, float* whd_host); /* 20000-entry f32 tables */
+int    sx_synchronize(sx_ctx* ctx);
+
+/* ---- device memory plumbing (for hosts without their own allocator, e.g. ctypes bindings) --------------- */
+void* sx_device_alloc(sx_ctx* ctx, size_t bytes);
+int   sx_device_free(sx_ctx* ctx, void* ptr);
+/*! kind: 1 host->device, 2 device->host, 3 device->device; synchronous w.r.t. the context stream */
+int   sx_memcpy(sx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+int   sx_memset(sx_ctx* ctx, void* dst, int value, size_t bytes);
+
+/* ---- cstone: SFC keys, sorting, tree -------------------------------------------------------------------- */
+int sx_sfc_keys(sx_ctx* ctx, const double* x, const double* y, const double* z, uint64_t* keys, size_t n,
+                const sx_box* box);
+/*! sort keys ascending in place (stable) and write the permutation: order[i] = old index of sorted element i */
+int sx_sort_keys(sx_ctx* ctx, uint64_t* keys, uint32_t* order, size_t n);
+/*! dst[i] = src[order[i]] for elements of elemBytes (1,2,4,8,16) */
+int sx_gather(sx_ctx* ctx, const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes);
+/*! fully converged cornerstone leaves of sorted keys (the unique tree of csarray.hpp:456-467).
+ *  leaves: capacity+1 entries, counts: capacity. *numLeaves receives the count; SX_ERR_ARG if capacity is short. */
+int sx_compute_octree(sx_ctx* ctx, const uint64_t* sortedKeys, size_t n, uint32_t bucketSize, uint64_t* leaves,
+                      uint32_t* counts, int32_t capacity, int32_t* numLeaves);
+int sx_build_octree(sx_ctx* ctx, const uint64_t* leaves, int32_t numLeaves, const sx_octree* out);
+int sx_node_centers(sx_ctx* ctx, const uint64_t* prefixes, int32_t numNodes, const sx_box* box, double* centers,
+                    double* sizes);
+/*! layout[i] = exclusive prefix sum of counts (layout has numLeaves+1 entries) */
+int sx_leaf_layout(sx_ctx* ctx, const uint32_t* counts, int32_t numLeaves, uint32_t* layout);
+
+/* ---- sph ------------------------------------------------------------------------------------------------- */
+int sx_compute_groups(sx_ctx* ctx, uint32_t first, uint32_t last, sx_groups* groups);
+/*! neighbor search for targets [first,last) into the context's list; iterate_h != 0 runs the h-nc iteration
+ *  (mutates h). nc has length fields->n (written at [first,last)). stats may be NULL. */
+int sx_find_neighbors(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                      const sx_params* p, uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats);
+/*! copy the cached list out / in, CPU layout neighbors[(i-first)*ngmax + k] (device pointers); export zero-fills
+ *  slots k >= min(nc[i]-1, ngmax) */
+int sx_export_neighbors(sx_ctx* ctx, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
+                        uint32_t* neighbors);
+int sx_import_neighbors(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* neighbors);
+
+int sx_xmass(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+             const sx_tree* tree);
+/*! xmass on the cached (or imported) neighbor list, without a new search */
+int sx_xmass_only(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
+int sx_ve_def_gradh(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
+int sx_eos(sx_ctx* ctx, uint32_t first, uint32_t last, float mui, double gamma, const double* temp, const float* m,
+           const float* kx, const float* xm, const float* gradh, float* prho, float* c, float* rho, float* p);
+int sx_iad_divv_curlv(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
+int sx_av_switches(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                   double minDt);
+/*! writes ax,ay,az,du; *minDtCourant receives the min Courant time-step (float, like minDt_ve_device) */
+int sx_momentum_energy(sx_ctx* ctx, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
+                       const sx_box* box, float* minDtCourant);
+/*! 2nd-order Press position update + AB2 energy update on temp (positions.hpp:54-139, F2-correct); dt, dt_m1 double
+ *  as in the CPU path (the reference GPU path passes them as float). */
+int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
+                 double gamma, float muiConst, const sx_box* box);
+int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
+int sx_max_divv(sx_ctx* ctx, uint32_t first, uint32_t last, const float* divv, float* maxDivv);
+
+/* ---- device-resident simulation: one HydroVeProp step per call ----------------------------------------- */
+typedef struct sx_sim sx_sim;
+/*! Sedov lattice (sedov_init.hpp:48-130) of side^3 particles; with nranks > 1 only this rank's SFC share. */
+int    sx_sim_create(sx_sim** sim, sx_ctx* ctx, size_t capacity, const sx_params* p, const sx_box* box,
+                     uint32_t bucketSize);
+void   sx_sim_destroy(sx_sim* sim);
+int    sx_sim_init_sedov(sx_sim* sim, uint32_t side);
+/*! upload a host state (conserved fields, length n) */
+int    sx_sim_set_state(sx_sim* sim, size_t n, const double* x, const double* y, const double* z, const float* h,
+                        const float* m, const double* temp, const float* vx, const float* vy, const float* vz,
+                        const float* x_m1, const float* y_m1, const float* z_m1, const float* du_m1,
+                        const float* alpha, const uint64_t* id, double minDt, double minDt_m1);
+/*! device field pointers of the current state (valid until the next step) */
+int    sx_sim_fields(sx_sim* sim, sx_fields* f, uint64_t** id);
+size_t sx_sim_size(sx_sim* sim);
+/*! one VE step; the time-step scalars stay on the device (no host sync unless stats are requested) */
+int    sx_sim_step(sx_sim* sim);
+/*! minDt, minDt_m1, ttot, minDtCourant, minDtRho (synchronises) */
+int    sx_sim_scalars(sx_sim* sim, double out[5]);
+/*! per-stage device time of the last step (ms) measured with HIP events, names in stage order */
+int    sx_sim_stage_times(sx_sim* sim, float* ms, int cap, const char** names);
+int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,649 @@
+/*! @file sx_capi.cpp
+ * @brief C-ABI (include/sphexa_hip.h): context, per-call entry points mirroring sph::cuda::compute* and the
+ *        cstone GPU tree functions, and the device-resident VE step driver (sx_sim_*).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/sphexa_hip.h"
+#include "sx_hydro.hpp"
+#include "sx_tree.hpp"
+
+using namespace sx;
+
+// ---------------------------------------------------------------------------------------------------------------
+// kernel tables: sinc^6 kernel, K by Simpson (sph/sph_kernel_tables.hpp:27-101, kernels.hpp:35-57)
+// ---------------------------------------------------------------------------------------------------------------
+namespace
+{
+
+double wharmonic(double v)
+{
+    if (v == 0.0) return 1.0;
+    const double Pv = M_PI_2 * v;
+    return std::sin(Pv) / Pv;
+}
+
+double wharmonicDerivative(double v)
+{
+    if (v == 0.0) return 0.0;
+    const double Pv    = M_PI_2 * v;
+    const double sincv = std::sin(Pv) / Pv;
+    return sincv * M_PI_2 * ((std::cos(Pv) / std::sin(Pv)) - 1.0 / Pv);
+}
+
+double sinc6(double x) { return std::pow(wharmonic(x), 6.0); }
+double sinc6d(double x) { return 6.0 * std::pow(wharmonic(x), 6.0 - 1) * wharmonicDerivative(x); }
+double kvol(double x) { return 4.0 * M_PI * x * x * sinc6(x); }
+
+double simpsonK()
+{
+    const uint64_t n = 2000;
+    double a = 0, b = 2.0, h = (b - a) / double(n);
+    std::vector<double> odd(n / 2), even(n / 2 - 1);
+    for (uint64_t i = 0; i < odd.size(); ++i)
+        odd[i] = kvol(a + double(2 * (i + 1) - 1) * h);
+    for (uint64_t i = 0; i < even.size(); ++i)
+        even[i] = kvol(a + double(2 * (i + 1)) * h);
+    std::sort(odd.begin(), odd.end());
+    std::sort(even.begin(), even.end());
+    double so = 0, se = 0;
+    for (double v : odd)
+        so += v;
+    for (double v : even)
+        se += v;
+    return 1.0 / (h / 3.0 * (kvol(a) + kvol(b) + 4.0 * so + 2.0 * se));
+}
+
+void makeTables(std::vector<float>& wh, std::vector<float>& whd)
+{
+    wh.resize(kTableSize);
+    whd.resize(kTableSize);
+    const float dx = (float)((2.0 - 0.0) / (kTableSize - 1));
+    for (size_t i = 0; i < (size_t)kTableSize; ++i)
+    {
+        float nv = (float)(0.0 + (float)i * dx);
+        wh[i]    = (float)sinc6((double)nv);
+        whd[i]   = (float)sinc6d((double)nv);
+    }
+}
+
+DevBox toDev(const sx_box* b)
+{
+    DevBox d{};
+    for (int k = 0; k < 6; ++k)
+        d.lim[k] = b->lim[k];
+    d.anyPbc = 0;
+    for (int k = 0; k < 3; ++k)
+    {
+        d.l[k]   = b->lim[2 * k + 1] - b->lim[2 * k];
+        d.il[k]  = 1.0 / (b->lim[2 * k + 1] - b->lim[2 * k]);
+        d.pbc[k] = b->bnd[k] == 1;
+        d.fbc[k] = b->bnd[k] == 2;
+        d.anyPbc |= d.pbc[k];
+    }
+    return d;
+}
+
+double quantMargin(const DevBox& b)
+{
+    double l = std::max(b.l[0], std::max(b.l[1], b.l[2]));
+    return 4.0 * l / double(1u << kMaxLevel);
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------------------------------
+struct sx_ctx
+{
+    int         device{0};
+    hipStream_t own{nullptr};
+    hipStream_t stream{nullptr};
+    bool        exact{false};
+    Arena       arena;
+    float2*     wh{nullptr};
+    float2*     whd{nullptr};
+    double      K{0};
+    std::string err;
+
+    // neighbor-list cache
+    uint32_t* nidx{nullptr};
+    uint32_t  nbFirst{0}, nbLast{0}, nbNgmax{0};
+    bool      nbValid{false};
+    size_t    nbFields{0};
+
+    uint32_t* stats{nullptr}; // device, 8 words
+    uint32_t* statsHost{nullptr};
+    float*    minDt{nullptr}; // device scalar
+    unsigned* maxU{nullptr};  // device scalar
+    float*    hostScalar{nullptr};
+
+    float*   powTab{nullptr}; // updateH factor by nc, glibc powf (sx_device.hpp)
+    uint32_t powTabNg0{0};
+
+    const HydroLaunch& hydro() const { return exact ? hydro_exact() : hydro_fast(); }
+};
+
+//! updateH's pow factor for every nc < kPowTable, computed with the host libm powf the reference calls
+static const float* ensurePowTab(sx_ctx* c, uint32_t ng0)
+{
+    if (c->powTab && c->powTabNg0 == ng0) return c->powTab;
+    std::vector<float> t(kPowTable);
+    const float        c0 = 1023.0f;
+    const float        ex = (float)(1.0 / 10.0);
+    t[0]                  = INFINITY;
+    for (uint32_t nc = 1; nc < kPowTable; ++nc)
+    {
+        volatile float base = 1.0f + c0 * ng0 / (float)nc; // volatile: keep the call out of constant folding
+        t[nc]               = powf(base, ex);
+    }
+    c->powTab = c->arena.get<float>("powTab", kPowTable);
+    if (hipMemcpy(c->powTab, t.data(), kPowTable * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    c->powTabNg0 = ng0;
+    return c->powTab;
+}
+
+static int fail(sx_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+#define SX_HIP(ctx, call)                                                                                              \
+    do {                                                                                                               \
+        hipError_t e_ = (call);                                                                                        \
+        if (e_ != hipSuccess) return fail(ctx, SX_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));         \
+    } while (0)
+
+static uint32_t* ensureNidx(sx_ctx* c, uint32_t first, uint32_t last, uint32_t ngmax)
+{
+    size_t groups = (size_t(last - first) + kGroupSize - 1) / kGroupSize;
+    c->nidx       = c->arena.get<uint32_t>("nidx", std::max<size_t>(1, groups) * ngmax * kWave);
+    return c->nidx;
+}
+
+extern "C"
+{
+    void*         sx_ctx_stream_internal(sx_ctx* c) { return c->stream; }
+    int           sx_ctx_exact_internal(sx_ctx* c) { return c->exact ? 1 : 0; }
+    const float2* sx_ctx_table_internal(sx_ctx* c, int which) { return which ? c->whd : c->wh; }
+    const float*  sx_ctx_powtab_internal(sx_ctx* c, uint32_t ng0) { return ensurePowTab(c, ng0); }
+
+    double sx_kernel_constant(void)
+    {
+        static double K = simpsonK();
+        return K;
+    }
+
+    int sx_create(sx_ctx** out, int device)
+    {
+        auto* c   = new sx_ctx;
+        c->device = device;
+        if (hipSetDevice(device) != hipSuccess) return fail(c, SX_ERR_HIP, "hipSetDevice"), *out = c, SX_ERR_HIP;
+        SX_HIP(c, hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+        c->stream = c->own;
+        c->K      = sx_kernel_constant();
+        std::vector<float> wh, whd;
+        makeTables(wh, whd);
+        float* tmp = c->arena.get<float>("tables.raw", 2 * kTableSize);
+        SX_HIP(c, hipMemcpy(tmp, wh.data(), kTableSize * 4, hipMemcpyHostToDevice));
+        SX_HIP(c, hipMemcpy(tmp + kTableSize, whd.data(), kTableSize * 4, hipMemcpyHostToDevice));
+        c->wh  = c->arena.get<float2>("tables.wh", kTableSize);
+        c->whd = c->arena.get<float2>("tables.whd", kTableSize);
+        tablePairs(tmp, c->wh, c->stream);
+        tablePairs(tmp + kTableSize, c->whd, c->stream);
+        c->stats      = c->arena.get<uint32_t>("stats", 8);
+        c->statsHost  = c->arena.pinned<uint32_t>("statsHost", 8);
+        c->minDt      = c->arena.get<float>("minDt", 1);
+        c->maxU       = c->arena.get<unsigned>("maxU", 1);
+        c->hostScalar = c->arena.pinned<float>("hostScalar", 2);
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        *out = c;
+        return SX_OK;
+    }
+
+    void sx_destroy(sx_ctx* c)
+    {
+        if (!c) return;
+        (void)hipDeviceSynchronize();
+        c->arena.release();
+        if (c->own) (void)hipStreamDestroy(c->own);
+        delete c;
+    }
+
+    int sx_set_stream(sx_ctx* c, void* s)
+    {
+        c->stream = s ? (hipStream_t)s : c->own;
+        return SX_OK;
+    }
+    void*       sx_get_stream(sx_ctx* c) { return c->stream; }
+    const char* sx_last_error(sx_ctx* c) { return c ? c->err.c_str() : "no context"; }
+    int         sx_set_exact(sx_ctx* c, int e)
+    {
+        c->exact = e != 0;
+        return SX_OK;
+    }
+    int sx_synchronize(sx_ctx* c)
+    {
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        return SX_OK;
+    }
+
+    void* sx_device_alloc(sx_ctx* c, size_t bytes)
+    {
+        void* p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess)
+        {
+            fail(c, SX_ERR_NOMEM, "hipMalloc failed");
+            return nullptr;
+        }
+        return p;
+    }
+    int sx_device_free(sx_ctx* c, void* p)
+    {
+        SX_HIP(c, hipFree(p));
+        return SX_OK;
+    }
+    int sx_memcpy(sx_ctx* c, void* dst, const void* src, size_t bytes, int kind)
+    {
+        hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost
+                                                                          : hipMemcpyDeviceToDevice;
+        SX_HIP(c, hipMemcpyAsync(dst, src, bytes, k, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        return SX_OK;
+    }
+    int sx_memset(sx_ctx* c, void* dst, int value, size_t bytes)
+    {
+        SX_HIP(c, hipMemsetAsync(dst, value, bytes, c->stream));
+        return SX_OK;
+    }
+
+    int sx_copy_tables(sx_ctx* c, float* wh, float* whd)
+    {
+        std::vector<float> a, b;
+        makeTables(a, b);
+        std::copy(a.begin(), a.end(), wh);
+        std::copy(b.begin(), b.end(), whd);
+        return SX_OK;
+    }
+
+    // ---- cstone ------------------------------------------------------------------------------------------------
+
+    int sx_sfc_keys(sx_ctx* c, const double* x, const double* y, const double* z, uint64_t* keys, size_t n,
+                    const sx_box* box)
+    {
+        SX_HIP(c, launchSfcKeys(x, y, z, keys, n, toDev(box), c->stream));
+        return SX_OK;
+    }
+
+    int sx_sort_keys(sx_ctx* c, uint64_t* keys, uint32_t* order, size_t n)
+    {
+        SX_HIP(c, sortKeys(c->arena, keys, order, n, c->stream));
+        return SX_OK;
+    }
+
+    int sx_gather(sx_ctx* c, const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes)
+    {
+        SX_HIP(c, gather(order, n, src, dst, elemBytes, c->stream));
+        return SX_OK;
+    }
+
+    int sx_compute_octree(sx_ctx* c, const uint64_t* keys, size_t n, uint32_t bucket, uint64_t* leaves,
+                          uint32_t* counts, int32_t capacity, int32_t* numLeaves)
+    {
+        sx_box  ub{{0, 1, 0, 1, 0, 1}, {0, 0, 0}};
+        DevTree t;
+        SX_HIP(c, buildTree(c->arena, keys, n, bucket, toDev(&ub), t, c->stream));
+        *numLeaves = t.numLeaves;
+        if (capacity < t.numLeaves) return fail(c, SX_ERR_ARG, "sx_compute_octree: capacity too small");
+        SX_HIP(c, hipMemcpyAsync(leaves, t.leaves, (t.numLeaves + 1) * 8, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipMemcpyAsync(counts, t.counts, t.numLeaves * 4, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        return SX_OK;
+    }
+
+    int sx_build_octree(sx_ctx* c, const uint64_t* leaves, int32_t numLeaves, const sx_octree* out)
+    {
+        // the cornerstone leaf starts, used as keys with bucket 1, reproduce exactly this tree: a leaf holds one
+        // start key (its own), every internal node holds at least two
+        DevTree t;
+        sx_box  ub{{0, 1, 0, 1, 0, 1}, {0, 0, 0}};
+        SX_HIP(c, buildTree(c->arena, leaves, (size_t)numLeaves, 1, toDev(&ub), t, c->stream));
+        if (t.numLeaves != numLeaves) return fail(c, SX_ERR_ARG, "sx_build_octree: leaves are not a cornerstone tree");
+        int nn = t.numNodes;
+        SX_HIP(c, hipMemcpyAsync(out->prefixes, t.prefixes, nn * 8, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipMemcpyAsync(out->childOffsets, t.childOffsets, (nn + 1) * 4, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipMemcpyAsync(out->parents, t.parents, t.parentsSize() * 4, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipMemcpyAsync(out->levelRange, t.levelRange, (kMaxLevel + 2) * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        SX_HIP(c, hipMemcpyAsync(out->internalToLeaf, t.internalToLeaf, nn * 4, hipMemcpyDeviceToDevice, c->stream));
+        SX_HIP(c, hipMemcpyAsync(out->leafToInternal, t.leafToInternal, nn * 4, hipMemcpyDeviceToDevice, c->stream));
+        return SX_OK;
+    }
+
+    int sx_node_centers(sx_ctx* c, const uint64_t* prefixes, int32_t numNodes, const sx_box* box, double* centers,
+                        double* sizes)
+    {
+        SX_HIP(c, nodeCenters(prefixes, numNodes, toDev(box), centers, sizes, c->stream));
+        return SX_OK;
+    }
+
+    int sx_leaf_layout(sx_ctx* c, const uint32_t* counts, int32_t numLeaves, uint32_t* layout)
+    {
+        SX_HIP(c, leafLayout(c->arena, counts, numLeaves, layout, c->stream));
+        return SX_OK;
+    }
+
+    // ---- sph ---------------------------------------------------------------------------------------------------
+
+    int sx_compute_groups(sx_ctx* c, uint32_t first, uint32_t last, sx_groups* g)
+    {
+        g->firstBody  = first;
+        g->lastBody   = last;
+        g->numGroups  = (last - first + kGroupSize - 1) / kGroupSize;
+        g->groupStart = nullptr;
+        g->groupEnd   = nullptr;
+        (void)c;
+        return SX_OK;
+    }
+
+    int sx_find_neighbors(sx_ctx* c, const sx_fields* f, const sx_tree* tree, const sx_box* box, const sx_params* p,
+                          uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats)
+    {
+        if (!f || !tree || !box || !p || last < first || last > f->n)
+            return fail(c, SX_ERR_ARG, "sx_find_neighbors: bad arguments");
+        NsArgs a{};
+        a.first          = first;
+        a.last           = last;
+        a.numGroups      = (last - first + kGroupSize - 1) / kGroupSize;
+        a.ngmax          = p->ngmax;
+        a.ng0            = p->ng0;
+        a.iterateH       = iterate_h;
+        a.x              = f->x;
+        a.y              = f->y;
+        a.z              = f->z;
+        a.h              = f->h;
+        a.nc             = f->nc;
+        a.nidx           = ensureNidx(c, first, last, p->ngmax);
+        a.childOffsets   = tree->childOffsets;
+        a.internalToLeaf = tree->internalToLeaf;
+        a.layout         = tree->layout;
+        a.centers        = tree->centers;
+        a.sizes          = tree->sizes;
+        a.box            = toDev(box);
+        a.margin         = quantMargin(a.box);
+        a.stats          = c->stats;
+        a.powTab         = ensurePowTab(c, p->ng0);
+        if (!a.nidx || !a.powTab) return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
+        SX_HIP(c, hipMemsetAsync(c->stats, 0, 32, c->stream));
+        SX_HIP(c, findNeighbors(a, c->stream));
+        SX_HIP(c, hipMemcpyAsync(c->statsHost, c->stats, 32, hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        c->nbFirst = first;
+        c->nbLast  = last;
+        c->nbNgmax = p->ngmax;
+        c->nbValid = true;
+        if (stats)
+        {
+            stats->numFailed     = c->statsHost[1];
+            stats->maxNeighbors  = c->statsHost[2];
+            stats->sumNeighbors  = *reinterpret_cast<uint64_t*>(c->statsHost + 4);
+            stats->sumCandidates = *reinterpret_cast<uint64_t*>(c->statsHost + 6);
+        }
+        if (c->statsHost[0] & 1u) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in neighbor search");
+        if (iterate_h && c->statsHost[1]) return fail(c, SX_ERR_NOT_CONVERGED, "coupled nc/h-updated failed to converge");
+        return SX_OK;
+    }
+
+    int sx_export_neighbors(sx_ctx* c, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
+                               uint32_t* out)
+    {
+        if (!c->nbValid || first != c->nbFirst || last != c->nbLast || ngmax != c->nbNgmax)
+            return fail(c, SX_ERR_ARG, "sx_export_neighbors: no matching neighbor list");
+        SX_HIP(c, exportNeighbors(c->nidx, nc, first, last, ngmax, out, c->stream));
+        return SX_OK;
+    }
+
+    int sx_import_neighbors(sx_ctx* c, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in)
+    {
+        uint32_t* nidx = ensureNidx(c, first, last, ngmax);
+        if (!nidx) return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
+        SX_HIP(c, importNeighbors(nidx, first, last, ngmax, in, c->stream));
+        c->nbFirst = first;
+        c->nbLast  = last;
+        c->nbNgmax = ngmax;
+        c->nbValid = true;
+        return SX_OK;
+    }
+} // extern "C"
+
+// ---- pair-kernel plumbing --------------------------------------------------------------------------------------
+
+namespace
+{
+
+struct Records
+{
+    RecX* rx;
+    RecV* rv;
+    RecT* rt;
+    RecC* rc;
+};
+
+Records records(sx_ctx* c, size_t n)
+{
+    return {c->arena.get<RecX>("rec.x", n), c->arena.get<RecV>("rec.v", n), c->arena.get<RecT>("rec.t", n),
+            c->arena.get<RecC>("rec.c", n)};
+}
+
+int checkList(sx_ctx* c, const sx_groups* g, const sx_params* p)
+{
+    if (!c->nbValid || g->firstBody != c->nbFirst || g->lastBody != c->nbLast || p->ngmax != c->nbNgmax)
+        return fail(c, SX_ERR_ARG, "no neighbor list for this range: call sx_xmass or sx_find_neighbors first");
+    return SX_OK;
+}
+
+PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                  const Records& r)
+{
+    PairArgs a{};
+    a.first          = g->firstBody;
+    a.last           = g->lastBody;
+    a.numGroups      = (g->lastBody - g->firstBody + kGroupSize - 1) / kGroupSize;
+    a.ngmax          = p->ngmax;
+    a.nidx           = c->nidx;
+    a.nc             = f->nc;
+    a.rx             = r.rx;
+    a.rv             = r.rv;
+    a.rt             = r.rt;
+    a.rc             = r.rc;
+    a.wh             = c->wh;
+    a.whd            = c->whd;
+    a.box            = toDev(box);
+    a.K              = p->K;
+    a.xm             = f->xm;
+    a.kx             = f->kx;
+    a.gradh          = f->gradh;
+    a.c11            = f->c11;
+    a.c12            = f->c12;
+    a.c13            = f->c13;
+    a.c22            = f->c22;
+    a.c23            = f->c23;
+    a.c33            = f->c33;
+    a.divv           = f->divv;
+    a.curlv          = f->curlv;
+    a.alpha          = f->alpha;
+    a.ax             = f->ax;
+    a.ay             = f->ay;
+    a.az             = f->az;
+    a.du             = f->du;
+    a.minDt          = c->minDt;
+    a.alphamin       = p->alphamin;
+    a.alphamax       = p->alphamax;
+    a.decay_constant = p->decay_constant;
+    a.Atmin          = p->Atmin;
+    a.Atmax          = p->Atmax;
+    a.ramp           = p->ramp;
+    a.Kcour          = (float)p->Kcour;
+    return a;
+}
+
+} // namespace
+
+extern "C"
+{
+
+    int sx_xmass(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                 const sx_tree* tree)
+    {
+        int rc = sx_find_neighbors(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
+        if (rc != SX_OK) return rc;
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        c->hydro().xmass(pairArgs(c, g, f, p, box, r), c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_xmass_only(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        c->hydro().xmass(pairArgs(c, g, f, p, box, r), c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_ve_def_gradh(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packT(f->n, f->xm, nullptr, nullptr, nullptr, r.rt, c->stream);
+        c->hydro().veDefGradh(pairArgs(c, g, f, p, box, r), c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_eos(sx_ctx* c, uint32_t first, uint32_t last, float mui, double gamma, const double* temp, const float* m,
+               const float* kx, const float* xm, const float* gradh, float* prho, float* cs, float* rho, float* pr)
+    {
+        EosArgs a{first, last, mui, gamma, temp, m, kx, xm, gradh, prho, cs, rho, pr};
+        c->hydro().eos(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_iad_divv_curlv(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packV(f->n, f->vx, f->vy, f->vz, nullptr, r.rv, c->stream);
+        packT(f->n, f->xm, f->kx, nullptr, nullptr, r.rt, c->stream);
+        c->hydro().iadDivvCurlv(pairArgs(c, g, f, p, box, r), c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_av_switches(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                       double minDt)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
+        packT(f->n, f->xm, f->kx, nullptr, f->alpha, r.rt, c->stream);
+        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, f->divv, r.rc, c->stream);
+        PairArgs a = pairArgs(c, g, f, p, box, r);
+        a.dt       = minDt;
+        c->hydro().avSwitches(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_momentum_energy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
+                           const sx_box* box, float* minDtCourant)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        if (f->tdpdTrho) return fail(c, SX_ERR_ARG, "tdpdTrho != NULL is not supported by the VE momentum kernel");
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
+        packT(f->n, f->xm, f->kx, f->prho, f->alpha, r.rt, c->stream);
+        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, nullptr, r.rc, c->stream);
+        float huge = 1e10f; // momentum_energy_gpu.cu:127
+        SX_HIP(c, hipMemcpyAsync(c->minDt, &huge, 4, hipMemcpyHostToDevice, c->stream));
+        PairArgs a = pairArgs(c, g, f, p, box, r);
+        a.groupDt  = groupDt;
+        c->hydro().momentumEnergy(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->minDt, 4, hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        if (minDtCourant) *minDtCourant = c->hostScalar[0];
+        return SX_OK;
+    }
+
+    int sx_positions(sx_ctx* c, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
+                     double gamma, float muiConst, const sx_box* box)
+    {
+        PosArgs a{};
+        a.first   = first;
+        a.last    = last;
+        a.dt      = dt;
+        a.dt_m1   = dt_m1;
+        a.dtPtr   = nullptr;
+        a.box     = toDev(box);
+        a.x       = f->x;
+        a.y       = f->y;
+        a.z       = f->z;
+        a.x_m1    = f->x_m1;
+        a.y_m1    = f->y_m1;
+        a.z_m1    = f->z_m1;
+        a.vx      = f->vx;
+        a.vy      = f->vy;
+        a.vz      = f->vz;
+        a.ax      = f->ax;
+        a.ay      = f->ay;
+        a.az      = f->az;
+        a.temp    = f->temp;
+        a.du      = f->du;
+        a.du_m1   = f->du_m1;
+        a.h       = f->h;
+        a.constCv = idealGasCv(muiConst, gamma);
+        c->hydro().positions(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_update_h(sx_ctx* c, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h)
+    {
+        const float* tab = ensurePowTab(c, ng0);
+        if (!tab) return fail(c, SX_ERR_NOMEM, "powTab");
+        c->hydro().updateH(first, last, ng0, nc, h, tab, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_max_divv(sx_ctx* c, uint32_t first, uint32_t last, const float* divv, float* out)
+    {
+        SX_HIP(c, maxFloat(divv, first, last, c->maxU, c->stream));
+        unsigned u;
+        SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->maxU, 4, hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        std::memcpy(&u, c->hostScalar, 4);
+        u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+        std::memcpy(out, &u, 4);
+        return SX_OK;
+    }
+
+} // extern "C"

@@ -1,0 +1,163 @@
+/*! @file sx_device.hpp
+ * @brief gfx950 device helpers shared by the hot-path kernels: box / periodic folding, kernel-table lookup,
+ *        packed neighbor records, wave64 reductions.
+ *
+ * Arithmetic follows the reference expressions and promotions exactly (see oracle/sph_oracle.c for the CPU
+ * restatement): e.g. the legacy applyPBC<double,float> subtracts the box length in double and rounds to float
+ * (cstone/sfc/box.hpp:233-255).  Files compiled with -ffp-contract=off (the "exact" variant) reproduce the CPU
+ * reference bit-for-bit given the same neighbor order; the default variant lets the compiler form FMAs.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sx
+{
+
+constexpr int kWave       = 64;    // CDNA4 wavefront
+constexpr int kTableSize  = 20000; // sph::lt::kTableSize (table_lookup.hpp:12)
+constexpr int kMaxLevel   = 21;    // maxTreeLevel<uint64_t>
+constexpr int kGroupSize  = 64;    // particles per neighbor-list block = one wavefront
+
+//! box data as the kernels need it (cstone::Box<double>, sfc/box.hpp:111-191)
+struct DevBox
+{
+    double lim[6];
+    double l[3];  // lengths_  = max - min
+    double il[3]; // inverseLengths_ = 1 / (max - min)
+    int    pbc[3];
+    int    fbc[3];
+    int    anyPbc;
+};
+
+//! packed per-particle records gathered by neighbor index (16-byte aligned, one or two dwordx4 each)
+struct __attribute__((aligned(16))) RecX
+{
+    double x, y, z;
+    float  h, m;
+};
+struct __attribute__((aligned(16))) RecV
+{
+    float vx, vy, vz, c;
+};
+struct __attribute__((aligned(16))) RecT
+{
+    float xm, kx, prho, alpha;
+};
+struct __attribute__((aligned(16))) RecC
+{
+    float c11, c12, c13, c22, c23, c33, divv, pad;
+};
+
+//! lt::lookup<float> (table_lookup.hpp:14-26) on a pair table {t[i], t[i+1]-t[i]}: one 8-byte gather.
+//! The stored difference is the same float subtraction the reference performs, so results are identical.
+__device__ __forceinline__ float lookup(const float2* __restrict__ tab, float v)
+{
+    constexpr int   numIntervals = kTableSize - 1;
+    constexpr float dx           = 2.0f / numIntervals;
+    constexpr float invDx        = 1.0f / dx;
+    int             idx          = (int)(v * invDx);
+    if (idx >= numIntervals) return 0.0f;
+    float2 e          = tab[idx];
+    float  derivative = e.y * invDx;
+    return e.x + derivative * (v - (float)idx * dx);
+}
+
+//! legacy applyPBC<double,float> (box.hpp:233-255)
+__device__ __forceinline__ void applyPBC(const DevBox& b, float r, float& xx, float& yy, float& zz)
+{
+    if (b.pbc[0] && xx > r) xx = (float)((double)xx - b.l[0]);
+    else if (b.pbc[0] && xx < -r) xx = (float)((double)xx + b.l[0]);
+    if (b.pbc[1] && yy > r) yy = (float)((double)yy - b.l[1]);
+    else if (b.pbc[1] && yy < -r) yy = (float)((double)yy + b.l[1]);
+    if (b.pbc[2] && zz > r) zz = (float)((double)zz - b.l[2]);
+    else if (b.pbc[2] && zz < -r) zz = (float)((double)zz + b.l[2]);
+}
+
+constexpr uint32_t kPowTable = 1u << 16; //!< nc values covered by the host-computed powf table
+
+/*! updateH<float> (kernels.hpp:26-32): h * 0.5 * std::pow(1 + 1023*ng0/nc, 0.1f).
+ *  The reference calls glibc powf, which is not correctly rounded (0.5+ ULP on e.g. nc = 166 is reached only
+ *  via 1 + 102300/nc; 112 of nc <= 2e5 differ from a correctly rounded pow).  nc is an integer and ng0 fixed per
+ *  run, so the factor is tabulated on the host with glibc powf itself (powTab[nc], nc < 2^16) and the device
+ *  result is bit-identical; beyond the table a double pow is used (never reached: nc <= N and the h iteration
+ *  keeps nc near ng0). */
+__device__ __forceinline__ float updateH(unsigned ng0, unsigned nc, float h, const float* __restrict__ powTab)
+{
+    float f;
+    if (nc < kPowTable) { f = powTab[nc]; }
+    else
+    {
+        const float c0   = 1023.0f;
+        const float ex   = (float)(1.0 / 10.0);
+        float       base = 1.0f + c0 * ng0 / (float)nc;
+        f                = (float)pow((double)base, (double)ex);
+    }
+    return h * 0.5f * f;
+}
+
+//! tsKCourant<float> (kernels.hpp:12-18)
+__device__ __forceinline__ float tsKCourant(float maxvsignal, float h, float c, float Kcour)
+{
+    float v = maxvsignal > 0.0f ? maxvsignal : c;
+    return Kcour * h / v;
+}
+
+//! idealGasCv<float,double> (sph/eos.hpp:13-18)
+__host__ __device__ __forceinline__ float idealGasCv(float mui, double gamma)
+{
+    const float R = 8.317e7f;
+    return (float)((double)(R / mui) / (gamma - 1.0f));
+}
+
+// ---- wave64 reductions (cross-lane through DPP/ds_swizzle via __shfl_xor) ----------------------------------
+
+template<class T>
+__device__ __forceinline__ T waveMin(T v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+    {
+        T w = __shfl_xor(v, o, kWave);
+        v   = w < v ? w : v;
+    }
+    return v;
+}
+
+template<class T>
+__device__ __forceinline__ T waveMax(T v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+    {
+        T w = __shfl_xor(v, o, kWave);
+        v   = w > v ? w : v;
+    }
+    return v;
+}
+
+template<class T>
+__device__ __forceinline__ T waveSum(T v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__device__ __forceinline__ double readlaneD(double v, int k)
+{
+    int2 p = *reinterpret_cast<int2*>(&v);
+    p.x    = __builtin_amdgcn_readlane(p.x, k);
+    p.y    = __builtin_amdgcn_readlane(p.y, k);
+    return *reinterpret_cast<double*>(&p);
+}
+
+//! float atomic min for non-negative values via the ordered int representation
+__device__ __forceinline__ void atomicMinPos(float* addr, float v)
+{
+    atomicMin(reinterpret_cast<int*>(addr), __float_as_int(v));
+}
+
+} // namespace sx

@@ -1,0 +1,163 @@
+/*! @file sx_tree.hpp
+ * @brief device arena, tree container and host launchers of the cstone part (sx_tree.hip) and the neighbor
+ *        search (sx_neighbors.hip).
+ */
+#pragma once
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "sx_device.hpp"
+
+namespace sx
+{
+
+//! grow-only named device (and pinned host) buffers owned by a context; no allocation inside a steady-state step
+class Arena
+{
+public:
+    ~Arena() { release(); }
+
+    template<class T>
+    T* get(const std::string& tag, size_t count)
+    {
+        return static_cast<T*>(getBytes(tag, std::max<size_t>(1, count) * sizeof(T), false));
+    }
+    template<class T>
+    T* pinned(const std::string& tag, size_t count)
+    {
+        return static_cast<T*>(getBytes(tag, std::max<size_t>(1, count) * sizeof(T), true));
+    }
+    size_t bytesAllocated() const
+    {
+        size_t s = 0;
+        for (auto& kv : bufs_)
+            if (!kv.second.host) s += kv.second.bytes;
+        return s;
+    }
+    void release()
+    {
+        for (auto& kv : bufs_)
+        {
+            if (kv.second.host) (void)hipHostFree(kv.second.ptr);
+            else (void)hipFree(kv.second.ptr);
+        }
+        bufs_.clear();
+    }
+    bool failed() const { return failed_; }
+
+private:
+    struct Buf
+    {
+        void*  ptr{nullptr};
+        size_t bytes{0};
+        bool   host{false};
+    };
+    void* getBytes(const std::string& tag, size_t bytes, bool host)
+    {
+        auto it = bufs_.find(tag);
+        if (it != bufs_.end() && it->second.bytes >= bytes) return it->second.ptr;
+        if (it != bufs_.end())
+        {
+            (void)hipDeviceSynchronize();
+            if (it->second.host) (void)hipHostFree(it->second.ptr);
+            else (void)hipFree(it->second.ptr);
+            bufs_.erase(it);
+        }
+        size_t alloc = bytes + bytes / 8 + 256; // 12.5 % growth headroom (allocGrowthRate-style)
+        void*  p     = nullptr;
+        hipError_t e = host ? hipHostMalloc(&p, alloc) : hipMalloc(&p, alloc);
+        if (e != hipSuccess)
+        {
+            failed_ = true;
+            return nullptr;
+        }
+        bufs_[tag] = Buf{p, alloc, host};
+        return p;
+    }
+    std::map<std::string, Buf> bufs_;
+    bool                       failed_{false};
+};
+
+//! the converged tree of one sync, in the reference OctreeData + OctreeNsView format
+struct DevTree
+{
+    int       numLeaves{0}, numNodes{0}, numInternal{0};
+    uint64_t* leaves{nullptr};   // numLeaves + 1
+    uint32_t* counts{nullptr};   // numLeaves + 1 (trailing 0 for the layout scan)
+    uint32_t* layout{nullptr};   // numLeaves + 1
+    uint64_t* prefixes{nullptr}; // numNodes
+    int32_t*  childOffsets{nullptr};
+    int32_t*  parents{nullptr};
+    int32_t*  levelRange{nullptr};
+    int32_t*  internalToLeaf{nullptr};
+    int32_t*  leafToInternal{nullptr};
+    double*   centers{nullptr};
+    double*   sizes{nullptr};
+
+    int  parentsSize() const { return std::max(1, (numNodes - 1) / 8); }
+    void reserve(Arena& a)
+    {
+        leaves         = a.get<uint64_t>("dt.leaves", numLeaves + 1);
+        counts         = a.get<uint32_t>("dt.counts", numLeaves + 1);
+        layout         = a.get<uint32_t>("dt.layout", numLeaves + 1);
+        prefixes       = a.get<uint64_t>("dt.prefixes", numNodes);
+        childOffsets   = a.get<int32_t>("dt.childOffsets", numNodes + 1);
+        parents        = a.get<int32_t>("dt.parents", parentsSize());
+        levelRange     = a.get<int32_t>("dt.levelRange", kMaxLevel + 2);
+        internalToLeaf = a.get<int32_t>("dt.internalToLeaf", numNodes);
+        leafToInternal = a.get<int32_t>("dt.leafToInternal", numNodes);
+        centers        = a.get<double>("dt.centers", 3 * (size_t)numNodes);
+        sizes          = a.get<double>("dt.sizes", 3 * (size_t)numNodes);
+    }
+};
+
+//! neighbor-search arguments (sx_neighbors.hip)
+struct NsArgs
+{
+    uint32_t        first, last, numGroups, ngmax, ng0;
+    int             iterateH;
+    const double *  x, *y, *z;
+    float*          h;
+    uint32_t*       nc;
+    uint32_t*       nidx;
+    // tree (OctreeNsView)
+    const int32_t*  childOffsets;
+    const int32_t*  internalToLeaf;
+    const uint32_t* layout;
+    const double*   centers;
+    const double*   sizes;
+    DevBox          box;
+    double          margin; // node-box inflation covering key quantisation round-off
+    const float*    powTab; // glibc powf(1 + 1023*ng0/nc, 0.1f) by nc (updateH)
+    uint32_t*       stats;  // [0] error flags, [1] failures, [2] max count, [3] pad, [4..5] sum nbrs (u64), [6..7] sum cand
+};
+
+hipError_t launchSfcKeys(const double* x, const double* y, const double* z, uint64_t* keys, size_t n,
+                         const DevBox& b, hipStream_t s);
+hipError_t sortKeys(Arena& arena, uint64_t* keys, uint32_t* order, size_t n, hipStream_t s);
+hipError_t gather(const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes, hipStream_t s);
+hipError_t buildTree(Arena& arena, const uint64_t* keys, size_t n, uint32_t bucket, const DevBox& box, DevTree& t,
+                     hipStream_t s);
+hipError_t nodeCenters(const uint64_t* prefixes, int numNodes, const DevBox& b, double* centers, double* sizes,
+                       hipStream_t s);
+hipError_t leafLayout(Arena& arena, const uint32_t* counts, int numLeaves, uint32_t* layout, hipStream_t s);
+hipError_t maxFloat(const float* v, uint32_t first, uint32_t last, unsigned* out, hipStream_t s);
+void       packX(size_t n, const double* x, const double* y, const double* z, const float* h, const float* m, RecX* out,
+                 hipStream_t s);
+void       packV(size_t n, const float* vx, const float* vy, const float* vz, const float* c, RecV* out, hipStream_t s);
+void       packT(size_t n, const float* xm, const float* kx, const float* prho, const float* alpha, RecT* out,
+                 hipStream_t s);
+void       packC(size_t n, const float* c11, const float* c12, const float* c13, const float* c22, const float* c23,
+                 const float* c33, const float* divv, RecC* out, hipStream_t s);
+void       tablePairs(const float* t, float2* out, hipStream_t s);
+
+hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
+hipError_t exportNeighbors(const uint32_t* nidx, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
+                           uint32_t* out, hipStream_t s);
+hipError_t importNeighbors(uint32_t* nidx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in,
+                           hipStream_t s);
+
+} // namespace sx

@@ -1,0 +1,338 @@
+"""ctypes binding of libsphexa_hip.so (include/sphexa_hip.h) -- the host-side mirror used by tests and bench.
+
+The product is the C-ABI library; this module only marshals plain pointers.  It never falls back to a CPU
+path: if the library is missing, importing `lib()` raises.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(os.path.dirname(HERE))          # .../sph-exa_amd
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "libsphexa_hip.so")
+HEADER = os.path.join(ROOT, "include", "sphexa_hip.h")
+
+SX_OK, SX_ERR_TRAVERSAL, SX_ERR_NOT_CONVERGED, SX_ERR_HIP, SX_ERR_ARG, SX_ERR_NOMEM = range(6)
+KTABLE = 20000
+GROUP = 64
+
+
+class SxBox(C.Structure):
+    _fields_ = [("lim", C.c_double * 6), ("bnd", C.c_int32 * 3)]
+
+
+class SxParams(C.Structure):
+    _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
+                ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
+                ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double)]
+
+
+_P = C.c_void_p
+FIELD_ORDER = [  # sx_fields, ParticlesData order
+    ("x", _P), ("y", _P), ("z", _P), ("x_m1", _P), ("y_m1", _P), ("z_m1", _P), ("vx", _P), ("vy", _P), ("vz", _P),
+    ("rho", _P), ("u", _P), ("p", _P), ("prho", _P), ("tdpdTrho", _P), ("h", _P), ("m", _P), ("c", _P),
+    ("ax", _P), ("ay", _P), ("az", _P), ("du", _P), ("du_m1", _P), ("c11", _P), ("c12", _P), ("c13", _P),
+    ("c22", _P), ("c23", _P), ("c33", _P), ("mue", _P), ("mui", _P), ("temp", _P), ("cv", _P), ("xm", _P),
+    ("kx", _P), ("divv", _P), ("curlv", _P), ("alpha", _P), ("gradh", _P), ("keys", _P), ("nc", _P),
+    ("dV11", _P), ("dV12", _P), ("dV13", _P), ("dV22", _P), ("dV23", _P), ("dV33", _P), ("markRamp", _P),
+    ("rung", _P)]
+
+
+class SxFields(C.Structure):
+    _fields_ = [("n", C.c_size_t)] + FIELD_ORDER
+
+
+class SxTree(C.Structure):
+    _fields_ = [("numLeafNodes", C.c_int32), ("numNodes", C.c_int32), ("prefixes", _P), ("childOffsets", _P),
+                ("internalToLeaf", _P), ("levelRange", _P), ("leaves", _P), ("layout", _P), ("centers", _P),
+                ("sizes", _P), ("searchExtFactor", C.c_float)]
+
+
+class SxGroups(C.Structure):
+    _fields_ = [("firstBody", C.c_uint32), ("lastBody", C.c_uint32), ("numGroups", C.c_uint32),
+                ("groupStart", _P), ("groupEnd", _P)]
+
+
+class SxOctree(C.Structure):
+    _fields_ = [("prefixes", _P), ("childOffsets", _P), ("parents", _P), ("levelRange", _P),
+                ("internalToLeaf", _P), ("leafToInternal", _P)]
+
+
+class SxNbStats(C.Structure):
+    _fields_ = [("sumNeighbors", C.c_uint64), ("maxNeighbors", C.c_uint32), ("numFailed", C.c_uint32),
+                ("sumCandidates", C.c_uint64)]
+
+
+# field dtypes (sph::SphTypes, sph/types.hpp:39-46)
+DTYPES = {k: np.float32 for k, _ in FIELD_ORDER}
+DTYPES.update(x=np.float64, y=np.float64, z=np.float64, u=np.float64, du=np.float64, temp=np.float64,
+              keys=np.uint64, nc=np.uint32, rung=np.uint8)
+
+_lib = None
+
+
+def header_symbols():
+    """every sx_* function declared in include/sphexa_hip.h"""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sx_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} not built (run __graft_entry__.build() or make -C sph-exa_amd)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u32, sz = C.c_void_p, C.c_int32, C.c_uint32, C.c_size_t
+    sig = {
+        "sx_create": (C.c_int, [C.POINTER(vp), C.c_int]),
+        "sx_destroy": (None, [vp]),
+        "sx_set_stream": (C.c_int, [vp, vp]),
+        "sx_get_stream": (vp, [vp]),
+        "sx_last_error": (C.c_char_p, [vp]),
+        "sx_set_exact": (C.c_int, [vp, C.c_int]),
+        "sx_kernel_constant": (C.c_double, []),
+        "sx_copy_tables": (C.c_int, [vp, vp, vp]),
+        "sx_synchronize": (C.c_int, [vp]),
+        "sx_device_alloc": (vp, [vp, sz]),
+        "sx_device_free": (C.c_int, [vp, vp]),
+        "sx_memcpy": (C.c_int, [vp, vp, vp, sz, C.c_int]),
+        "sx_memset": (C.c_int, [vp, vp, C.c_int, sz]),
+        "sx_sfc_keys": (C.c_int, [vp, vp, vp, vp, vp, sz, C.POINTER(SxBox)]),
+        "sx_sort_keys": (C.c_int, [vp, vp, vp, sz]),
+        "sx_gather": (C.c_int, [vp, vp, sz, vp, vp, C.c_int]),
+        "sx_compute_octree": (C.c_int, [vp, vp, sz, u32, vp, vp, i32, C.POINTER(i32)]),
+        "sx_build_octree": (C.c_int, [vp, vp, i32, C.POINTER(SxOctree)]),
+        "sx_node_centers": (C.c_int, [vp, vp, i32, C.POINTER(SxBox), vp, vp]),
+        "sx_leaf_layout": (C.c_int, [vp, vp, i32, vp]),
+        "sx_compute_groups": (C.c_int, [vp, u32, u32, C.POINTER(SxGroups)]),
+        "sx_find_neighbors": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.POINTER(SxBox),
+                                        C.POINTER(SxParams), u32, u32, C.c_int, C.POINTER(SxNbStats)]),
+        "sx_export_neighbors": (C.c_int, [vp, vp, u32, u32, u32, vp]),
+        "sx_import_neighbors": (C.c_int, [vp, u32, u32, u32, vp]),
+        "sx_xmass": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams), C.POINTER(SxBox),
+                               C.POINTER(SxTree)]),
+        "sx_xmass_only": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                    C.POINTER(SxBox)]),
+        "sx_ve_def_gradh": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                      C.POINTER(SxBox)]),
+        "sx_eos": (C.c_int, [vp, u32, u32, C.c_float, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "sx_iad_divv_curlv": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                        C.POINTER(SxBox)]),
+        "sx_av_switches": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                     C.POINTER(SxBox), C.c_double]),
+        "sx_momentum_energy": (C.c_int, [vp, C.POINTER(SxGroups), vp, C.POINTER(SxFields), C.POINTER(SxParams),
+                                         C.POINTER(SxBox), C.POINTER(C.c_float)]),
+        "sx_positions": (C.c_int, [vp, u32, u32, C.c_double, C.c_double, C.POINTER(SxFields), C.c_double,
+                                   C.c_float, C.POINTER(SxBox)]),
+        "sx_update_h": (C.c_int, [vp, u32, u32, u32, vp, vp]),
+        "sx_max_divv": (C.c_int, [vp, u32, u32, vp, C.POINTER(C.c_float)]),
+        "sx_sim_create": (C.c_int, [C.POINTER(vp), vp, sz, C.POINTER(SxParams), C.POINTER(SxBox), u32]),
+        "sx_sim_destroy": (None, [vp]),
+        "sx_sim_init_sedov": (C.c_int, [vp, u32]),
+        "sx_sim_set_state": (C.c_int, [vp, sz] + [vp] * 15 + [C.c_double, C.c_double]),
+        "sx_sim_fields": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(vp)]),
+        "sx_sim_size": (sz, [vp]),
+        "sx_sim_step": (C.c_int, [vp]),
+        "sx_sim_scalars": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "sx_sim_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
+        "sx_sim_last_stats": (C.c_int, [vp, C.POINTER(SxNbStats)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def default_params(K=None, ngmax=150, ng0=100):
+    """ParticlesData defaults (particles_data.hpp:86-138)."""
+    if K is None:
+        K = lib().sx_kernel_constant()
+    return SxParams(K=K, ng0=ng0, ngmax=ngmax, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0, alphamin=0.05,
+                    alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
+                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1)
+
+
+def make_box(lim, bnd):
+    b = SxBox()
+    for k in range(6):
+        b.lim[k] = float(lim[k])
+    for k in range(3):
+        b.bnd[k] = int(bnd[k])
+    return b
+
+
+class SxError(RuntimeError):
+    pass
+
+
+class Context:
+    def __init__(self, device=0, exact=False):
+        self.L = lib()
+        self.h = C.c_void_p()
+        rc = self.L.sx_create(C.byref(self.h), device)
+        self.check(rc, "sx_create")
+        self.L.sx_set_exact(self.h, 1 if exact else 0)
+        self.allocs = []
+
+    def check(self, rc, what=""):
+        if rc != SX_OK:
+            msg = self.L.sx_last_error(self.h) if self.h else b"?"
+            raise SxError(f"{what}: code {rc}: {msg.decode() if msg else ''}")
+
+    def set_exact(self, exact):
+        self.L.sx_set_exact(self.h, 1 if exact else 0)
+
+    # ---- device arrays --------------------------------------------------------------------------------------
+    def alloc(self, n, dtype):
+        nbytes = int(n) * np.dtype(dtype).itemsize
+        p = self.L.sx_device_alloc(self.h, nbytes)
+        if not p:
+            raise SxError("device alloc failed")
+        self.allocs.append(p)
+        return DeviceArray(self, p, int(n), dtype)
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        d = self.alloc(arr.size, arr.dtype)
+        self.check(self.L.sx_memcpy(self.h, d.ptr, arr.ctypes.data, arr.nbytes, 1), "upload")
+        return d
+
+    def free_all(self):
+        for p in self.allocs:
+            self.L.sx_device_free(self.h, p)
+        self.allocs = []
+
+    def close(self):
+        self.free_all()
+        if self.h:
+            self.L.sx_destroy(self.h)
+            self.h = None
+
+    def sync(self):
+        self.check(self.L.sx_synchronize(self.h), "sync")
+
+
+class DeviceArray:
+    def __init__(self, ctx, ptr, n, dtype):
+        self.ctx, self.ptr, self.n, self.dtype = ctx, ptr, n, np.dtype(dtype)
+
+    def get(self):
+        out = np.empty(self.n, self.dtype)
+        self.ctx.check(self.ctx.L.sx_memcpy(self.ctx.h, out.ctypes.data, self.ptr, out.nbytes, 2), "download")
+        return out
+
+    def set(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=self.dtype)
+        assert arr.size == self.n
+        self.ctx.check(self.ctx.L.sx_memcpy(self.ctx.h, self.ptr, arr.ctypes.data, arr.nbytes, 1), "upload")
+
+
+class DeviceState:
+    """A full ParticlesData-like device field set built from a host dict of numpy arrays."""
+
+    def __init__(self, ctx, host):
+        self.ctx = ctx
+        n = len(host["x"])
+        self.n = n
+        self.dev = {}
+        self.fields = SxFields()
+        self.fields.n = n
+        for name, _ in FIELD_ORDER:
+            if name in ("rho", "p", "tdpdTrho", "u", "mue", "mui", "cv", "dV11", "dV12", "dV13", "dV22", "dV23",
+                        "dV33", "markRamp", "rung"):
+                continue
+            dt = DTYPES[name]
+            if name in host:
+                d = ctx.upload(np.asarray(host[name], dtype=dt))
+            else:
+                d = ctx.alloc(n, dt)
+                ctx.L.sx_memset(ctx.h, d.ptr, 0, n * np.dtype(dt).itemsize)
+            self.dev[name] = d
+            setattr(self.fields, name, d.ptr)
+
+    def get(self, name):
+        return self.dev[name].get()
+
+    def set(self, name, arr):
+        self.dev[name].set(arr)
+
+
+class Sim:
+    """device-resident VE propagator on one GPU (sx_sim_*)"""
+
+    def __init__(self, ctx, capacity, box, params=None, bucket=64):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.params = params or default_params()
+        self.box = box
+        self.h = C.c_void_p()
+        ctx.check(self.L.sx_sim_create(C.byref(self.h), ctx.h, int(capacity), C.byref(self.params), C.byref(box),
+                                       bucket), "sx_sim_create")
+
+    def init_sedov(self, side):
+        self.ctx.check(self.L.sx_sim_init_sedov(self.h, side), "init_sedov")
+
+    def set_state(self, st, minDt=1e-6, minDt_m1=1e-6):
+        arrs = [np.ascontiguousarray(st[k], dtype=t) for k, t in [
+            ("x", np.float64), ("y", np.float64), ("z", np.float64), ("h", np.float32), ("m", np.float32),
+            ("temp", np.float64), ("vx", np.float32), ("vy", np.float32), ("vz", np.float32), ("x_m1", np.float32),
+            ("y_m1", np.float32), ("z_m1", np.float32), ("du_m1", np.float32), ("alpha", np.float32),
+            ("id", np.uint64)]]
+        self._keep = arrs
+        self.ctx.check(self.L.sx_sim_set_state(self.h, arrs[0].size, *[a.ctypes.data for a in arrs],
+                                               float(minDt), float(minDt_m1)), "set_state")
+
+    def step(self):
+        rc = self.L.sx_sim_step(self.h)
+        if rc != SX_OK:
+            raise SxError(f"sx_sim_step failed with code {rc}")
+
+    def size(self):
+        return self.L.sx_sim_size(self.h)
+
+    def scalars(self):
+        out = (C.c_double * 5)()
+        self.ctx.check(self.L.sx_sim_scalars(self.h, out), "scalars")
+        return dict(zip(["minDt", "minDt_m1", "ttot", "minDtCourant", "minDtRho"], list(out)))
+
+    def fields(self):
+        f = SxFields()
+        idp = C.c_void_p()
+        self.L.sx_sim_fields(self.h, C.byref(f), C.byref(idp))
+        return f, idp.value
+
+    def get(self, names):
+        f, idp = self.fields()
+        n = self.size()
+        out = {}
+        for name in names:
+            ptr = idp if name == "id" else getattr(f, name)
+            dt = np.uint64 if name == "id" else DTYPES[name]
+            out[name] = DeviceArray(self.ctx, ptr, n, dt).get()
+        return out
+
+    def stage_times(self):
+        ms = (C.c_float * 16)()
+        names = (C.c_char_p * 16)()
+        k = self.L.sx_sim_stage_times(self.h, ms, 16, names)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def stats(self):
+        s = SxNbStats()
+        self.L.sx_sim_last_stats(self.h, C.byref(s))
+        return dict(sumNeighbors=s.sumNeighbors, maxNeighbors=s.maxNeighbors, numFailed=s.numFailed,
+                    sumCandidates=s.sumCandidates)
+
+    def close(self):
+        if self.h:
+            self.L.sx_sim_destroy(self.h)
+            self.h = None

@@ -1,0 +1,326 @@
+"""GPU parity: libsphexa_hip.so (through the C-ABI) against the CPU oracle and the reference fixtures.
+
+Integer / index work is bit-exact: Hilbert keys, sort order, cornerstone leaves and counts, every linked-octree
+array, node geometry, neighbor counts, neighbor SETS and h after the h-nc iteration.
+Float kernels:
+  * exact variant (no FMA) fed the reference's own neighbor list (same order) -> bit-identical to the reference;
+  * fast variant (FMA) -> rtol 2e-5 per element + 1e-6 of the field's max (float32 rounding of ~100-term sums);
+  * full VE steps (own neighbor search => different summation order) -> nc/h/id exact after step 1, floats within
+    rtol 1e-4 + 1e-5*max, energy conservation 1e-6 relative.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+import gpu_util as gutil
+import pyoracle as po
+import sphexa_amd as sx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sx.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return po.load_oracle()
+
+
+def rand_state(n, seed, clustered=True):
+    rng = np.random.default_rng(seed)
+    st = po.HostState(n)
+    st.x[:] = rng.uniform(-0.5, 0.5, n)
+    st.y[:] = rng.uniform(-0.5, 0.5, n)
+    st.z[:] = np.clip(rng.normal(0, 0.12, n), -0.5, 0.4999) if clustered else rng.uniform(-0.5, 0.5, n)
+    return st
+
+
+# ---- cstone: keys, sort, tree ---------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("case", ["lattice", "clustered", "uniform"])
+@pytest.mark.parametrize("bucket", [64, 16, 1])
+def test_keys_sort_tree_exact(ctx, ora, case, bucket):
+    if case == "lattice":
+        st, obox = po.sedov_state(24)
+    else:
+        st = rand_state(30000, 11, clustered=(case == "clustered"))
+        obox = po.make_box(-0.5, 0.5, True)
+    box = gutil.box_to_sx(obox)
+    n = st.n
+    x, y, z = ctx.upload(st.x), ctx.upload(st.y), ctx.upload(st.z)
+    keys = ctx.alloc(n, np.uint64)
+    ctx.check(ctx.L.sx_sfc_keys(ctx.h, x.ptr, y.ptr, z.ptr, keys.ptr, n, C.byref(box)), "keys")
+    ref_keys = ora.sfc_keys(st, obox).copy()
+    assert np.array_equal(keys.get(), ref_keys)
+    order = ctx.alloc(n, np.uint32)
+    ctx.check(ctx.L.sx_sort_keys(ctx.h, keys.ptr, order.ptr, n), "sort")
+    assert np.array_equal(order.get(), np.argsort(ref_keys, kind="stable"))
+    skeys = np.sort(ref_keys)
+    assert np.array_equal(keys.get(), skeys)
+    tree, host = gutil.device_tree(ctx, keys, n, bucket, box)
+    ref = ora.octree(skeys, bucket)
+    for k in ["leaves", "counts", "prefixes", "childOffsets", "parents", "levelRange", "internalToLeaf",
+              "leafToInternal"]:
+        assert np.array_equal(host[k], ref[k]), k
+    c, s = ora.node_centers(ref["prefixes"], obox)
+    assert np.array_equal(host["centers"], c) and np.array_equal(host["sizes"], s)
+    assert np.array_equal(host["layout"][:-1], np.concatenate([[0], np.cumsum(ref["counts"])[:-1]]))
+    ctx.free_all()
+
+
+def test_gather(ctx):
+    rng = np.random.default_rng(3)
+    n = 100003
+    order = rng.permutation(n).astype(np.uint32)
+    o = ctx.upload(order)
+    for dt in (np.uint8, np.float32, np.float64):
+        src = (rng.standard_normal(n) * 100).astype(dt)
+        s, d = ctx.upload(src), ctx.alloc(n, dt)
+        ctx.check(ctx.L.sx_gather(ctx.h, o.ptr, n, s.ptr, d.ptr, np.dtype(dt).itemsize), "gather")
+        assert np.array_equal(d.get(), src[order])
+    ctx.free_all()
+
+
+# ---- neighbor search ------------------------------------------------------------------------------------------
+
+def run_neighbors(ctx, ora, st, obox, bucket, iterate, h0, ngmax=150):
+    box = gutil.box_to_sx(obox)
+    n = st.n
+    st.h[:] = h0
+    ds = sx.DeviceState(ctx, gutil.host_dict(st))
+    tree, _ = gutil.device_tree(ctx, ds.dev["keys"], n, bucket, box)
+    p = sx.default_params(ngmax=ngmax)
+    stats = sx.SxNbStats()
+    rc = ctx.L.sx_find_neighbors(ctx.h, C.byref(ds.fields), C.byref(tree), C.byref(box), C.byref(p), 0, n,
+                                 int(iterate), C.byref(stats))
+    assert rc in (sx.SX_OK, sx.SX_ERR_NOT_CONVERGED), ctx.L.sx_last_error(ctx.h)
+    nc = ds.get("nc")
+    h = ds.get("h")
+    out = ctx.alloc(n * ngmax, np.uint32)
+    ctx.check(ctx.L.sx_export_neighbors(ctx.h, ds.dev["nc"].ptr, 0, n, ngmax, out.ptr), "export")
+    nbr = out.get()
+    # oracle on the same inputs
+    st.h[:] = h0
+    rn, rnc = ora.find_neighbors(st, obox, bucket=bucket, iterate_h=iterate, ngmax=ngmax)
+    return nc, h, nbr, rn, rnc, st.h.copy(), stats
+
+
+@pytest.mark.parametrize("periodic", [True, False])
+@pytest.mark.parametrize("iterate", [False, True])
+def test_neighbors_exact_random(ctx, ora, periodic, iterate):
+    st = rand_state(20000, 5)
+    obox = po.make_box(-0.5, 0.5, periodic)
+    gutil.sorted_state(st, obox, ora)
+    h0 = np.float32(0.02) * (1 + 0.5 * np.sin(st.x * 13)).astype(np.float32)
+    nc, h, nbr, rn, rnc, rh, stats = run_neighbors(ctx, ora, st, obox, 32, iterate, h0)
+    if iterate:
+        assert np.array_equal(h, rh)
+        assert np.array_equal(nc, rnc)
+    else:
+        assert np.array_equal(nc - 1, rnc)
+        rnc = rnc + 1
+    a = gutil.rows_sorted(nbr, nc, 150)
+    b = gutil.rows_sorted(rn, rnc, 150)
+    full = [i for i in range(st.n) if nc[i] - 1 <= 150]
+    assert all(np.array_equal(a[i], b[i]) for i in full)
+    ctx.free_all()
+
+
+@pytest.mark.parametrize("side", [16, 30])
+def test_neighbors_exact_sedov_lattice(ctx, ora, side):
+    st, obox = po.sedov_state(side)
+    gutil.sorted_state(st, obox, ora)
+    nc, h, nbr, rn, rnc, rh, stats = run_neighbors(ctx, ora, st, obox, 64, True, st.h.copy())
+    assert np.array_equal(h, rh) and np.array_equal(nc, rnc)
+    a = gutil.rows_sorted(nbr, nc, 150)
+    b = gutil.rows_sorted(rn, rnc, 150)
+    assert all(np.array_equal(a[i], b[i]) for i in range(st.n))
+    assert stats.numFailed == 0 and stats.maxNeighbors == int(nc.max()) - 1
+    ctx.free_all()
+
+
+def test_neighbors_edge_cases(ctx, ora):
+    """tiny and ragged inputs: one particle, fewer particles than a wave, a ragged last block, duplicates"""
+    for n in (1, 7, 65, 130):
+        st = rand_state(n, 100 + n, clustered=False)
+        if n == 130:
+            st.x[5], st.y[5], st.z[5] = st.x[4], st.y[4], st.z[4]  # coincident particles (d2 == 0, j != i)
+        obox = po.make_box(-0.5, 0.5, True)
+        gutil.sorted_state(st, obox, ora)
+        nc, h, nbr, rn, rnc, rh, _ = run_neighbors(ctx, ora, st, obox, 4, False, np.full(n, 0.2, np.float32))
+        assert np.array_equal(nc - 1, rnc)
+        a = gutil.rows_sorted(nbr, nc, 150)
+        b = gutil.rows_sorted(rn, rnc + 1, 150)
+        assert all(np.array_equal(a[i], b[i]) for i in range(n))
+    ctx.free_all()
+
+
+# ---- per-kernel parity on the reference's own neighbor list ---------------------------------------------------
+
+def kernel_chain(ctx, d, exact):
+    """run the VE kernels on fixture kernels.npz inputs with the reference neighbor list imported"""
+    ctx.set_exact(exact)
+    box = gutil.box_to_sx(gu.box_from(d["box"]))
+    st = gu.state_from(d, "in_")
+    n = st.n
+    host = gutil.host_dict(st)
+    host["h"] = d["h_after_iter"]
+    host["nc"] = d["nc"]
+    ds = sx.DeviceState(ctx, host)
+    p = sx.default_params()
+    nb = ctx.upload(d["nbr"])
+    ctx.check(ctx.L.sx_import_neighbors(ctx.h, 0, n, 150, nb.ptr), "import")
+    g = sx.SxGroups(firstBody=0, lastBody=n, numGroups=(n + 63) // 64)
+    L, h = ctx.L, ctx.h
+    out = {}
+    ctx.check(L.sx_xmass_only(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box)), "xmass")
+    out["xm"] = ds.get("xm")
+    ctx.check(L.sx_ve_def_gradh(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box)), "gradh")
+    out["kx"], out["gradh"] = ds.get("kx"), ds.get("gradh")
+    f = ds.fields
+    ctx.check(L.sx_eos(h, 0, n, 10.0, 5.0 / 3.0, f.temp, f.m, f.kx, f.xm, f.gradh, f.prho, f.c, None, None), "eos")
+    out["prho"], out["c"] = ds.get("prho"), ds.get("c")
+    ctx.check(L.sx_iad_divv_curlv(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box)), "iad")
+    for k in ["c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv"]:
+        out[k] = ds.get(k)
+    ctx.check(L.sx_av_switches(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box), float(st.minDt)), "av")
+    out["alpha"] = ds.get("alpha")
+    mdt = C.c_float()
+    ctx.check(L.sx_momentum_energy(h, C.byref(g), None, C.byref(ds.fields), C.byref(p), C.byref(box),
+                                   C.byref(mdt)), "momentum")
+    out["minDtCourant"] = np.array([mdt.value])
+    for k in ["du", "ax", "ay", "az"]:
+        out[k] = ds.get(k)
+    ctx.set_exact(False)
+    return out
+
+
+KERNEL_OUT = ["xm", "kx", "gradh", "prho", "c", "c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv", "alpha",
+              "du", "ax", "ay", "az", "minDtCourant"]
+
+
+def test_kernels_exact_variant_bitwise(ctx):
+    d = gu.load("kernels.npz")
+    out = kernel_chain(ctx, d, exact=True)
+    for k in KERNEL_OUT:
+        ref = d[k].astype(out[k].dtype)
+        assert np.array_equal(out[k], ref), (k, np.max(np.abs(out[k].astype(float) - ref)))
+    ctx.free_all()
+
+
+def test_kernels_fast_variant_tolerance(ctx):
+    d = gu.load("kernels.npz")
+    out = kernel_chain(ctx, d, exact=False)
+    for k in KERNEL_OUT:
+        ok, info = gutil.close(out[k], d[k], rtol=2e-5, atol_frac=1e-6)
+        assert ok, (k, info)
+    ctx.free_all()
+
+
+def test_xmass_with_own_search_matches_reference(ctx, ora):
+    """sx_xmass = search + h iteration + xm (computeXMass semantics): nc and h exact, xm within float tolerance"""
+    d = gu.load("kernels.npz")
+    box = gutil.box_to_sx(gu.box_from(d["box"]))
+    st = gu.state_from(d, "in_")
+    n = st.n
+    ds = sx.DeviceState(ctx, gutil.host_dict(st))
+    tree, _ = gutil.device_tree(ctx, ds.dev["keys"], n, 64, box)
+    p = sx.default_params()
+    g = sx.SxGroups(firstBody=0, lastBody=n, numGroups=(n + 63) // 64)
+    ctx.check(ctx.L.sx_xmass(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box), C.byref(tree)), "xm")
+    assert np.array_equal(ds.get("nc"), d["nc"])
+    assert np.array_equal(ds.get("h"), d["h_after_iter"])
+    ok, info = gutil.close(ds.get("xm"), d["xm"], rtol=2e-6)
+    assert ok, info
+    ctx.free_all()
+
+
+# ---- full VE steps --------------------------------------------------------------------------------------------
+
+FLOATS = ["x", "y", "z", "vx", "vy", "vz", "temp", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "xm", "kx", "prho",
+          "c", "divv", "c11", "c22", "c33", "du", "ax", "ay", "az"]
+
+
+def compare_state(got, ref, strict_discrete, rtol=1e-4, atol_frac=1e-5):
+    order_g = np.argsort(got["id"])
+    order_r = np.argsort(ref.id)
+    if strict_discrete:
+        assert np.array_equal(got["nc"][order_g], ref.nc[order_r])
+        assert np.array_equal(got["h"][order_g], ref.h[order_r])
+    else:
+        assert np.mean(got["nc"][order_g] == ref.nc[order_r]) > 0.999
+    for k in FLOATS:
+        ok, info = gutil.close(got[k][order_g], ref.arrays[k][order_r], rtol, atol_frac)
+        assert ok, (k, info)
+
+
+@pytest.mark.parametrize("ic,side,steps", [("sedov", 16, 3), ("noh", 16, 3)])
+def test_full_steps_vs_oracle(ctx, ora, ic, side, steps):
+    st, obox = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
+    box = gutil.box_to_sx(obox)
+    sim = sx.Sim(ctx, st.n, box)
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    ref = st.copy()
+    for s in range(steps):
+        sim.step()
+        ora.step(ref, obox)
+        got = sim.get(["id", "nc", "h"] + FLOATS)
+        compare_state(got, ref, strict_discrete=(s == 0))
+        sc = sim.scalars()
+        assert sc["minDt"] == pytest.approx(ref.minDt, rel=1e-5)
+        assert sc["ttot"] == pytest.approx(ref.ttot, rel=1e-5)
+    sim.close()
+
+
+def test_golden_fixture_steps(ctx):
+    d = gu.load("sedov10.npz")
+    obox = gu.box_from(d["box"])
+    st = gu.state_from(d, "s0_")
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    for s in (1, 2, 3):
+        sim.step()
+        ref = gu.state_from(d, f"s{s}_")
+        got = sim.get(["id", "nc", "h"] + FLOATS)
+        compare_state(got, ref, strict_discrete=(s == 1))
+    sim.close()
+
+
+def test_sedov_n50_energy_and_counts(ctx, ora):
+    """BASELINE config 1 size (n=50, 1.25e5 particles): one step vs the oracle, then energy conservation."""
+    st, obox = po.sedov_state(50)
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    e0 = po.total_energy(st)
+    ref = st.copy()
+    sim.step()
+    ora.step(ref, obox)
+    got = sim.get(["id", "nc", "h"] + FLOATS)
+    compare_state(got, ref, strict_discrete=True)
+    assert int(np.round(np.mean(got["nc"]))) == 94  # 93 neighbors + self on the lattice
+    for _ in range(4):
+        sim.step()
+    g = sim.get(["vx", "vy", "vz", "temp", "m"])
+    hs = po.HostState(st.n)
+    for k in ("vx", "vy", "vz", "temp", "m"):
+        hs.arrays[k][:] = g[k]
+    assert abs(po.total_energy(hs) / e0 - 1) < 1e-6
+    sim.close()
+
+
+def test_device_sedov_ic_matches_numpy(ctx):
+    st, obox = po.sedov_state(20)
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.init_sedov(20)
+    got = sim.get(["x", "y", "z", "h", "m", "temp", "alpha", "id"])
+    for k in ("x", "y", "z", "h", "m", "alpha", "id"):
+        assert np.array_equal(got[k], st.arrays[k]), k
+    assert np.allclose(got["temp"], st.temp, rtol=4e-16, atol=0)
+    sim.close()
