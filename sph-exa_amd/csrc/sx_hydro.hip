@@ -26,9 +26,8 @@ constexpr int kBlock = 256;
 #define SX_PAIR_PROLOGUE                                                                                               \
     const uint32_t gw   = (blockIdx.x * kBlock + threadIdx.x) >> 6;                                                    \
     const uint32_t lane = threadIdx.x & 63;                                                                            \
-    if (gw >= a.numGroups) return;                                                                                     \
     const uint32_t i     = a.first + gw * kGroupSize + lane;                                                           \
-    const bool     valid = i < a.last;                                                                                 \
+    const bool     valid = gw < a.numGroups && i < a.last; /* no early return: momentum has a block barrier */     \
     unsigned       cnt   = 0;                                                                                          \
     if (valid)                                                                                                         \
     {                                                                                                                  \
@@ -375,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
     }
     // wave min -> block min -> one atomic per block (momentum_energy_gpu.cu:94-118)
     float wmin = waveMin(dt_lane);
-    if (a.groupDt != nullptr && lane == 0)
+    if (a.groupDt != nullptr && lane == 0 && gw < a.numGroups)
     {
         float old = a.groupDt[gw];
         a.groupDt[gw] = wmin < old ? wmin : old;
