@@ -111,6 +111,16 @@ __host__ __device__ __forceinline__ float idealGasCv(float mui, double gamma)
     return (float)((double)(R / mui) / (gamma - 1.0f));
 }
 
+/*! XCD-aware block remap (HIP guide 5.5 T1): workgroups are dealt round-robin to the 8 XCDs (block b -> XCD b%8),
+ *  so consecutive SFC blocks would land on different L2s and every XCD would stream the whole active window.
+ *  This bijection gives XCD x a contiguous range of logical blocks, processed in order, so the neighbor records a
+ *  block gathers are mostly already in that XCD's 4 MB L2. Placement only affects speed, never results. */
+__device__ __forceinline__ uint32_t xcdBlock(uint32_t b, uint32_t nb)
+{
+    const uint32_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return (x < r) ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 // ---- wave64 reductions (cross-lane through DPP/ds_swizzle via __shfl_xor) ----------------------------------
 
 template<class T>

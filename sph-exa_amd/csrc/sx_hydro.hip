@@ -24,7 +24,7 @@ namespace SX_VARIANT
 constexpr int kBlock = 256;
 
 #define SX_PAIR_PROLOGUE                                                                                               \
-    const uint32_t gw   = (blockIdx.x * kBlock + threadIdx.x) >> 6;                                                    \
+    const uint32_t gw   = (xcdBlock(blockIdx.x, gridDim.x) * kBlock + threadIdx.x) >> 6;                               \
     const uint32_t lane = threadIdx.x & 63;                                                                            \
     const uint32_t i     = a.first + gw * kGroupSize + lane;                                                           \
     const bool     valid = gw < a.numGroups && i < a.last; /* no early return: momentum has a block barrier */     \

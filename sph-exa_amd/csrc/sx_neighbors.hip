@@ -40,7 +40,7 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
 
     const int      wave = threadIdx.x >> 6;
     const int      lane = threadIdx.x & 63;
-    const uint32_t g    = blockIdx.x * kNsWaves + wave;
+    const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * kNsWaves + wave;
     if (g >= a.numGroups) return;
     int* queue = s_queue[wave];
     int* cand  = s_cand[wave];
