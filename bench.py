@@ -34,6 +34,7 @@ def parse():
     ap.add_argument("--bucket", type=int, default=64)
     ap.add_argument("--exact", action="store_true", help="use the no-FMA (bit-reproducible) kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="rccl", help="rccl (one GPU per rank) or host (staged, tests)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
 
@@ -82,14 +83,17 @@ def main():
     import sphexa_amd as sx
 
     side = args.side or int(round(200 * n_gpus ** (1.0 / 3.0)))
-    ctx = sx.Context(local, exact=args.exact)
+    n_total = side ** 3
+    ctx = sx.Context(0 if args.backend == "host" else local, exact=args.exact)
     box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
-    # interim multi-GPU: each rank runs the side^3/N share as an independent periodic replica
-    rank_side = side if world == 1 else int(round(side / world ** (1.0 / 3.0)))
-    n_local = rank_side ** 3
-    sim = sx.Sim(ctx, n_local, box, bucket=args.bucket)
-    sim.init_sedov(rank_side)
-
+    # capacity: the rank's share plus halos (surface layer of the SFC domain) with headroom
+    cap = n_total if world == 1 else int(1.6 * n_total / world) + 65536
+    sim = sx.Sim(ctx, cap, box, bucket=args.bucket)
+    comm = None
+    if world > 1:
+        comm = sx.Comm(args.backend)
+        sim.set_comm(comm)
+    sim.init_sedov(side, rank, world)
     for _ in range(args.warmup):
         sim.step()
 
@@ -115,7 +119,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = sim.stats()
-    n_total = n_local * world
+    n_local = sim.size()
     ms_step = el / args.steps * 1e3
     ng = stats["sumNeighbors"] / max(1, n_local)
     mom_ms = stage_sum.get("MomentumEnergy", float("nan")) / args.steps
@@ -137,7 +141,9 @@ def main():
         "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint",
         "config": {"workload": f"Sedov -n {side} ({side ** 3} particles), VE propagator, {args.steps} steps",
                    "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
-                   "parallelism": "1 GPU" if world == 1 else f"{world} independent replicas (interim)",
+                   "parallelism": "1 GPU" if world == 1 else
+                   f"{world} GPUs: SFC domain decomposition, RCCL halo + particle exchange ({args.backend})",
+                   "halos_per_gpu": sim.layout()["n"] - n_local,
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
         "roofline": {"bound": "hbm", "kernel": "momentumEnergyKernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -151,6 +157,8 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     sim.close()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if rank == 0:
         print(json.dumps(out))

@@ -223,6 +223,20 @@ int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double d
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
 int sx_max_divv(sx_ctx* ctx, uint32_t first, uint32_t last, const float* divv, float* maxDivv);
 
+/* ---- multi-GPU transport (replaces the reference's MPI calls, see sph-exa_amd/csrc/sx_comm.hpp) ---------- */
+typedef struct sx_comm sx_comm;
+/*! host-staged collectives supplied by the caller (e.g. torch.distributed gloo): buffers are host memory,
+ *  send/recv segments contiguous in rank order; return 0 on success. op: 0 = u32 sum, 1 = f64 min. */
+typedef int (*sx_alltoallv_cb)(void* user, const void* sendHost, const uint64_t* sendBytes, void* recvHost,
+                               const uint64_t* recvBytes);
+typedef int (*sx_allreduce_cb)(void* user, void* bufHost, uint64_t count, int op);
+/*! RCCL unique id (128 bytes) created on rank 0 and broadcast by the caller's control plane */
+int  sx_comm_unique_id(void* id128);
+/*! RCCL communicator over the node's GPUs (the calling process must have selected its device via sx_create) */
+int  sx_comm_create_rccl(sx_comm** comm, int rank, int size, const void* id128);
+int  sx_comm_create_host(sx_comm** comm, int rank, int size, sx_alltoallv_cb a2a, sx_allreduce_cb ar, void* user);
+void sx_comm_destroy(sx_comm* comm);
+
 /* ---- device-resident simulation: one HydroVeProp step per call ----------------------------------------- */
 typedef struct sx_sim sx_sim;
 /*! Sedov lattice (sedov_init.hpp:48-130) of side^3 particles; with nranks > 1 only this rank's SFC share. */
@@ -230,6 +244,15 @@ int    sx_sim_create(sx_sim** sim, sx_ctx* ctx, size_t capacity, const sx_params
                      uint32_t bucketSize);
 void   sx_sim_destroy(sx_sim* sim);
 int    sx_sim_init_sedov(sx_sim* sim, uint32_t side);
+/*! distribute the step over a communicator: SFC assignment by a global key histogram (all ranks equal counts),
+ *  particle exchange, halo discovery and the reference's five halo exchanges per step
+ *  (ve_hydro.hpp:150-186), global time-step min.  rank/size come from the communicator. */
+int    sx_sim_set_comm(sx_sim* sim, sx_comm* comm);
+/*! this rank's share of a Sedov lattice of side^3 particles (contiguous lattice-index slab; the first step's
+ *  sync moves particles to their SFC owner) */
+int    sx_sim_init_sedov_rank(sx_sim* sim, uint32_t side, int rank, int size);
+/*! local particle range [first,last) and total (with halos) of the last step */
+int    sx_sim_layout(sx_sim* sim, uint64_t out[4]);
 /*! upload a host state (conserved fields, length n) */
 int    sx_sim_set_state(sx_sim* sim, size_t n, const double* x, const double* y, const double* z, const float* h,
                         const float* m, const double* temp, const float* vx, const float* vy, const float* vz,

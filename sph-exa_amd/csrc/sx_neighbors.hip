@@ -6,12 +6,11 @@
  *
  * Per block (wave):
  *   1. wave reductions give the block's bounding box and max h;
- *   2. a wave-cooperative BFS over the linked octree (8 nodes x 8 children = 64 lanes per step, queue and
- *      candidate-leaf list in LDS) collects every leaf whose geometric box comes within 2*hmax of the block box
- *      (minimum-image folding on periodic axes, box inflated by the key-quantisation margin);
- *   3. each candidate leaf's particles (a contiguous SFC range) are loaded coalesced, one per lane, and
- *      broadcast lane by lane with v_readlane: every lane tests the candidate against its own particle with the
- *      reference CPU criterion, in double, without FMA contraction (this file is compiled -ffp-contract=off):
+ *   2. waveCollectLeaves (sx_traverse.hpp) gathers every leaf whose geometric box comes within 2*hmax of the
+ *      block box (minimum image on periodic axes, inflated by the key-quantisation margin);
+ *   3. each candidate leaf's particles (a contiguous SFC range) are loaded coalesced, one per lane, and broadcast
+ *      lane by lane with v_readlane: every lane tests the candidate against its own particle with the reference CPU
+ *      criterion, in double, without FMA contraction (this file is compiled -ffp-contract=off):
  *          d2 = dx*dx + dy*dy + dz*dz  <  (double)(4.0f*h*h),   j != i,
  *      dx folded with rint() on periodic axes when the particle is within 2h of the box edge (findneighbors.hpp:118);
  *      hits are appended to the lane-interleaved list nidx[(block*ngmax + k)*64 + lane] (k < ngmax, counting on);
@@ -19,19 +18,13 @@
  *      updates per lane (the CPU loop's `iteration++ < 10`), so h, nc and the neighbor SET are identical to the
  *      CPU reference.
  */
+#include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
 namespace sx
 {
 
-constexpr int kNsWaves = 4;    // waves per workgroup
-constexpr int kQCap    = 512;  // internal-node ring per wave
-constexpr int kCCap    = 2048; // candidate leaves per wave
-
-__device__ __forceinline__ double foldPbc(double d, const DevBox& b, int k)
-{
-    return d - (double)b.pbc[k] * b.l[k] * rint(d * b.il[k]);
-}
+constexpr int kNsWaves = 4; // waves per workgroup
 
 __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
 {
@@ -41,7 +34,7 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
     const int      wave = threadIdx.x >> 6;
     const int      lane = threadIdx.x & 63;
     const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * kNsWaves + wave;
-    if (g >= a.numGroups) return;
+    if (g >= a.numGroups) return; // whole wave, no block barrier in this kernel
     int* queue = s_queue[wave];
     int* cand  = s_cand[wave];
 
@@ -53,11 +46,10 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
 
     uint32_t* nlist = a.nidx + (size_t)g * a.ngmax * kWave + lane;
 
-    const uint64_t ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const unsigned ngmin  = a.ng0 / 4;
-    int            iteration = 0;
-    bool           active    = valid;
-    unsigned       count     = 0;
+    const unsigned     ngmin      = a.ng0 / 4;
+    int                iteration  = 0;
+    bool               active     = valid;
+    unsigned           count      = 0;
     unsigned long long candTested = 0;
 
     // block bounding box (positions do not change between iterations)
@@ -73,88 +65,38 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
         const float  hmax = waveMax(valid ? hi : 0.0f);
         const double R    = 2.0 * (double)hmax * (1.0 + 1e-6) + a.margin;
         const double R2   = R * R;
-
-        auto overlaps = [&](int node) -> bool {
-            const double* c  = a.centers + 3 * (size_t)node;
-            const double* sz = a.sizes + 3 * (size_t)node;
-            double        d0 = c[0] - gcx, d1 = c[1] - gcy, d2 = c[2] - gcz;
-            d0               = fabs(foldPbc(d0, a.box, 0)) - sz[0] - gsx;
-            d1               = fabs(foldPbc(d1, a.box, 1)) - sz[1] - gsy;
-            d2               = fabs(foldPbc(d2, a.box, 2)) - sz[2] - gsz;
-            d0               = d0 > 0 ? d0 : 0;
-            d1               = d1 > 0 ? d1 : 0;
-            d2               = d2 > 0 ? d2 : 0;
-            return d0 * d0 + d1 * d1 + d2 * d2 < R2;
-        };
-
-        int numCand = 0, qh = 0, qt = 0, overflow = 0;
-        if (overlaps(0))
-        {
-            if (a.childOffsets[0] == 0) { numCand = 1, cand[0] = 0; }
-            else { queue[0] = 0, qt = 1; }
-        }
-        __builtin_amdgcn_wave_barrier();
-        while (qh < qt)
-        {
-            const int take = min(8, qt - qh);
-            const int slot = lane >> 3, oct = lane & 7;
-            const bool ok  = slot < take;
-            int  node      = ok ? queue[(qh + slot) & (kQCap - 1)] : 0;
-            int  child     = ok ? a.childOffsets[node] + oct : 0;
-            bool pass      = ok && overlaps(child);
-            bool isLeaf    = pass && a.childOffsets[child] == 0;
-            bool isInner   = pass && !isLeaf;
-            uint64_t bl = __ballot(isLeaf), bi = __ballot(isInner);
-            if (isLeaf)
-            {
-                int pos = numCand + __popcll(bl & ltMask);
-                if (pos < kCCap) cand[pos] = child;
-            }
-            if (isInner) { queue[(qt + __popcll(bi & ltMask)) & (kQCap - 1)] = child; }
-            numCand += __popcll(bl);
-            qt += __popcll(bi);
-            qh += take;
-            if (qt - qh > kQCap) overflow = 1;
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (numCand > kCCap) overflow = 1;
-        if (overflow)
-        {
-            if (lane == 0) atomicOr(&a.stats[0], 1u);
-            numCand = min(numCand, kCCap);
-        }
+        bool         overflow;
+        const int    numCand = waveCollectLeaves(
+            a.childOffsets,
+            [&](int node) {
+                return boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, gcx, gcy, gcz, gsx, gsy, gsz,
+                                a.box) < R2;
+            },
+            queue, cand, lane, overflow);
+        if (overflow && lane == 0) atomicOr(&a.stats[0], 1u);
 
         // ---- 3. test candidates against each lane's own particle --------------------------------------
-        const float  r2f    = 4.0f * hi * hi;
-        const double radSq  = (double)r2f;
-        const double tw     = 2.0 * (double)hi;
-        const bool   inside = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) && (zi - tw >= a.box.lim[4]) &&
-                            (xi + tw <= a.box.lim[1]) && (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
-        const bool usePbc   = a.box.anyPbc && !inside;
-        const bool anyPbcUse = __ballot(usePbc && valid) != 0;
-        const float hLane   = valid ? hi : 0.0f;
+        const float  r2f       = 4.0f * hi * hi;
+        const double radSq     = (double)r2f;
+        const double tw        = 2.0 * (double)hi;
+        const bool   inside    = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) &&
+                            (zi - tw >= a.box.lim[4]) && (xi + tw <= a.box.lim[1]) &&
+                            (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
+        const bool   usePbc    = a.box.anyPbc && !inside;
+        const bool   anyPbcUse = __ballot(usePbc && valid) != 0;
+        const double rr        = 2.0 * (double)(valid ? hi : 0.0f) * (1.0 + 1e-6) + a.margin;
 
         count = 0;
         for (int c = 0; c < numCand; ++c)
         {
-            const int node = __builtin_amdgcn_readfirstlane(cand[c]);
-            const int leaf = a.internalToLeaf[node];
+            const int      node = __builtin_amdgcn_readfirstlane(cand[c]);
+            const int      leaf = a.internalToLeaf[node];
             const uint32_t p0 = a.layout[leaf], p1 = a.layout[leaf + 1];
             if (p0 == p1) continue;
-            // per-lane sphere-vs-leaf prune (conservative), skip the leaf if no lane can reach it
-            {
-                const double* cc = a.centers + 3 * (size_t)node;
-                const double* sz = a.sizes + 3 * (size_t)node;
-                double d0 = fabs(foldPbc(cc[0] - xi, a.box, 0)) - sz[0];
-                double d1 = fabs(foldPbc(cc[1] - yi, a.box, 1)) - sz[1];
-                double d2 = fabs(foldPbc(cc[2] - zi, a.box, 2)) - sz[2];
-                d0 = d0 > 0 ? d0 : 0;
-                d1 = d1 > 0 ? d1 : 0;
-                d2 = d2 > 0 ? d2 : 0;
-                double rr = 2.0 * (double)hLane * (1.0 + 1e-6) + a.margin;
-                bool   reach = valid && (d0 * d0 + d1 * d1 + d2 * d2 < rr * rr);
-                if (__ballot(reach) == 0) continue;
-            }
+            // per-lane sphere-vs-leaf prune (conservative): skip the leaf if no lane can reach it
+            const bool reach = valid && boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, xi, yi, zi,
+                                                 0.0, 0.0, 0.0, a.box) < rr * rr;
+            if (__ballot(reach) == 0) continue;
             for (uint32_t s0 = p0; s0 < p1; s0 += kWave)
             {
                 const uint32_t jl = s0 + lane;
@@ -232,10 +174,10 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
         a.nc[i] = count + 1;
         if (a.iterateH) a.h[i] = hi;
     }
-    // statistics
-    const unsigned failed  = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
-    const unsigned nfail   = waveSum(failed);
-    const unsigned maxCnt  = waveMax(valid ? count : 0u);
+    // statistics (NcStats-like)
+    const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
+    const unsigned           nfail  = waveSum(failed);
+    const unsigned           maxCnt = waveMax(valid ? count : 0u);
     const unsigned long long stored = waveSum((unsigned long long)(valid ? min(count, a.ngmax) : 0u));
     const unsigned long long tested = waveSum(valid ? candTested : 0ull);
     if (lane == 0)

@@ -1,28 +1,55 @@
 /*! @file sx_sim.cpp
  * @brief Device-resident VE time step (sx_sim_*): HydroVeProp::computeForces + integrate
- *        (main/src/propagator/ve_hydro.hpp:132-218) for one GPU, all state kept in HBM.
+ *        (main/src/propagator/ve_hydro.hpp:132-218), on one GPU or SFC-decomposed over several.
  *
- * Step = sync (Hilbert keys, radix sort, reorder of every conserved field, converged tree) -> neighbor search with
- * h-nc iteration -> XMass -> VeDefGradh -> EOS -> IAD+divv/curlv -> max divv -> AV switches -> momentum/energy ->
- * time-step (device scalar, no host round trip) -> positions/energy -> h update.
+ * Step = sync -> neighbor search with h-nc iteration -> XMass -> [halo xm] -> VeDefGradh -> EOS
+ *        -> [halo v,prho,c,kx] -> IAD+divv/curlv -> [halo c_ij,divv] -> AV switches -> [halo alpha]
+ *        -> momentum/energy -> global time-step min -> positions/energy -> h update.
+ *
+ * sync, one GPU: Hilbert keys, radix sort, reorder of every conserved field, converged tree.
+ * sync, P GPUs (replaces cstone::Domain::sync, domain.hpp:196-244, with an MI355X-first design):
+ *   1. sort local particles by key;
+ *   2. global key histogram (2^18 bins, allreduce) -> equal-count SFC splitters, identical on every rank
+ *      (the reference's global cornerstone tree + MPI_Allreduce of counts, update_mpi_gpu.cuh:75);
+ *   3. particle exchange to the SFC owner (alltoallv of 80-byte AoS records; skipped when nothing moves);
+ *   4. halo discovery: each rank publishes request boxes = AABB of every 2048-particle SFC chunk grown by
+ *      2*hmax(chunk)*margin; every rank marks (wave-cooperative tree traversal of its own tree) the particles
+ *      inside each peer's boxes -> send lists; halos land in place, [halos of lower ranks | local | higher];
+ *   5. the combined array is key-sorted by construction -> one tree over locals + halos.
+ *   After the h iteration the request margin is checked; if some particle outgrew it, discovery is redone.
+ * Halo exchanges carry exactly the reference's fields (ve_hydro.hpp:150-186): x,y,z,h,m at setup, then xm,
+ * then vx,vy,vz,prho,c,kx, then c11..c33,divv, then alpha.
  */
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
-#include <type_traits>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/sphexa_hip.h"
+#include "sx_comm.hpp"
 #include "sx_hydro.hpp"
+#include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
 using namespace sx;
 
+extern "C" void*          sx_ctx_stream_internal(sx_ctx* c);
+extern "C" int            sx_ctx_exact_internal(sx_ctx* c);
+extern "C" const float2*  sx_ctx_table_internal(sx_ctx* c, int which);
+extern "C" const float*   sx_ctx_powtab_internal(sx_ctx* c, uint32_t ng0);
+extern "C" sx::Transport* sx_comm_transport_internal(sx_comm* c);
+
 namespace
 {
+
+constexpr int      kHistBits   = 18;    // global key histogram resolution (level 6)
+constexpr uint32_t kChunk      = 2048;  // particles per halo request box
+constexpr double   kHaloMargin = 1.05;  // request radius = 2 * hmax(chunk) * margin (+ quantisation margin)
 
 DevBox toDevBox(const sx_box* b)
 {
@@ -44,12 +71,32 @@ DevBox toDevBox(const sx_box* b)
 struct Scalars
 {
     double   minDt, minDt_m1, ttot, minDtCourant, minDtRho;
+    double   dtCand;   // rank-local candidate, globally min-reduced
     float    courant;  // atomic-min target of the momentum kernel
     unsigned maxDivvU; // order-preserving image of max divv
 };
 
-//! computeTimestep (ts_global.hpp:97-112, single rank) and rhoTimestep (:72-94) on the device
-__global__ void timestepKernel(Scalars* s, double Krho, double maxDtIncrease)
+//! particle record of the SFC exchange (conserved fields of the VE propagator, ve_hydro.hpp:74)
+struct __attribute__((aligned(16))) PRec
+{
+    double   x, y, z, temp;
+    float    h, m, vx, vy, vz, xm1, ym1, zm1, dum1, alpha;
+    uint64_t id;
+};
+static_assert(sizeof(PRec) == 80, "PRec layout");
+
+//! halo request box: AABB grown by the search radius
+struct __attribute__((aligned(16))) ReqBox
+{
+    double c[3], s[3];
+    double hmax;
+    int32_t owner, pad;
+};
+
+// ---- time step --------------------------------------------------------------------------------------------
+
+//! rhoTimestep (ts_global.hpp:72-94) and the rank-local part of computeTimestep (:97-112)
+__global__ void dtCandidateKernel(Scalars* s, double Krho, double maxDtIncrease)
 {
     unsigned u = s->maxDivvU;
     u          = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
@@ -60,6 +107,13 @@ __global__ void timestepKernel(Scalars* s, double Krho, double maxDtIncrease)
     double cand[3]  = {s->minDtCourant, s->minDtRho, maxDtIncrease * s->minDt};
     for (int k = 0; k < 3; ++k)
         m = cand[k] < m ? cand[k] : m;
+    s->dtCand = m;
+}
+
+//! after the (MPI_Allreduce-equivalent) global min: ttot, minDt_m1, minDt
+__global__ void dtApplyKernel(Scalars* s)
+{
+    double m = s->dtCand;
     s->ttot += m;
     s->minDt_m1 = s->minDt;
     s->minDt    = m;
@@ -71,51 +125,229 @@ __global__ void resetScalarsKernel(Scalars* s)
     s->maxDivvU = 0;
 }
 
-//! Sedov lattice (grid.hpp:102-132, sedov_init.hpp:48-96), particle index = z-major lattice index
-__global__ void sedovInitKernel(uint32_t side, size_t n, double* x, double* y, double* z, float* h, float* m,
-                                double* temp, float* vx, float* vy, float* vz, float* xm1, float* ym1, float* zm1,
-                                float* dum1, float* alpha, uint64_t* id, float hInit, float mPart, double ener0,
-                                double width2, double u0, float cv)
+// ---- initial conditions -----------------------------------------------------------------------------------
+
+//! Sedov lattice (grid.hpp:102-132, sedov_init.hpp:48-96); particles [lfirst, lfirst + n) of the z-major lattice
+__global__ void sedovInitKernel(uint32_t side, size_t lfirst, size_t n, double* x, double* y, double* z, float* h,
+                                float* m, double* temp, float* vx, float* vy, float* vz, float* xm1, float* ym1,
+                                float* zm1, float* dum1, float* alpha, uint64_t* id, float hInit, float mPart,
+                                double ener0, double width2, double u0, float cv)
 {
-    size_t li = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (li >= n) return;
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    size_t       li = lfirst + t;
     const double r = 0.5, step = (2. * r) / side, r_ini = -r + 0.5 * step;
     size_t       i = li / ((size_t)side * side), j = (li / side) % side, k = li % side;
     double       lz = r_ini + (i * step), ly = r_ini + (j * step), lx = r_ini + (k * step);
-    x[li] = lx;
-    y[li] = ly;
-    z[li] = lz;
-    h[li] = hInit;
-    m[li] = mPart;
+    x[t] = lx;
+    y[t] = ly;
+    z[t] = lz;
+    h[t] = hInit;
+    m[t] = mPart;
     double r2 = lx * lx + ly * ly + lz * lz;
     double ui = ener0 * exp(-(r2 / width2)) + u0;
-    temp[li]  = ui / (double)cv;
-    vx[li] = vy[li] = vz[li] = 0.f;
-    xm1[li] = ym1[li] = zm1[li] = 0.f;
-    dum1[li]  = 0.f;
-    alpha[li] = 0.05f;
-    id[li]    = li;
+    temp[t]   = ui / (double)cv;
+    vx[t] = vy[t] = vz[t] = 0.f;
+    xm1[t] = ym1[t] = zm1[t] = 0.f;
+    dum1[t]  = 0.f;
+    alpha[t] = 0.05f;
+    id[t]    = li;
 }
 
-} // namespace
+// ---- domain decomposition kernels -------------------------------------------------------------------------
 
-struct sx_sim
+__global__ void histKernel(const uint64_t* keys, size_t n, uint32_t* bins)
 {
-    sx_ctx*   ctx;
-    sx_params p;
-    sx_box    box;
-    DevBox    dbox;
-    uint32_t  bucket;
-    size_t    cap{0}, n{0};
-    Arena     mem; // persistent particle fields (double-buffered conserved set)
-    Arena     work;
-    DevTree   tree;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&bins[keys[i] >> (63 - kHistBits)], 1u);
+}
 
-    // conserved (A/B for the reorder)
+__global__ void lowerBoundsKernel(const uint64_t* keys, size_t n, const uint64_t* split, int P, uint64_t* out)
+{
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > P) return;
+    uint64_t v  = split[q];
+    size_t   lo = 0, hi = n;
+    while (lo < hi)
+    {
+        size_t mid = (lo + hi) >> 1;
+        if (keys[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    out[q] = lo;
+}
+
+struct Fields
+{
     double *  x, *y, *z, *temp;
     float *   h, *m, *vx, *vy, *vz, *xm1, *ym1, *zm1, *dum1, *alpha;
     uint64_t* id;
-    // dependent
+};
+
+__global__ void packPRecKernel(Fields f, size_t n, PRec* out)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = PRec{f.x[i],   f.y[i],   f.z[i],   f.temp[i], f.h[i],    f.m[i],     f.vx[i], f.vy[i],
+                  f.vz[i],  f.xm1[i], f.ym1[i], f.zm1[i],  f.dum1[i], f.alpha[i], f.id[i]};
+}
+
+__global__ void unpackPRecKernel(const PRec* in, size_t n, Fields f)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    PRec r    = in[i];
+    f.x[i]    = r.x;
+    f.y[i]    = r.y;
+    f.z[i]    = r.z;
+    f.temp[i] = r.temp;
+    f.h[i]    = r.h;
+    f.m[i]    = r.m;
+    f.vx[i]   = r.vx;
+    f.vy[i]   = r.vy;
+    f.vz[i]   = r.vz;
+    f.xm1[i]  = r.xm1;
+    f.ym1[i]  = r.ym1;
+    f.zm1[i]  = r.zm1;
+    f.dum1[i] = r.dum1;
+    f.alpha[i] = r.alpha;
+    f.id[i]   = r.id;
+}
+
+//! request box of every kChunk SFC-consecutive local particles: AABB grown by 2*hmax*margin + quantisation margin
+__global__ void chunkBoxKernel(const double* x, const double* y, const double* z, const float* h, size_t n,
+                               double margin, double qmargin, int owner, ReqBox* out)
+{
+    const size_t c0   = (size_t)blockIdx.x * kChunk;
+    const size_t c1   = min(n, c0 + kChunk);
+    double       lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float        hm   = 0;
+    for (size_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+    {
+        lo[0] = fmin(lo[0], x[i]), hi[0] = fmax(hi[0], x[i]);
+        lo[1] = fmin(lo[1], y[i]), hi[1] = fmax(hi[1], y[i]);
+        lo[2] = fmin(lo[2], z[i]), hi[2] = fmax(hi[2], z[i]);
+        hm    = fmaxf(hm, h[i]);
+    }
+    __shared__ double s[6][4];
+    __shared__ float  sh[4];
+    for (int k = 0; k < 3; ++k)
+    {
+        lo[k] = waveMin(lo[k]);
+        hi[k] = waveMax(hi[k]);
+    }
+    hm = waveMax(hm);
+    int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+    {
+        for (int k = 0; k < 3; ++k)
+            s[k][w] = lo[k], s[3 + k][w] = hi[k];
+        sh[w] = hm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        int nw = blockDim.x >> 6;
+        for (int v = 1; v < nw; ++v)
+            for (int k = 0; k < 3; ++k)
+                s[k][0] = fmin(s[k][0], s[k][v]), s[3 + k][0] = fmax(s[3 + k][0], s[3 + k][v]), sh[0] = fmaxf(sh[0], sh[v]);
+        ReqBox b;
+        double R = 2.0 * (double)sh[0] * margin + qmargin;
+        for (int k = 0; k < 3; ++k)
+        {
+            b.c[k] = 0.5 * (s[k][0] + s[3 + k][0]);
+            b.s[k] = 0.5 * (s[3 + k][0] - s[k][0]) + R;
+        }
+        b.hmax  = sh[0];
+        b.owner = owner;
+        b.pad   = 0;
+        out[blockIdx.x] = b;
+    }
+}
+
+//! 1 if some particle of the chunk grew beyond the chunk's request radius during the h iteration
+__global__ void chunkCheckKernel(const float* h, size_t n, const ReqBox* boxes, double margin, unsigned* flag)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ReqBox& b = boxes[i / kChunk];
+    if ((double)h[i] > b.hmax * margin) atomicOr(flag, 1u);
+}
+
+/*! one wave per peer request box: traverse the local tree, mark local particles inside the box (minimum image)
+ *  for the box owner.  mark: one bit per rank (<= 64 ranks). */
+__global__ __launch_bounds__(256) void markHalosKernel(const ReqBox* boxes, int numBoxes, const int32_t* childOffsets,
+                                                       const int32_t* internalToLeaf, const uint32_t* layout,
+                                                       const double* centers, const double* sizes, const double* x,
+                                                       const double* y, const double* z, DevBox box, double qmargin,
+                                                       unsigned long long* mark, uint32_t* err)
+{
+    __shared__ int s_queue[4][kQCap];
+    __shared__ int s_cand[4][kCCap];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int bi   = blockIdx.x * 4 + wave;
+    if (bi >= numBoxes) return;
+    const ReqBox b = boxes[bi];
+    bool         overflow;
+    const int    numCand = waveCollectLeaves(
+        childOffsets,
+        [&](int node) {
+            return boxDist2(centers + 3 * (size_t)node, sizes + 3 * (size_t)node, b.c[0], b.c[1], b.c[2],
+                            b.s[0] + qmargin, b.s[1] + qmargin, b.s[2] + qmargin, box) <= 0.0;
+        },
+        s_queue[wave], s_cand[wave], lane, overflow);
+    if (overflow && lane == 0) atomicOr(err, 1u);
+    const unsigned long long bit = 1ull << b.owner;
+    for (int c = 0; c < numCand; ++c)
+    {
+        const int      node = __builtin_amdgcn_readfirstlane(s_cand[wave][c]);
+        const int      leaf = internalToLeaf[node];
+        const uint32_t p0 = layout[leaf], p1 = layout[leaf + 1];
+        for (uint32_t p = p0 + lane; p < p1; p += 64)
+        {
+            double d0 = fabs(foldPbc(x[p] - b.c[0], box, 0));
+            double d1 = fabs(foldPbc(y[p] - b.c[1], box, 1));
+            double d2 = fabs(foldPbc(z[p] - b.c[2], box, 2));
+            if (d0 <= b.s[0] && d1 <= b.s[1] && d2 <= b.s[2]) atomicOr(&mark[p], bit);
+        }
+    }
+}
+
+__global__ void maskFlagKernel(const unsigned long long* mark, size_t n, int q, uint32_t* flag)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i <= n) flag[i] = (i < n) ? (uint32_t)((mark[i] >> q) & 1ull) : 0u;
+}
+
+__global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, size_t n, uint32_t* out)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) out[scan[i]] = (uint32_t)i;
+}
+
+static inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+} // namespace
+
+// ---------------------------------------------------------------------------------------------------------------
+
+struct sx_sim
+{
+    sx_ctx*        ctx;
+    sx::Transport* comm{nullptr};
+    sx_params      p;
+    sx_box         box;
+    DevBox         dbox;
+    uint32_t       bucket;
+    size_t         cap{0}, n{0}, first{0}, last{0};
+    Arena          mem;
+    Arena          work;
+    DevTree        tree;
+    DevTree        localTree;
+
+    double *  x, *y, *z, *temp;
+    float *   h, *m, *vx, *vy, *vz, *xm1, *ym1, *zm1, *dum1, *alpha;
+    uint64_t* id;
     uint64_t* keys;
     uint32_t *order, *nc;
     float *   xm, *kx, *gradh, *prho, *c, *divv, *curlv, *c11, *c12, *c13, *c22, *c23, *c33, *ax, *ay, *az;
@@ -136,39 +368,43 @@ struct sx_sim
         void*  alt;
         int    elemBytes;
     };
-    std::vector<Spare> spares; // double buffers of the conserved fields for the SFC reorder
+    std::vector<Spare> spares; // double buffers of the conserved fields
+
+    // halo bookkeeping of the current step
+    std::vector<uint64_t> haloSend, haloSendOff, haloRecv, haloRecvOff;
+    uint32_t*             sendIdx{nullptr};
+    uint64_t              numSend{0};
+    uint64_t              numHalos{0};
+    uint64_t*             cntBuf{nullptr};
 
     std::vector<hipEvent_t>  ev;
     std::vector<std::string> stageNames;
     std::vector<float>       stageMs;
     sx_nbstats               lastStats{};
-};
+    int                      haloRetries{0};
 
-// internal: accessors implemented in sx_capi.cpp
-extern "C" void* sx_ctx_stream_internal(sx_ctx* c);
-extern "C" int   sx_ctx_exact_internal(sx_ctx* c);
-extern "C" const float2* sx_ctx_table_internal(sx_ctx* c, int which);
-extern "C" const float*  sx_ctx_powtab_internal(sx_ctx* c, uint32_t ng0);
+    Fields fields() const { return Fields{x, y, z, temp, h, m, vx, vy, vz, xm1, ym1, zm1, dum1, alpha, id}; }
+};
 
 namespace
 {
 
 void allocFields(sx_sim* s, size_t cap)
 {
-    auto& a = s->mem;
-    s->x    = a.get<double>("x", cap);
-    s->y    = a.get<double>("y", cap);
-    s->z    = a.get<double>("z", cap);
-    s->temp = a.get<double>("temp", cap);
-    s->h    = a.get<float>("h", cap);
-    s->m    = a.get<float>("m", cap);
-    s->vx   = a.get<float>("vx", cap);
-    s->vy   = a.get<float>("vy", cap);
-    s->vz   = a.get<float>("vz", cap);
-    s->xm1  = a.get<float>("x_m1", cap);
-    s->ym1  = a.get<float>("y_m1", cap);
-    s->zm1  = a.get<float>("z_m1", cap);
-    s->dum1 = a.get<float>("du_m1", cap);
+    auto& a  = s->mem;
+    s->x     = a.get<double>("x", cap);
+    s->y     = a.get<double>("y", cap);
+    s->z     = a.get<double>("z", cap);
+    s->temp  = a.get<double>("temp", cap);
+    s->h     = a.get<float>("h", cap);
+    s->m     = a.get<float>("m", cap);
+    s->vx    = a.get<float>("vx", cap);
+    s->vy    = a.get<float>("vy", cap);
+    s->vz    = a.get<float>("vz", cap);
+    s->xm1   = a.get<float>("x_m1", cap);
+    s->ym1   = a.get<float>("y_m1", cap);
+    s->zm1   = a.get<float>("z_m1", cap);
+    s->dum1  = a.get<float>("du_m1", cap);
     s->alpha = a.get<float>("alpha", cap);
     s->id    = a.get<uint64_t>("id", cap);
     s->keys  = a.get<uint64_t>("keys", cap);
@@ -197,7 +433,8 @@ void allocFields(sx_sim* s, size_t cap)
     s->rc    = a.get<RecC>("rc", cap);
     auto spare = [&](auto*& field, const char* tag) {
         using T = std::remove_reference_t<decltype(*field)>;
-        s->spares.push_back({reinterpret_cast<void**>(&field), a.get<T>(std::string(tag) + ".alt", cap), (int)sizeof(T)});
+        s->spares.push_back(
+            {reinterpret_cast<void**>(&field), a.get<T>(std::string(tag) + ".alt", cap), (int)sizeof(T)});
     };
     spare(s->x, "x");
     spare(s->y, "y");
@@ -215,19 +452,19 @@ void allocFields(sx_sim* s, size_t cap)
     spare(s->alpha, "alpha");
     spare(s->id, "id");
     size_t groups = (cap + kGroupSize - 1) / kGroupSize;
-    s->nidx      = a.get<uint32_t>("nidx", groups * s->p.ngmax * kWave);
-    s->stats     = a.get<uint32_t>("stats", 8);
-    s->statsHost = a.pinned<uint32_t>("statsHost", 8);
-    s->sc        = a.get<Scalars>("scalars", 1);
-    s->scHost    = a.pinned<Scalars>("scalarsHost", 1);
+    s->nidx       = a.get<uint32_t>("nidx", groups * s->p.ngmax * kWave);
+    s->stats      = a.get<uint32_t>("stats", 8);
+    s->statsHost  = a.pinned<uint32_t>("statsHost", 8);
+    s->sc         = a.get<Scalars>("scalars", 1);
+    s->scHost     = a.pinned<Scalars>("scalarsHost", 1);
 }
 
 PairArgs simPairArgs(sx_sim* s)
 {
     PairArgs a{};
-    a.first          = 0;
-    a.last           = (uint32_t)s->n;
-    a.numGroups      = (uint32_t)((s->n + kGroupSize - 1) / kGroupSize);
+    a.first          = (uint32_t)s->first;
+    a.last           = (uint32_t)s->last;
+    a.numGroups      = (uint32_t)((s->last - s->first + kGroupSize - 1) / kGroupSize);
     a.ngmax          = s->p.ngmax;
     a.nidx           = s->nidx;
     a.nc             = s->nc;
@@ -267,12 +504,260 @@ PairArgs simPairArgs(sx_sim* s)
     return a;
 }
 
-} // namespace
+double quantMargin(const DevBox& b)
+{
+    return 4.0 * std::max(b.l[0], std::max(b.l[1], b.l[2])) / double(1u << kMaxLevel);
+}
 
 #define SIM_HIP(call)                                                                                                  \
     do {                                                                                                               \
         if ((call) != hipSuccess) return SX_ERR_HIP;                                                                   \
     } while (0)
+#define SIM_COMM(call)                                                                                                 \
+    do {                                                                                                               \
+        if (!(call)) return SX_ERR_HIP;                                                                                \
+    } while (0)
+
+//! sort the local particles [0,nl) of the primary arrays by key (keys[0..nl) computed) via the spare buffers
+int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
+{
+    SIM_HIP(sortKeys(s->work, s->keys, s->order, nl, st));
+    for (auto& sp : s->spares)
+    {
+        SIM_HIP(gather(s->order, nl, *sp.field, sp.alt, sp.elemBytes, st));
+        std::swap(*sp.field, sp.alt);
+    }
+    return SX_OK;
+}
+
+//! exchange one set of fields for the halos of this step (send lists built by discoverHalos)
+int haloExchange(sx_sim* s, std::initializer_list<std::pair<void*, int>> fields, hipStream_t st)
+{
+    if (!s->comm || s->comm->size() == 1) return SX_OK;
+    const int P = s->comm->size();
+    for (auto [ptr, es] : fields)
+    {
+        char* f   = static_cast<char*>(ptr);
+        char* buf = s->work.get<char>("halo.send", std::max<uint64_t>(1, s->numSend) * 8);
+        if (s->numSend) SIM_HIP(gather(s->sendIdx, s->numSend, f + s->first * es, buf, es, st));
+        std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
+        for (int q = 0; q < P; ++q)
+        {
+            sb[q] = s->haloSend[q] * es;
+            so[q] = s->haloSendOff[q] * es;
+            rb[q] = s->haloRecv[q] * es;
+            ro[q] = s->haloRecvOff[q] * es;
+        }
+        SIM_COMM(s->comm->alltoallv(buf, sb.data(), so.data(), f, rb.data(), ro.data(), st));
+    }
+    return SX_OK;
+}
+
+/*! distributed sync: SFC assignment, particle exchange, halo discovery + setup exchange, combined tree.
+ *  On entry the local particles are [first,last); on exit [first,last) again with halos around them. */
+int distributedSync(sx_sim* s, hipStream_t st, double margin)
+{
+    sx::Transport* T  = s->comm;
+    const int      P  = T->size(), r = T->rank();
+    size_t         nl = s->last - s->first;
+    const double   qm = quantMargin(s->dbox);
+
+    // --- 1. local keys + sort (compacts locals to [0, nl))
+    SIM_HIP(launchSfcKeys(s->x + s->first, s->y + s->first, s->z + s->first, s->keys, nl, s->dbox, st));
+    if (s->first != 0)
+    {
+        for (auto& sp : s->spares)
+        {
+            SIM_HIP(hipMemcpyAsync(sp.alt, static_cast<char*>(*sp.field) + s->first * sp.elemBytes, nl * sp.elemBytes,
+                                   hipMemcpyDeviceToDevice, st));
+            std::swap(*sp.field, sp.alt);
+        }
+    }
+    if (int e = sortLocals(s, nl, st)) return e;
+
+    // --- 2. global histogram -> splitters
+    const size_t nb   = size_t(1) << kHistBits;
+    uint32_t*    bins = s->work.get<uint32_t>("dom.bins", nb);
+    SIM_HIP(hipMemsetAsync(bins, 0, nb * 4, st));
+    if (nl) histKernel<<<grid(nl), 256, 0, st>>>(s->keys, nl, bins);
+    SIM_COMM(T->allreduceSumU32(bins, nb, st));
+    std::vector<uint32_t> hb(nb);
+    SIM_HIP(hipMemcpyAsync(hb.data(), bins, nb * 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    uint64_t total = 0;
+    for (auto v : hb)
+        total += v;
+    std::vector<uint64_t> split(P + 1, 0);
+    split[P] = uint64_t(1) << 63;
+    {
+        uint64_t acc = 0;
+        int      q   = 1;
+        for (size_t b = 0; b < nb && q < P; ++b)
+        {
+            while (q < P && acc >= (total * q) / P)
+                split[q++] = uint64_t(b) << (63 - kHistBits);
+            acc += hb[b];
+        }
+        while (q < P)
+            split[q++] = uint64_t(1) << 63;
+    }
+
+    // --- 3. particle exchange
+    uint64_t* dsplit = s->work.get<uint64_t>("dom.split", P + 1);
+    uint64_t* dseg   = s->work.get<uint64_t>("dom.seg", P + 1);
+    SIM_HIP(hipMemcpyAsync(dsplit, split.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
+    lowerBoundsKernel<<<1, 64, 0, st>>>(s->keys, nl, dsplit, P, dseg);
+    std::vector<uint64_t> seg(P + 1);
+    SIM_HIP(hipMemcpyAsync(seg.data(), dseg, 8 * (P + 1), hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    seg[0] = 0;
+    seg[P] = nl;
+    std::vector<uint64_t> sendCnt(P), recvCnt;
+    for (int q = 0; q < P; ++q)
+        sendCnt[q] = seg[q + 1] - seg[q];
+    s->cntBuf = s->work.get<uint64_t>("dom.cnt", 2 * P);
+    SIM_COMM(T->exchangeCounts(sendCnt, recvCnt, st, s->cntBuf));
+    bool moved = false;
+    for (int q = 0; q < P; ++q)
+        moved |= (q != r) && (sendCnt[q] || recvCnt[q]);
+    if (moved)
+    {
+        uint64_t nNew = 0;
+        for (int q = 0; q < P; ++q)
+            nNew += recvCnt[q];
+        if (nNew > s->cap) return SX_ERR_NOMEM;
+        PRec* sbuf = s->work.get<PRec>("dom.psend", nl);
+        PRec* rbuf = s->work.get<PRec>("dom.precv", nNew);
+        if (nl) packPRecKernel<<<grid(nl), 256, 0, st>>>(s->fields(), nl, sbuf);
+        std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
+        uint64_t              acc = 0;
+        for (int q = 0; q < P; ++q)
+        {
+            sb[q] = sendCnt[q] * sizeof(PRec);
+            so[q] = seg[q] * sizeof(PRec);
+            rb[q] = recvCnt[q] * sizeof(PRec);
+            ro[q] = acc * sizeof(PRec);
+            acc += recvCnt[q];
+        }
+        SIM_COMM(T->alltoallv(sbuf, sb.data(), so.data(), rbuf, rb.data(), ro.data(), st));
+        nl = nNew;
+        if (nl) unpackPRecKernel<<<grid(nl), 256, 0, st>>>(rbuf, nl, s->fields());
+        SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, nl, s->dbox, st));
+        if (int e = sortLocals(s, nl, st)) return e;
+    }
+
+    // --- 4. halo discovery: request boxes, exchange, mark, send lists
+    const size_t nChunks = (nl + kChunk - 1) / kChunk;
+    ReqBox*      myBoxes = s->work.get<ReqBox>("dom.mybox", nChunks);
+    if (nChunks) chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
+    std::vector<uint64_t> boxCnt(P, nChunks), boxRecv;
+    boxCnt[r] = 0;
+    SIM_COMM(T->exchangeCounts(boxCnt, boxRecv, st, s->cntBuf));
+    uint64_t nRemote = 0;
+    for (int q = 0; q < P; ++q)
+        nRemote += boxRecv[q];
+    ReqBox* remote = s->work.get<ReqBox>("dom.rbox", nRemote);
+    {
+        std::vector<uint64_t> sb(P), so(P, 0), rb(P), ro(P);
+        uint64_t              acc = 0;
+        for (int q = 0; q < P; ++q)
+        {
+            sb[q] = boxCnt[q] * sizeof(ReqBox);
+            rb[q] = boxRecv[q] * sizeof(ReqBox);
+            ro[q] = acc * sizeof(ReqBox);
+            acc += boxRecv[q];
+        }
+        SIM_COMM(T->alltoallv(myBoxes, sb.data(), so.data(), remote, rb.data(), ro.data(), st));
+    }
+    SIM_HIP(buildTree(s->work, s->keys, nl, s->bucket, s->dbox, s->localTree, st));
+    auto* mark = s->work.get<unsigned long long>("dom.mark", nl);
+    auto* err  = s->work.get<uint32_t>("dom.err", 1);
+    SIM_HIP(hipMemsetAsync(mark, 0, nl * 8, st));
+    SIM_HIP(hipMemsetAsync(err, 0, 4, st));
+    if (nRemote && nl)
+        markHalosKernel<<<grid(nRemote, 4), 256, 0, st>>>(
+            remote, (int)nRemote, s->localTree.childOffsets, s->localTree.internalToLeaf, s->localTree.layout,
+            s->localTree.centers, s->localTree.sizes, s->x, s->y, s->z, s->dbox, qm, mark, err);
+    uint32_t* flag = s->work.get<uint32_t>("dom.flag", nl + 1);
+    uint32_t* scan = s->work.get<uint32_t>("dom.scan", nl + 1);
+    s->haloSend.assign(P, 0);
+    s->haloSendOff.assign(P, 0);
+    std::vector<uint64_t> counts(P, 0);
+    // count per peer, then compact in rank order
+    s->sendIdx      = s->work.get<uint32_t>("dom.sendIdx", std::max<size_t>(1, nl) * std::min(P - 1, 8));
+    uint64_t offset = 0;
+    size_t   tmpB   = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nl + 1, st);
+    void*    tmp    = s->work.get<char>("dom.scantmp", tmpB);
+    uint32_t* hcnt  = s->work.pinned<uint32_t>("dom.hcnt", 2);
+    for (int q = 0; q < P; ++q)
+    {
+        if (q == r || nl == 0) continue;
+        maskFlagKernel<<<grid(nl + 1), 256, 0, st>>>(mark, nl, q, flag);
+        hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nl + 1, st);
+        SIM_HIP(hipMemcpyAsync(hcnt, scan + nl, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        uint64_t cq = hcnt[0];
+        if (offset + cq > std::max<size_t>(1, nl) * std::min(P - 1, 8))
+            s->sendIdx = nullptr; // capacity exceeded (more than 8 full copies): give up loudly
+        if (!s->sendIdx) return SX_ERR_NOMEM;
+        scatterIdxKernel<<<grid(nl), 256, 0, st>>>(flag, scan, nl, s->sendIdx + offset);
+        s->haloSend[q]    = cq;
+        s->haloSendOff[q] = offset;
+        offset += cq;
+    }
+    s->numSend = offset;
+    SIM_COMM(T->exchangeCounts(s->haloSend, s->haloRecv, st, s->cntBuf));
+    s->haloRecv[r] = 0;
+    uint64_t nLow = 0, nHigh = 0;
+    for (int q = 0; q < P; ++q)
+        (q < r ? nLow : nHigh) += s->haloRecv[q];
+    if (nLow + nl + nHigh > s->cap) return SX_ERR_NOMEM;
+    s->haloRecvOff.assign(P, 0);
+    {
+        uint64_t lo = 0, hi = nLow + nl;
+        for (int q = 0; q < P; ++q)
+        {
+            if (q < r) { s->haloRecvOff[q] = lo, lo += s->haloRecv[q]; }
+            else if (q > r) { s->haloRecvOff[q] = hi, hi += s->haloRecv[q]; }
+        }
+    }
+    s->numHalos = nLow + nHigh;
+
+    // --- 5. move locals to [nLow, nLow + nl), exchange x,y,z,h,m, keys + tree over everything
+    if (nLow)
+    {
+        for (auto& sp : s->spares)
+        {
+            SIM_HIP(hipMemcpyAsync(static_cast<char*>(sp.alt) + nLow * sp.elemBytes, *sp.field, nl * sp.elemBytes,
+                                   hipMemcpyDeviceToDevice, st));
+            std::swap(*sp.field, sp.alt);
+        }
+    }
+    s->first = nLow;
+    s->last  = nLow + nl;
+    s->n     = nLow + nl + nHigh;
+    if (int e = haloExchange(s, {{s->x, 8}, {s->y, 8}, {s->z, 8}, {s->h, 4}, {s->m, 4}}, st)) return e;
+    SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, s->n, s->dbox, st));
+    SIM_HIP(buildTree(s->work, s->keys, s->n, s->bucket, s->dbox, s->tree, st));
+    unsigned errH = 0;
+    SIM_HIP(hipMemcpy(&errH, err, 4, hipMemcpyDeviceToHost));
+    if (errH) return SX_ERR_TRAVERSAL;
+    return SX_OK;
+}
+
+int localSync(sx_sim* s, hipStream_t st)
+{
+    const size_t n = s->n;
+    SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, n, s->dbox, st));
+    if (int e = sortLocals(s, n, st)) return e;
+    SIM_HIP(buildTree(s->work, s->keys, n, s->bucket, s->dbox, s->tree, st));
+    s->first = 0;
+    s->last  = n;
+    return SX_OK;
+}
+
+} // namespace
 
 extern "C"
 {
@@ -293,15 +778,15 @@ extern "C"
             delete s;
             return SX_ERR_NOMEM;
         }
-        const char* names[] = {"sync", "FindNeighbors", "XMass", "VeDefGradh", "EOS", "IadDivvCurlv",
-                               "AVswitches", "MomentumEnergy", "UpdateQuantities"};
+        const char* names[] = {"sync",       "FindNeighbors", "XMass",      "VeDefGradh",     "EOS",
+                               "IadDivvCurlv", "AVswitches",  "MomentumEnergy", "UpdateQuantities"};
         s->stageNames.assign(std::begin(names), std::end(names));
         s->ev.resize(s->stageNames.size() + 1);
         for (auto& e : s->ev)
-            hipEventCreate(&e);
+            (void)hipEventCreate(&e);
         s->stageMs.assign(s->stageNames.size(), 0.f);
-        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 1e10f, 0};
-        hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
+        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
+        (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
         return SX_OK;
     }
@@ -315,27 +800,49 @@ extern "C"
         delete s;
     }
 
-    size_t sx_sim_size(sx_sim* s) { return s->n; }
-
-    int sx_sim_init_sedov(sx_sim* s, uint32_t side)
+    int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
-        size_t n = (size_t)side * side * side;
+        s->comm = sx_comm_transport_internal(c);
+        return SX_OK;
+    }
+
+    size_t sx_sim_size(sx_sim* s) { return s->last - s->first; }
+
+    int sx_sim_layout(sx_sim* s, uint64_t out[4])
+    {
+        out[0] = s->first;
+        out[1] = s->last;
+        out[2] = s->n;
+        out[3] = s->haloRetries;
+        return SX_OK;
+    }
+
+    int sx_sim_init_sedov_rank(sx_sim* s, uint32_t side, int rank, int size)
+    {
+        size_t N  = (size_t)side * side * side;
+        size_t f  = N * rank / size, l = N * (rank + 1) / size;
+        size_t n  = l - f;
         if (n > s->cap) return SX_ERR_ARG;
-        s->n           = n;
-        double r       = 0.5;
-        double hInit   = std::cbrt(3.0 / (4 * M_PI) * s->p.ng0 * std::pow(2 * r, 3) / n) * 0.5;
-        double width   = 0.1;
-        double ener0   = 1.0 / std::pow(M_PI, 1.5) / 1. / std::pow(width, 3.0);
-        float  cv      = idealGasCv(s->p.muiConst, s->p.gamma);
-        auto   st      = (hipStream_t)sx_ctx_stream_internal(s->ctx);
-        sedovInitKernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-            side, n, s->x, s->y, s->z, s->h, s->m, s->temp, s->vx, s->vy, s->vz, s->xm1, s->ym1, s->zm1, s->dum1,
-            s->alpha, s->id, (float)hInit, (float)(1.0 / n), ener0, width * width, 1e-8, cv);
-        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 1e10f, 0};
+        s->n          = n;
+        s->first      = 0;
+        s->last       = n;
+        double r      = 0.5;
+        double hInit  = std::cbrt(3.0 / (4 * M_PI) * s->p.ng0 * std::pow(2 * r, 3) / N) * 0.5;
+        double width  = 0.1;
+        double ener0  = 1.0 / std::pow(M_PI, 1.5) / 1. / std::pow(width, 3.0);
+        float  cv     = idealGasCv(s->p.muiConst, s->p.gamma);
+        auto   st     = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        if (n)
+            sedovInitKernel<<<grid(n), 256, 0, st>>>(side, f, n, s->x, s->y, s->z, s->h, s->m, s->temp, s->vx, s->vy,
+                                                     s->vz, s->xm1, s->ym1, s->zm1, s->dum1, s->alpha, s->id,
+                                                     (float)hInit, (float)(1.0 / N), ener0, width * width, 1e-8, cv);
+        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
         SIM_HIP(hipMemcpyAsync(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice, st));
         SIM_HIP(hipStreamSynchronize(st));
         return SX_OK;
     }
+
+    int sx_sim_init_sedov(sx_sim* s, uint32_t side) { return sx_sim_init_sedov_rank(s, side, 0, 1); }
 
     int sx_sim_set_state(sx_sim* s, size_t n, const double* x, const double* y, const double* z, const float* h,
                          const float* m, const double* temp, const float* vx, const float* vy, const float* vz,
@@ -343,8 +850,10 @@ extern "C"
                          const float* alpha, const uint64_t* id, double minDt, double minDt_m1)
     {
         if (n > s->cap) return SX_ERR_ARG;
-        s->n    = n;
-        auto cp = [n](void* d, const void* h, size_t es) { return hipMemcpy(d, h, n * es, hipMemcpyHostToDevice); };
+        s->n     = n;
+        s->first = 0;
+        s->last  = n;
+        auto cp  = [n](void* d, const void* h, size_t es) { return hipMemcpy(d, h, n * es, hipMemcpyHostToDevice); };
         SIM_HIP(cp(s->x, x, 8));
         SIM_HIP(cp(s->y, y, 8));
         SIM_HIP(cp(s->z, z, 8));
@@ -360,133 +869,176 @@ extern "C"
         SIM_HIP(cp(s->dum1, du_m1, 4));
         SIM_HIP(cp(s->alpha, alpha, 4));
         SIM_HIP(cp(s->id, id, 8));
-        Scalars init{minDt, minDt_m1, 0.0, INFINITY, INFINITY, 1e10f, 0};
+        Scalars init{minDt, minDt_m1, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
         SIM_HIP(hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice));
         return SX_OK;
     }
 
     int sx_sim_fields(sx_sim* s, sx_fields* f, uint64_t** id)
     {
+        // pointers to the LOCAL particles [first, last) of the last step
         std::memset(f, 0, sizeof(*f));
-        f->n     = s->n;
-        f->x     = s->x;
-        f->y     = s->y;
-        f->z     = s->z;
-        f->x_m1  = s->xm1;
-        f->y_m1  = s->ym1;
-        f->z_m1  = s->zm1;
-        f->vx    = s->vx;
-        f->vy    = s->vy;
-        f->vz    = s->vz;
-        f->prho  = s->prho;
-        f->h     = s->h;
-        f->m     = s->m;
-        f->c     = s->c;
-        f->ax    = s->ax;
-        f->ay    = s->ay;
-        f->az    = s->az;
-        f->du    = s->du;
-        f->du_m1 = s->dum1;
-        f->c11   = s->c11;
-        f->c12   = s->c12;
-        f->c13   = s->c13;
-        f->c22   = s->c22;
-        f->c23   = s->c23;
-        f->c33   = s->c33;
-        f->temp  = s->temp;
-        f->xm    = s->xm;
-        f->kx    = s->kx;
-        f->divv  = s->divv;
-        f->curlv = s->curlv;
-        f->alpha = s->alpha;
-        f->gradh = s->gradh;
-        f->keys  = s->keys;
-        f->nc    = s->nc;
-        if (id) *id = s->id;
+        size_t o = s->first;
+        f->n     = s->last - s->first;
+        f->x     = s->x + o;
+        f->y     = s->y + o;
+        f->z     = s->z + o;
+        f->x_m1  = s->xm1 + o;
+        f->y_m1  = s->ym1 + o;
+        f->z_m1  = s->zm1 + o;
+        f->vx    = s->vx + o;
+        f->vy    = s->vy + o;
+        f->vz    = s->vz + o;
+        f->prho  = s->prho + o;
+        f->h     = s->h + o;
+        f->m     = s->m + o;
+        f->c     = s->c + o;
+        f->ax    = s->ax + o;
+        f->ay    = s->ay + o;
+        f->az    = s->az + o;
+        f->du    = s->du + o;
+        f->du_m1 = s->dum1 + o;
+        f->c11   = s->c11 + o;
+        f->c12   = s->c12 + o;
+        f->c13   = s->c13 + o;
+        f->c22   = s->c22 + o;
+        f->c23   = s->c23 + o;
+        f->c33   = s->c33 + o;
+        f->temp  = s->temp + o;
+        f->xm    = s->xm + o;
+        f->kx    = s->kx + o;
+        f->divv  = s->divv + o;
+        f->curlv = s->curlv + o;
+        f->alpha = s->alpha + o;
+        f->gradh = s->gradh + o;
+        f->keys  = s->keys + o;
+        f->nc    = s->nc + o;
+        if (id) *id = s->id + o;
         return SX_OK;
     }
 
     int sx_sim_step(sx_sim* s)
     {
-        hipStream_t       st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
-        const HydroLaunch& H = sx_ctx_exact_internal(s->ctx) ? hydro_exact() : hydro_fast();
-        const size_t      n  = s->n;
-        int               ev = 0;
+        hipStream_t        st  = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        const HydroLaunch& H   = sx_ctx_exact_internal(s->ctx) ? hydro_exact() : hydro_fast();
+        const bool         dist = s->comm && s->comm->size() > 1;
+        int                ev  = 0;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
 
-        // ---- sync: keys, sort, reorder, tree -------------------------------------------------------------
-        SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, n, s->dbox, st));
-        SIM_HIP(sortKeys(s->work, s->keys, s->order, n, st));
-        for (auto& sp : s->spares)
-        {
-            SIM_HIP(gather(s->order, n, *sp.field, sp.alt, sp.elemBytes, st));
-            std::swap(*sp.field, sp.alt);
-        }
-        SIM_HIP(buildTree(s->work, s->keys, n, s->bucket, s->dbox, s->tree, st));
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-
-        // ---- neighbors + h iteration ---------------------------------------------------------------------
+        // h before the h iteration, to redo the search if the halo margin proves too small
+        float* h0     = dist ? s->work.get<float>("h0", s->cap) : nullptr;
+        double margin = kHaloMargin;
         NsArgs na{};
-        na.first          = 0;
-        na.last           = (uint32_t)n;
-        na.numGroups      = (uint32_t)((n + kGroupSize - 1) / kGroupSize);
-        na.ngmax          = s->p.ngmax;
-        na.ng0            = s->p.ng0;
-        na.iterateH       = 1;
-        na.x              = s->x;
-        na.y              = s->y;
-        na.z              = s->z;
-        na.h              = s->h;
-        na.nc             = s->nc;
-        na.nidx           = s->nidx;
-        na.childOffsets   = s->tree.childOffsets;
-        na.internalToLeaf = s->tree.internalToLeaf;
-        na.layout         = s->tree.layout;
-        na.centers        = s->tree.centers;
-        na.sizes          = s->tree.sizes;
-        na.box            = s->dbox;
-        na.margin         = 4.0 * std::max(s->dbox.l[0], std::max(s->dbox.l[1], s->dbox.l[2])) / double(1u << kMaxLevel);
-        na.stats          = s->stats;
-        na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
-        SIM_HIP(hipMemsetAsync(s->stats, 0, 32, st));
-        resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
-        SIM_HIP(findNeighbors(na, st));
-        SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, 32, hipMemcpyDeviceToHost, st));
+        for (int attempt = 0;; ++attempt)
+        {
+            if (dist)
+            {
+                if (attempt == 0)
+                {
+                    if (int e = distributedSync(s, st, margin)) return e;
+                }
+                else
+                {
+                    // restore pre-iteration h of the locals, then rediscover halos with a larger margin
+                    SIM_HIP(hipMemcpyAsync(s->h + s->first, h0, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
+                    if (int e = distributedSync(s, st, margin)) return e;
+                }
+                SIM_HIP(hipMemcpyAsync(h0, s->h + s->first, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
+            }
+            else if (attempt == 0)
+            {
+                if (int e = localSync(s, st)) return e;
+            }
+            if (attempt == 0) SIM_HIP(hipEventRecord(s->ev[ev++], st));
+
+            // ---- neighbors + h iteration on the local targets --------------------------------------------
+            na.first          = (uint32_t)s->first;
+            na.last           = (uint32_t)s->last;
+            na.numGroups      = (uint32_t)((s->last - s->first + kGroupSize - 1) / kGroupSize);
+            na.ngmax          = s->p.ngmax;
+            na.ng0            = s->p.ng0;
+            na.iterateH       = 1;
+            na.x              = s->x;
+            na.y              = s->y;
+            na.z              = s->z;
+            na.h              = s->h;
+            na.nc             = s->nc;
+            na.nidx           = s->nidx;
+            na.childOffsets   = s->tree.childOffsets;
+            na.internalToLeaf = s->tree.internalToLeaf;
+            na.layout         = s->tree.layout;
+            na.centers        = s->tree.centers;
+            na.sizes          = s->tree.sizes;
+            na.box            = s->dbox;
+            na.margin         = quantMargin(s->dbox);
+            na.stats          = s->stats;
+            na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
+            SIM_HIP(hipMemsetAsync(s->stats, 0, 32, st));
+            resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
+            SIM_HIP(findNeighbors(na, st));
+            SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, 32, hipMemcpyDeviceToHost, st));
+            if (!dist) break;
+            // halo sufficiency: every local particle's final h within its chunk's request margin
+            const size_t nl  = s->last - s->first;
+            auto*        flg = s->work.get<unsigned>("dom.hflag", 1);
+            SIM_HIP(hipMemsetAsync(flg, 0, 4, st));
+            if (nl)
+                chunkCheckKernel<<<grid(nl), 256, 0, st>>>(s->h + s->first, nl, s->work.get<ReqBox>("dom.mybox", 1),
+                                                         margin, flg);
+            unsigned hf = 0;
+            SIM_HIP(hipMemcpyAsync(s->statsHost + 3, flg, 4, hipMemcpyDeviceToHost, st));
+            SIM_HIP(hipStreamSynchronize(st));
+            hf = s->statsHost[3];
+            if (!hf) break;
+            if (attempt >= 3) return SX_ERR_NOT_CONVERGED;
+            margin *= 1.5;
+            s->haloRetries++;
+        }
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
 
-        PairArgs pa = simPairArgs(s);
+        const size_t n  = s->n;
+        PairArgs     pa = simPairArgs(s);
         // ---- XMass
         packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
         H.xmass(pa, st);
+        if (int e = haloExchange(s, {{s->xm, 4}}, st)) return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- VeDefGradh
         packT(n, s->xm, nullptr, nullptr, nullptr, s->rt, st);
         H.veDefGradh(pa, st);
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- EOS
-        EosArgs ea{0, (uint32_t)n, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm, s->gradh, s->prho, s->c,
-                   nullptr, nullptr};
+        // ---- EOS, then the v/prho/c/kx halo exchange
+        EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
+                   s->gradh, s->prho, s->c, nullptr, nullptr};
         H.eos(ea, st);
+        if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}}, st))
+            return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- IAD + divv/curlv, rho time-step
+        // ---- IAD + divv/curlv, rho time-step, then the c_ij/divv exchange
         packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
         packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
         H.iadDivvCurlv(pa, st);
-        SIM_HIP(maxFloat(s->divv, 0, (uint32_t)n, &s->sc->maxDivvU, st));
+        SIM_HIP(maxFloat(s->divv, (uint32_t)s->first, (uint32_t)s->last, &s->sc->maxDivvU, st));
+        if (int e = haloExchange(
+                s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}}, st))
+            return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- AV switches
+        // ---- AV switches, then the alpha exchange
         packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, s->divv, s->rc, st);
         H.avSwitches(pa, st);
+        if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- momentum + energy
         packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
         H.momentumEnergy(pa, st);
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- integrate
-        timestepKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease);
+        // ---- integrate: global time-step, positions, h
+        dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease);
+        if (dist) SIM_COMM(s->comm->allreduceMinF64(&s->sc->dtCand, 1, st));
+        dtApplyKernel<<<1, 1, 0, st>>>(s->sc);
         PosArgs qa{};
-        qa.first   = 0;
-        qa.last    = (uint32_t)n;
+        qa.first   = (uint32_t)s->first;
+        qa.last    = (uint32_t)s->last;
         qa.dtPtr   = &s->sc->minDt;
         qa.box     = s->dbox;
         qa.x       = s->x;
@@ -507,13 +1059,13 @@ extern "C"
         qa.h       = s->h;
         qa.constCv = idealGasCv(s->p.muiConst, s->p.gamma);
         H.positions(qa, st);
-        H.updateH(0, (uint32_t)n, s->p.ng0, s->nc, s->h, na.powTab, st);
+        H.updateH((uint32_t)s->first, (uint32_t)s->last, s->p.ng0, s->nc, s->h, na.powTab, st);
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         SIM_HIP(hipGetLastError());
         SIM_HIP(hipStreamSynchronize(st));
 
         for (size_t k = 0; k < s->stageMs.size(); ++k)
-            hipEventElapsedTime(&s->stageMs[k], s->ev[k], s->ev[k + 1]);
+            (void)hipEventElapsedTime(&s->stageMs[k], s->ev[k], s->ev[k + 1]);
         s->lastStats.numFailed     = s->statsHost[1];
         s->lastStats.maxNeighbors  = s->statsHost[2];
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);

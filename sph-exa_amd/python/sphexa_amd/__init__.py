@@ -74,6 +74,11 @@ DTYPES.update(x=np.float64, y=np.float64, z=np.float64, u=np.float64, du=np.floa
 
 _lib = None
 
+# host-staged transport callbacks (sx_alltoallv_cb / sx_allreduce_cb)
+ALLTOALLV_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
+                           C.POINTER(C.c_uint64))
+ALLREDUCE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
+
 
 def header_symbols():
     """every sx_* function declared in include/sphexa_hip.h"""
@@ -143,6 +148,13 @@ def lib():
         "sx_sim_scalars": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sx_sim_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_last_stats": (C.c_int, [vp, C.POINTER(SxNbStats)]),
+        "sx_sim_set_comm": (C.c_int, [vp, vp]),
+        "sx_sim_init_sedov_rank": (C.c_int, [vp, u32, C.c_int, C.c_int]),
+        "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_comm_unique_id": (C.c_int, [vp]),
+        "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
+        "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
+        "sx_comm_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -266,6 +278,73 @@ class DeviceState:
         self.dev[name].set(arr)
 
 
+class Comm:
+    """Inter-GPU transport. backend 'rccl' (RCCL over xGMI, production) or 'host' (staged through host memory and
+    torch.distributed -- used to run several ranks on one GPU in tests). torch.distributed must be initialised
+    (gloo) by the caller; it is only the control plane (unique-id broadcast) for 'rccl'."""
+
+    def __init__(self, backend="rccl"):
+        import torch
+        import torch.distributed as dist
+
+        self.L = lib()
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+        self.h = C.c_void_p()
+        if backend == "rccl":
+            uid = (C.c_uint8 * 128)()
+            if self.rank == 0:
+                rc = self.L.sx_comm_unique_id(uid)
+                if rc != SX_OK:
+                    raise SxError("ncclGetUniqueId failed")
+            t = torch.tensor(list(uid), dtype=torch.uint8)
+            dist.broadcast(t, 0)
+            for k in range(128):
+                uid[k] = int(t[k])
+            rc = self.L.sx_comm_create_rccl(C.byref(self.h), self.rank, self.size, uid)
+        else:
+            def a2a(user, send, sendBytes, recv, recvBytes):
+                try:
+                    sb = [int(sendBytes[q]) for q in range(self.size)]
+                    rb = [int(recvBytes[q]) for q in range(self.size)]
+                    src = np.ctypeslib.as_array((C.c_uint8 * max(1, sum(sb))).from_address(send)) if sum(sb) else \
+                        np.zeros(1, np.uint8)
+                    out = torch.empty(sum(rb), dtype=torch.uint8)
+                    dist.all_to_all_single(out, torch.from_numpy(src[:sum(sb)].copy()), rb, sb)
+                    if sum(rb):
+                        C.memmove(recv, out.numpy().ctypes.data, sum(rb))
+                    return 0
+                except Exception as e:  # noqa: BLE001 -- report through the return code
+                    print("alltoallv callback failed:", e)
+                    return 1
+
+            def allreduce(user, buf, count, op):
+                try:
+                    if op == 0:
+                        a = np.ctypeslib.as_array((C.c_uint32 * count).from_address(buf))
+                        t = torch.from_numpy(a.astype(np.int64))
+                        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                        a[:] = t.numpy().astype(np.uint32)
+                    else:
+                        a = np.ctypeslib.as_array((C.c_double * count).from_address(buf))
+                        t = torch.from_numpy(a.copy())
+                        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                        a[:] = t.numpy()
+                    return 0
+                except Exception as e:  # noqa: BLE001
+                    print("allreduce callback failed:", e)
+                    return 1
+
+            self._cbs = (ALLTOALLV_CB(a2a), ALLREDUCE_CB(allreduce))
+            rc = self.L.sx_comm_create_host(C.byref(self.h), self.rank, self.size, self._cbs[0], self._cbs[1], None)
+        if rc != SX_OK:
+            raise SxError(f"communicator creation failed ({backend}): {rc}")
+
+    def close(self):
+        if self.h:
+            self.L.sx_comm_destroy(self.h)
+            self.h = None
+
+
 class Sim:
     """device-resident VE propagator on one GPU (sx_sim_*)"""
 
@@ -278,8 +357,17 @@ class Sim:
         ctx.check(self.L.sx_sim_create(C.byref(self.h), ctx.h, int(capacity), C.byref(self.params), C.byref(box),
                                        bucket), "sx_sim_create")
 
-    def init_sedov(self, side):
-        self.ctx.check(self.L.sx_sim_init_sedov(self.h, side), "init_sedov")
+    def init_sedov(self, side, rank=0, size=1):
+        self.ctx.check(self.L.sx_sim_init_sedov_rank(self.h, side, rank, size), "init_sedov")
+
+    def set_comm(self, comm):
+        self.comm = comm
+        self.ctx.check(self.L.sx_sim_set_comm(self.h, comm.h), "set_comm")
+
+    def layout(self):
+        out = (C.c_uint64 * 4)()
+        self.L.sx_sim_layout(self.h, out)
+        return dict(first=out[0], last=out[1], n=out[2], haloRetries=out[3])
 
     def set_state(self, st, minDt=1e-6, minDt_m1=1e-6):
         arrs = [np.ascontiguousarray(st[k], dtype=t) for k, t in [

@@ -1,0 +1,70 @@
+"""Worker for the multi-rank tests (launched by torch.distributed.run with the gloo control plane).
+
+  python -m torch.distributed.run --nproc-per-node P --master-addr 127.0.0.1 --master-port X \
+      tests/dist_worker.py --out DIR [--backend host|rccl] [--side S] [--steps K] [--ic sedov|sedov_dev]
+
+Each rank owns an index slice of the IC, runs K distributed VE steps, and writes its local particles
+(id, nc, h and the compared float fields) plus scalars to DIR/rank<r>.npz.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sph-exa_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+FIELDS = ["x", "y", "z", "vx", "vy", "vz", "temp", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "xm", "kx", "prho", "c",
+          "divv", "c11", "c22", "c33", "du", "ax", "ay", "az"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--backend", default="host")
+    ap.add_argument("--side", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--ic", default="sedov")
+    args = ap.parse_args()
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    rank, size = dist.get_rank(), dist.get_world_size()
+    import pyoracle as po
+    import sphexa_amd as sx
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ctx = sx.Context(0 if args.backend == "host" else local)
+    comm = sx.Comm(args.backend)
+    st, obox = po.sedov_state(args.side)
+    box = sx.make_box(list(obox.lim), list(obox.bnd))
+    sim = sx.Sim(ctx, 2 * st.n // size + 4096, box)
+    sim.set_comm(comm)
+    if args.ic == "sedov_dev":
+        sim.init_sedov(args.side, rank, size)
+    else:
+        f, l = st.n * rank // size, st.n * (rank + 1) // size
+        sim.set_state({k: v[f:l] for k, v in st.arrays.items()}, st.minDt, st.minDt_m1)
+    out = {}
+    for s in range(args.steps):
+        sim.step()
+        got = sim.get(["id", "nc", "h"] + FIELDS)
+        for k, v in got.items():
+            out[f"s{s}_{k}"] = v
+        sc = sim.scalars()
+        out[f"s{s}_scalars"] = np.array([sc["minDt"], sc["minDt_m1"], sc["ttot"]])
+        lay = sim.layout()
+        out[f"s{s}_layout"] = np.array([lay["first"], lay["last"], lay["n"], lay["haloRetries"]])
+    np.savez(os.path.join(args.out, f"rank{rank}.npz"), **out)
+    sim.close()
+    comm.close()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
