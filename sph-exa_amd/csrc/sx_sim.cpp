@@ -986,6 +986,8 @@ extern "C"
                 chunkCheckKernel<<<grid(nl), 256, 0, st>>>(s->h + s->first, nl, s->work.get<ReqBox>("dom.mybox", 1),
                                                          margin, flg);
             unsigned hf = 0;
+            // the retry decision must be global: a rank redoing the sync alone would deadlock the collectives
+            SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
             SIM_HIP(hipMemcpyAsync(s->statsHost + 3, flg, 4, hipMemcpyDeviceToHost, st));
             SIM_HIP(hipStreamSynchronize(st));
             hf = s->statsHost[3];

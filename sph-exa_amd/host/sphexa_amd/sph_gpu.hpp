@@ -1,0 +1,264 @@
+/*! @file sph_gpu.hpp
+ * @brief C++20 mirror of SPH-EXA's GPU seam (sph/include/sph/sph_gpu.hpp:15-80) on top of libsphexa_hip.so.
+ *
+ * Drop-in for the `sph::cuda::compute*` functions that ve_hydro.hpp calls through the HaveGpu<Acc> dispatch
+ * (e.g. hydro_ve/xmass.hpp:69-74): same names, same argument meaning, same error behaviour (std::runtime_error with
+ * the reference messages of xmass_gpu.cu:126-127).  Header-only, no HIP or thrust dependency: the dataset is
+ * accessed duck-typed through `d.devData.<field>` (thrust::device_vector or anything with data()), `d.treeView`
+ * (cstone::OctreeNsView), and the ParticlesData scalar members (K, ng0, ngmax, Kcour, Krho, gamma, muiConst,
+ * alphamin, alphamax, decay_constant, Atmin, Atmax, ramp, minDt, minDtCourant).
+ *
+ * Replacing the reference's GPU kernels therefore means compiling this header instead of the hydro_ve
+ * `*_gpu.cu` translation units.
+ */
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+
+#include "sphexa_hip.h"
+
+namespace sphexa_amd
+{
+
+namespace detail
+{
+// raw device pointer of a thrust::device_vector (data().get()), a std::vector-like (data()) or a raw pointer
+template<class V>
+auto raw(V& v, int) -> decltype(v.data().get())
+{
+    return v.data().get();
+}
+template<class V>
+auto raw(V& v, long) -> decltype(v.data())
+{
+    return v.data();
+}
+template<class T>
+T* raw(T* p, int)
+{
+    return p;
+}
+template<class V>
+auto rawPtr(V& v)
+{
+    return (v.size() == 0) ? decltype(raw(v, 0)){nullptr} : raw(v, 0);
+}
+} // namespace detail
+
+//! one context per process (the reference uses the device exposed by the launcher, gpu_config.cuh:62-67)
+inline sx_ctx* context(int device = 0)
+{
+    static sx_ctx* ctx = [device] {
+        sx_ctx* c = nullptr;
+        if (sx_create(&c, device) != SX_OK) throw std::runtime_error("sphexa_amd: sx_create failed");
+        return c;
+    }();
+    return ctx;
+}
+
+inline void check(int rc, const char* what)
+{
+    if (rc == SX_OK) return;
+    if (rc == SX_ERR_TRAVERSAL) throw std::runtime_error("GPU traversal stack exhausted in neighbor search\n");
+    if (rc == SX_ERR_NOT_CONVERGED) throw std::runtime_error("coupled nc/h-updated failed to converge");
+    throw std::runtime_error(std::string(what) + ": " + sx_last_error(context()));
+}
+
+template<class Box>
+sx_box toBox(const Box& b)
+{
+    sx_box r{};
+    r.lim[0] = b.xmin(), r.lim[1] = b.xmax(), r.lim[2] = b.ymin(), r.lim[3] = b.ymax(), r.lim[4] = b.zmin(),
+    r.lim[5] = b.zmax();
+    r.bnd[0] = (int32_t)b.boundaryX(), r.bnd[1] = (int32_t)b.boundaryY(), r.bnd[2] = (int32_t)b.boundaryZ();
+    return r;
+}
+
+template<class Dataset>
+sx_params toParams(const Dataset& d)
+{
+    sx_params p{};
+    p.K              = d.K;
+    p.ng0            = d.ng0;
+    p.ngmax          = d.ngmax;
+    p.Kcour          = d.Kcour;
+    p.Krho           = d.Krho;
+    p.gamma          = d.gamma;
+    p.muiConst       = d.muiConst;
+    p.alphamin       = d.alphamin;
+    p.alphamax       = d.alphamax;
+    p.decay_constant = d.decay_constant;
+    p.Atmin          = d.Atmin;
+    p.Atmax          = d.Atmax;
+    p.ramp           = d.ramp;
+    p.maxDtIncrease  = 1.1;
+    return p;
+}
+
+//! DeviceParticlesData (particles_data_gpu.cuh:51-211) -> sx_fields, in the reference field order
+template<class Dataset>
+sx_fields toFields(Dataset& d)
+{
+    using detail::rawPtr;
+    auto&     dv = d.devData;
+    sx_fields f{};
+    f.n        = dv.x.size();
+    f.x        = rawPtr(dv.x);
+    f.y        = rawPtr(dv.y);
+    f.z        = rawPtr(dv.z);
+    f.x_m1     = rawPtr(dv.x_m1);
+    f.y_m1     = rawPtr(dv.y_m1);
+    f.z_m1     = rawPtr(dv.z_m1);
+    f.vx       = rawPtr(dv.vx);
+    f.vy       = rawPtr(dv.vy);
+    f.vz       = rawPtr(dv.vz);
+    f.rho      = rawPtr(dv.rho);
+    f.p        = rawPtr(dv.p);
+    f.prho     = rawPtr(dv.prho);
+    f.tdpdTrho = rawPtr(dv.tdpdTrho);
+    f.h        = rawPtr(dv.h);
+    f.m        = rawPtr(dv.m);
+    f.c        = rawPtr(dv.c);
+    f.ax       = rawPtr(dv.ax);
+    f.ay       = rawPtr(dv.ay);
+    f.az       = rawPtr(dv.az);
+    f.du       = rawPtr(dv.du);
+    f.du_m1    = rawPtr(dv.du_m1);
+    f.c11      = rawPtr(dv.c11);
+    f.c12      = rawPtr(dv.c12);
+    f.c13      = rawPtr(dv.c13);
+    f.c22      = rawPtr(dv.c22);
+    f.c23      = rawPtr(dv.c23);
+    f.c33      = rawPtr(dv.c33);
+    f.temp     = rawPtr(dv.temp);
+    f.xm       = rawPtr(dv.xm);
+    f.kx       = rawPtr(dv.kx);
+    f.divv     = rawPtr(dv.divv);
+    f.curlv    = (dv.curlv.size() == dv.x.size()) ? rawPtr(dv.curlv) : nullptr; // iad_divv_curlv.hpp:77
+    f.alpha    = rawPtr(dv.alpha);
+    f.gradh    = rawPtr(dv.gradh);
+    f.keys     = rawPtr(dv.keys);
+    f.nc       = rawPtr(dv.nc);
+    return f;
+}
+
+//! cstone::OctreeNsView<double, uint64_t> -> sx_tree (centers/sizes are Vec3<double> arrays)
+template<class TreeView>
+sx_tree toTree(const TreeView& t)
+{
+    sx_tree r{};
+    r.numLeafNodes    = t.numLeafNodes;
+    r.prefixes        = reinterpret_cast<const uint64_t*>(t.prefixes);
+    r.childOffsets    = t.childOffsets;
+    r.internalToLeaf  = t.internalToLeaf;
+    r.levelRange      = t.levelRange;
+    r.leaves          = reinterpret_cast<const uint64_t*>(t.leaves);
+    r.layout          = t.layout;
+    r.centers         = reinterpret_cast<const double*>(t.centers);
+    r.sizes           = reinterpret_cast<const double*>(t.sizes);
+    r.searchExtFactor = t.searchExtFactor;
+    return r;
+}
+
+template<class GroupView>
+sx_groups toGroups(const GroupView& g)
+{
+    return sx_groups{(uint32_t)g.firstBody, (uint32_t)g.lastBody, (uint32_t)g.numGroups, g.groupStart, g.groupEnd};
+}
+
+} // namespace sphexa_amd
+
+namespace sph::cuda
+{
+
+//! sph_gpu.hpp:25 -- neighbor search + h-nc iteration + xm (xmass_gpu.cu:103-128)
+template<class GroupView, class Dataset, class Box>
+void computeXMass(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    auto t = sa::toTree(d.treeView);
+    sa::check(sx_xmass(sa::context(), &g, &f, &p, &b, &t), "computeXMass");
+}
+
+//! sph_gpu.hpp:37 (ve_def_gradh_gpu.cu:86)
+template<class GroupView, class Dataset, class Box>
+void computeVeDefGradh(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    sa::check(sx_ve_def_gradh(sa::context(), &g, &f, &p, &b), "computeVeDefGradh");
+}
+
+//! sph_gpu.hpp:40-43 (hydro_ve/eos_gpu.cu:74)
+template<class Tt, class Tm, class Thydro>
+void computeEOS(size_t firstParticle, size_t lastParticle, Tm mui, double gamma, const Tt* temp, const Tm* m,
+                const Thydro* kx, const Thydro* xm, const Thydro* gradh, Thydro* prho, Thydro* c, Thydro* rho,
+                Thydro* p)
+{
+    namespace sa = sphexa_amd;
+    sa::check(sx_eos(sa::context(), (uint32_t)firstParticle, (uint32_t)lastParticle, (float)mui, gamma, temp, m, kx,
+                     xm, gradh, prho, c, rho, p),
+              "computeEOS");
+}
+
+//! sph_gpu.hpp:45 (iad_divv_curlv_gpu.cu:91)
+template<class GroupView, class Dataset, class Box>
+void computeIadDivvCurlv(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    sa::check(sx_iad_divv_curlv(sa::context(), &g, &f, &p, &b), "computeIadDivvCurlv");
+}
+
+//! sph_gpu.hpp:48 (av_switches_gpu.cu:103); uses d.minDt like the reference
+template<class GroupView, class Dataset, class Box>
+void computeAVswitches(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    sa::check(sx_av_switches(sa::context(), &g, &f, &p, &b, d.minDt), "computeAVswitches");
+}
+
+//! sph_gpu.hpp:51-53 (momentum_energy_gpu.cu:121-145): writes ax,ay,az,du and d.minDtCourant
+template<bool avClean, class GroupView, class Dataset, class Box>
+void computeMomentumEnergy(const GroupView& grp, float* groupDt, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    static_assert(!avClean, "the AV-cleaning momentum variant is not provided by libsphexa_hip (DESIGN.md 9)");
+    auto  g = sa::toGroups(grp);
+    auto  f = sa::toFields(d);
+    auto  p = sa::toParams(d);
+    auto  b = sa::toBox(box);
+    float minDt;
+    sa::check(sx_momentum_energy(sa::context(), &g, groupDt, &f, &p, &b, &minDt), "computeMomentumEnergy");
+    d.minDtCourant = minDt;
+}
+
+//! sph_gpu.hpp:78 (update_h_gpu.cu:49-60)
+template<class GroupView, class Th>
+void updateSmoothingLengthGpu(const GroupView& grp, unsigned ng0, const unsigned* nc, Th* h)
+{
+    namespace sa = sphexa_amd;
+    sa::check(sx_update_h(sa::context(), (uint32_t)grp.firstBody, (uint32_t)grp.lastBody, ng0, nc, h),
+              "updateSmoothingLengthGpu");
+}
+
+} // namespace sph::cuda
