@@ -152,6 +152,7 @@ def main():
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
         "neighbors_per_particle": ng,
         "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),
+        "union_per_particle": stats["sumUnion"] / max(1, n_local),
         "minDt": sc["minDt"],
     }
     if rank == 0 and not args.no_cpu_baseline:

@@ -150,6 +150,7 @@ typedef struct sx_nbstats
     uint32_t maxNeighbors;   /* max true count (excluding self) */
     uint32_t numFailed;      /* h-nc iteration failures */
     uint64_t sumCandidates;  /* candidate particles tested (per target, summed) */
+    uint64_t sumUnion;       /* cluster neighbor-union entries, summed over 256-particle clusters */
 } sx_nbstats;
 
 typedef struct sx_ctx sx_ctx;

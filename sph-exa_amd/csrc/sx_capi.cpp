@@ -114,13 +114,13 @@ struct sx_ctx
     double      K{0};
     std::string err;
 
-    // neighbor-list cache
-    uint32_t* nidx{nullptr};
+    // neighbor-list cache (cluster lists from a search, global lists from an import)
+    NbLists   nb;
     uint32_t  nbFirst{0}, nbLast{0}, nbNgmax{0};
     bool      nbValid{false};
     size_t    nbFields{0};
 
-    uint32_t* stats{nullptr}; // device, 8 words
+    uint32_t* stats{nullptr}; // device, kStatsWords words
     uint32_t* statsHost{nullptr};
     float*    minDt{nullptr}; // device scalar
     unsigned* maxU{nullptr};  // device scalar
@@ -163,12 +163,6 @@ static int fail(sx_ctx* c, int code, const std::string& msg)
         if (e_ != hipSuccess) return fail(ctx, SX_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));         \
     } while (0)
 
-static uint32_t* ensureNidx(sx_ctx* c, uint32_t first, uint32_t last, uint32_t ngmax)
-{
-    size_t groups = (size_t(last - first) + kGroupSize - 1) / kGroupSize;
-    c->nidx       = c->arena.get<uint32_t>("nidx", std::max<size_t>(1, groups) * ngmax * kWave);
-    return c->nidx;
-}
 
 extern "C"
 {
@@ -200,8 +194,8 @@ extern "C"
         c->whd = c->arena.get<float2>("tables.whd", kTableSize);
         tablePairs(tmp, c->wh, c->stream);
         tablePairs(tmp + kTableSize, c->whd, c->stream);
-        c->stats      = c->arena.get<uint32_t>("stats", 8);
-        c->statsHost  = c->arena.pinned<uint32_t>("statsHost", 8);
+        c->stats      = c->arena.get<uint32_t>("stats", kStatsWords);
+        c->statsHost  = c->arena.pinned<uint32_t>("statsHost", kStatsWords);
         c->minDt      = c->arena.get<float>("minDt", 1);
         c->maxU       = c->arena.get<unsigned>("maxU", 1);
         c->hostScalar = c->arena.pinned<float>("hostScalar", 2);
@@ -372,7 +366,6 @@ extern "C"
         a.z              = f->z;
         a.h              = f->h;
         a.nc             = f->nc;
-        a.nidx           = ensureNidx(c, first, last, p->ngmax);
         a.childOffsets   = tree->childOffsets;
         a.internalToLeaf = tree->internalToLeaf;
         a.layout         = tree->layout;
@@ -382,10 +375,12 @@ extern "C"
         a.margin         = quantMargin(a.box);
         a.stats          = c->stats;
         a.powTab         = ensurePowTab(c, p->ng0);
-        if (!a.nidx || !a.powTab) return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
-        SX_HIP(c, hipMemsetAsync(c->stats, 0, 32, c->stream));
+        if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab)
+            return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
+        a.setLists(c->nb);
+        SX_HIP(c, hipMemsetAsync(c->stats, 0, kStatsWords * 4, c->stream));
         SX_HIP(c, findNeighbors(a, c->stream));
-        SX_HIP(c, hipMemcpyAsync(c->statsHost, c->stats, 32, hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipMemcpyAsync(c->statsHost, c->stats, kStatsWords * 4, hipMemcpyDeviceToHost, c->stream));
         SX_HIP(c, hipStreamSynchronize(c->stream));
         c->nbFirst = first;
         c->nbLast  = last;
@@ -397,6 +392,7 @@ extern "C"
             stats->maxNeighbors  = c->statsHost[2];
             stats->sumNeighbors  = *reinterpret_cast<uint64_t*>(c->statsHost + 4);
             stats->sumCandidates = *reinterpret_cast<uint64_t*>(c->statsHost + 6);
+            stats->sumUnion      = *reinterpret_cast<uint64_t*>(c->statsHost + 8);
         }
         if (c->statsHost[0] & 1u) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in neighbor search");
         if (iterate_h && c->statsHost[1]) return fail(c, SX_ERR_NOT_CONVERGED, "coupled nc/h-updated failed to converge");
@@ -408,15 +404,18 @@ extern "C"
     {
         if (!c->nbValid || first != c->nbFirst || last != c->nbLast || ngmax != c->nbNgmax)
             return fail(c, SX_ERR_ARG, "sx_export_neighbors: no matching neighbor list");
-        SX_HIP(c, exportNeighbors(c->nidx, nc, first, last, ngmax, out, c->stream));
+        NsArgs a{};
+        a.first = first, a.last = last, a.ngmax = ngmax, a.nc = const_cast<uint32_t*>(nc);
+        a.setLists(c->nb);
+        SX_HIP(c, exportNeighbors(a, out, c->stream));
         return SX_OK;
     }
 
     int sx_import_neighbors(sx_ctx* c, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in)
     {
-        uint32_t* nidx = ensureNidx(c, first, last, ngmax);
-        if (!nidx) return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
-        SX_HIP(c, importNeighbors(nidx, first, last, ngmax, in, c->stream));
+        if (!c->nb.reserve(c->arena, first, last, ngmax, false))
+            return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
+        SX_HIP(c, importNeighbors(c->nb.nidx, first, last, ngmax, in, c->stream));
         c->nbFirst = first;
         c->nbLast  = last;
         c->nbNgmax = ngmax;
@@ -459,7 +458,12 @@ PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_pa
     a.last           = g->lastBody;
     a.numGroups      = (g->lastBody - g->firstBody + kGroupSize - 1) / kGroupSize;
     a.ngmax          = p->ngmax;
-    a.nidx           = c->nidx;
+    a.localLists     = c->nb.local;
+    a.nidx           = c->nb.nidx;
+    a.nloc           = c->nb.nloc;
+    a.uni            = c->nb.uni;
+    a.ucount         = c->nb.ucount;
+    a.ucap           = c->nb.ucap;
     a.nc             = f->nc;
     a.rx             = r.rx;
     a.rv             = r.rv;

@@ -19,6 +19,13 @@ constexpr int kWave       = 64;    // CDNA4 wavefront
 constexpr int kTableSize  = 20000; // sph::lt::kTableSize (table_lookup.hpp:12)
 constexpr int kMaxLevel   = 21;    // maxTreeLevel<uint64_t>
 constexpr int kGroupSize  = 64;    // particles per neighbor-list block = one wavefront
+constexpr int kClusterWaves = 4;   // groups per cluster = waves per cluster workgroup
+constexpr int kCluster      = kGroupSize * kClusterWaves; // particles sharing one neighbor union
+
+//! words of u16 cluster-local neighbor positions per target (two per word)
+__host__ __device__ constexpr uint32_t nlocWords(uint32_t ngmax) { return (ngmax + 1) / 2; }
+//! union capacity per cluster: every union entry is a stored neighbor of at least one of its targets
+__host__ __device__ constexpr uint32_t unionCap(uint32_t ngmax) { return kCluster * ngmax; }
 
 //! box data as the kernels need it (cstone::Box<double>, sfc/box.hpp:111-191)
 struct DevBox
@@ -154,6 +161,18 @@ __device__ __forceinline__ T waveSum(T v)
     for (int o = 32; o > 0; o >>= 1)
         v += __shfl_xor(v, o, kWave);
     return v;
+}
+
+__device__ __forceinline__ uint64_t waveOr64(uint64_t v)
+{
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+    {
+        lo |= (uint32_t)__shfl_xor((int)lo, o, kWave);
+        hi |= (uint32_t)__shfl_xor((int)hi, o, kWave);
+    }
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ double readlaneD(double v, int k)

@@ -2,13 +2,16 @@
  * @brief VE hydro kernels for gfx950: XMass, VeDefGradh, IAD + divv/curlv, AV switches, momentum + energy,
  *        EOS, position/energy integration and h update.
  *
- * Pair kernels: one wavefront per 64-particle SFC block, one lane per target particle; each lane walks its own
- * neighbor list (lane-interleaved, nidx[(block*ngmax + k)*64 + lane], coalesced 256 B per k) and gathers the
+ * Gather kernels: one wavefront per 64-particle SFC block, one lane per target particle; each lane walks its own
+ * neighbor list (lane-interleaved, nidx[(block*ngmax + k)*64 + lane], coalesced 256 B per k, or the cluster
+ * union positions of sx_neighbors.hip resolved through uni[]) and gathers the
  * neighbor's packed 16-byte-aligned records (RecX 32 B, RecV/RecT 16 B, RecC 32 B) -- 1-2 dwordx4 per record
  * instead of one dword gather per SoA field.  Tables are {t[i], t[i+1]-t[i]} pairs: one 8-byte gather per lookup.
  *
  * The per-pair arithmetic is the reference's, expression by expression (citations per kernel; the CPU
- * restatement with identical structure is oracle/sph_oracle.c).  Compiled twice, see sx_hydro.hpp.
+ * restatement with identical structure is oracle/sph_oracle.c).  Compiled twice, see sx_hydro.hpp.  The exact
+ * variant always runs these kernels; the fast variant runs them only on global (imported) lists and otherwise the
+ * LDS-staged cluster kernels of sx_hydro_cluster.hip.
  */
 #include "sx_hydro.hpp"
 
@@ -22,6 +25,9 @@ namespace SX_VARIANT
 {
 
 constexpr int kBlock = 256;
+#define SX_STR2(x) #x
+#define SX_STR(x) SX_STR2(x)
+constexpr bool kFastClusters = SX_STR(SX_VARIANT)[0] == 'f';
 
 #define SX_PAIR_PROLOGUE                                                                                               \
     const uint32_t gw   = (xcdBlock(blockIdx.x, gridDim.x) * kBlock + threadIdx.x) >> 6;                               \
@@ -34,7 +40,14 @@ constexpr int kBlock = 256;
         unsigned c1 = a.nc[i] - 1;                                                                                     \
         cnt         = c1 < a.ngmax ? c1 : a.ngmax;                                                                     \
     }                                                                                                                  \
-    const uint32_t* nb = a.nidx + (size_t)gw * a.ngmax * kWave + lane;
+    const uint32_t* nb = a.localLists ? a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane                       \
+                                      : a.nidx + (size_t)gw * a.ngmax * kWave + lane;                                 \
+    const uint32_t* un = a.localLists ? a.uni + (size_t)(gw / kClusterWaves) * a.ucap : nullptr;                       \
+    auto nbj = [&](unsigned k) -> uint32_t {                                                                           \
+        if (!a.localLists) return nb[(size_t)k * kWave];                                                               \
+        uint32_t w = nb[(size_t)(k >> 1) * kWave];                                                                     \
+        return un[(k & 1) ? (w >> 16) : (w & 0xffffu)];                                                                \
+    };
 
 //! xmassJLoop (hydro_ve/xmass_kern.hpp:50-79)
 __global__ __launch_bounds__(kBlock) void xmassKernel(PairArgs a)
@@ -47,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(PairArgs a)
     float      rho0i = ri.m;
     for (unsigned k = 0; k < cnt; ++k)
     {
-        uint32_t   j  = nb[k * kWave];
+        uint32_t   j  = nbj(k);
         const RecX rj = a.rx[j];
         float      xx = (float)(ri.x - rj.x);
         float      yy = (float)(ri.y - rj.y);
@@ -75,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(PairArgs a)
     float      wrho0i   = -3.0f * ri.m;
     for (unsigned k = 0; k < cnt; ++k)
     {
-        uint32_t   j  = nb[k * kWave];
+        uint32_t   j  = nbj(k);
         const RecX rj = a.rx[j];
         float      xmassj = a.rt[j].xm;
         float      xx = (float)(ri.x - rj.x);
@@ -116,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(PairArgs a)
     float      t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
     for (unsigned k = 0; k < cnt; ++k)
     {
-        uint32_t   j  = nb[k * kWave];
+        uint32_t   j  = nbj(k);
         const RecX rj = a.rx[j];
         const RecT tj = a.rt[j];
         float      rx = (float)(ri.x - rj.x);
@@ -163,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(PairArgs a)
     float dVx0 = 0, dVx1 = 0, dVx2 = 0, dVy0 = 0, dVy1 = 0, dVy2 = 0, dVz0 = 0, dVz1 = 0, dVz2 = 0;
     for (unsigned k = 0; k < cnt; ++k)
     {
-        uint32_t   j  = nb[k * kWave];
+        uint32_t   j  = nbj(k);
         const RecX rj = a.rx[j];
         const RecV vj = a.rv[j];
         float      xmassj = a.rt[j].xm;
@@ -217,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(PairArgs a)
     float      gx = 0, gy = 0, gz = 0;
     for (unsigned k = 0; k < cnt; ++k)
     {
-        uint32_t   j  = nb[k * kWave];
+        uint32_t   j  = nbj(k);
         const RecX rj = a.rx[j];
         const RecV vj = a.rv[j];
         const RecT tj = a.rt[j];
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
         float      mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
         for (unsigned k = 0; k < cnt; ++k)
         {
-            uint32_t   j  = nb[k * kWave];
+            uint32_t   j  = nbj(k);
             const RecX rj = a.rx[j];
             const RecV vj = a.rv[j];
             const RecT tj = a.rt[j];
@@ -476,22 +489,27 @@ static inline unsigned pairGrid(const PairArgs& a) { return (a.numGroups * kWave
 
 static void launchXmass(const PairArgs& a, hipStream_t s)
 {
+    if (kFastClusters && a.localLists) return cluster::xmass(a, s);
     if (a.numGroups) xmassKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchVeDefGradh(const PairArgs& a, hipStream_t s)
 {
+    if (kFastClusters && a.localLists) return cluster::veDefGradh(a, s);
     if (a.numGroups) veDefGradhKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchIad(const PairArgs& a, hipStream_t s)
 {
+    if (kFastClusters && a.localLists) return cluster::iadDivvCurlv(a, s);
     if (a.numGroups) iadDivvCurlvKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchAv(const PairArgs& a, hipStream_t s)
 {
+    if (kFastClusters && a.localLists) return cluster::avSwitches(a, s);
     if (a.numGroups) avSwitchesKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchMomentum(const PairArgs& a, hipStream_t s)
 {
+    if (kFastClusters && a.localLists) return cluster::momentumEnergy(a, s);
     if (a.numGroups) momentumEnergyKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchEos(const EosArgs& a, hipStream_t s)

@@ -15,7 +15,14 @@ namespace sx
 struct PairArgs
 {
     uint32_t first, last, numGroups, ngmax;
-    const uint32_t* nidx; // [group][k][lane]
+    // neighbor lists (NbLists, sx_tree.hpp): global nidx[group][k][lane], or, with localLists, the cluster unions
+    // uni[cluster*ucap + u] (ucount[cluster] entries) and u16 positions nloc[group][k/2][lane]
+    int             localLists;
+    const uint32_t* nidx;
+    const uint32_t* nloc;
+    const uint32_t* uni;
+    const uint32_t* ucount;
+    uint32_t        ucap;
     const uint32_t* nc;   // includes self
     const RecX*     rx;
     const RecV*     rv;
@@ -81,5 +88,16 @@ struct HydroLaunch
 
 const HydroLaunch& hydro_exact();
 const HydroLaunch& hydro_fast();
+
+//! fast-variant pair kernels on cluster lists (sx_hydro_cluster.hip): one workgroup per 256-particle cluster, the
+//! cluster's neighbor union staged in LDS, the kernel W evaluated in registers
+namespace cluster
+{
+void xmass(const PairArgs&, hipStream_t);
+void veDefGradh(const PairArgs&, hipStream_t);
+void iadDivvCurlv(const PairArgs&, hipStream_t);
+void avSwitches(const PairArgs&, hipStream_t);
+void momentumEnergy(const PairArgs&, hipStream_t);
+} // namespace cluster
 
 } // namespace sx

@@ -1,0 +1,598 @@
+/*! @file sx_hydro_cluster.hip
+ * @brief Fast-variant VE pair kernels on cluster neighbor lists (gfx950): XMass, VeDefGradh, IAD + divv/curlv,
+ *        AV switches, momentum + energy.
+ *
+ * One 256-thread workgroup per 256-particle SFC cluster (four wave64 groups, one lane per target).  The neighbor
+ * search (sx_neighbors.hip) leaves, per cluster, the UNION of its targets' neighbors (uni[], typically 6-7 entries
+ * per target instead of ~120 per target) and, per target, u16 positions into it, two per word, lane-interleaved.
+ *
+ *   1. stage: the workgroup gathers the union's packed records (coalesced runs: the union is in leaf order) and
+ *      writes one compact LDS record per union entry: positions relative to the cluster origin (minimum image,
+ *      folded in double, rounded to float) plus the per-kernel neighbor fields, derived quantities precomputed
+ *      (vol = xm/kx, rho = kx*m/xm, 1/h, m/rho);
+ *   2. each lane walks its position list (one coalesced 256-B word load per two neighbors, prefetched four words
+ *      ahead) and reads its neighbors' records from LDS (ds_read_b128); the SPH kernel W(v) = sinc(pi v/2)^6 and
+ *      dW/dv are evaluated in registers with a degree-6 polynomial in v^2 (|error| < 2e-7 over [0,2), the same
+ *      order as the reference's 20000-point table interpolation), so the inner loop touches no global memory;
+ *   3. unions larger than the LDS capacity CH are processed in CH-sized chunks, every lane advancing through its
+ *      sorted position list chunk by chunk.
+ *
+ * The per-pair arithmetic follows the reference kernels (citations per kernel) in float with FMA contraction and
+ * reciprocal multiplies; results agree with the CPU reference to float rounding (tests/test_gpu_parity.py states
+ * the tolerance).  Bit-reproducible results come from the exact variant (sx_hydro.hip, -ffp-contract=off).
+ */
+#include "sx_hydro.hpp"
+#include "sx_traverse.hpp"
+
+namespace sx
+{
+namespace cluster
+{
+
+constexpr int kB = kCluster; // threads per workgroup
+
+//! sinc(pi v / 2) as a polynomial in t = v^2 on [0, 2] (least squares, sx_hydro_cluster.hip header)
+__device__ __forceinline__ float sincPoly(float t)
+{
+    float s = 3.08339593857454e-08f;
+    s       = fmaf(s, t, -2.262898533444968e-06f);
+    s       = fmaf(s, t, 0.00010206655861111358f);
+    s       = fmaf(s, t, -0.0029803994111716747f);
+    s       = fmaf(s, t, 0.050733841955661774f);
+    s       = fmaf(s, t, -0.411233514547348f);
+    return fmaf(s, t, 1.0f);
+}
+//! (d/dv sinc(pi v / 2)) / v as a polynomial in t = v^2
+__device__ __forceinline__ float dsincPolyOverV(float t)
+{
+    float s = 5.004272196629245e-08f;
+    s       = fmaf(s, t, -2.7139270741827204e-07f);
+    s       = fmaf(s, t, -1.9479362890706398e-05f);
+    s       = fmaf(s, t, 0.0008091478957794607f);
+    s       = fmaf(s, t, -0.01787404529750347f);
+    s       = fmaf(s, t, 0.20293137431144714f);
+    return fmaf(s, t, -0.8224664926528931f);
+}
+//! W(v) = sinc6 (sph_kernel_tables.hpp:27-40); 0 beyond the support like lt::lookup's last interval
+__device__ __forceinline__ float kernelW(float v)
+{
+    float s  = sincPoly(v * v);
+    float s2 = s * s;
+    return v < 2.0f ? s2 * s2 * s2 : 0.0f;
+}
+//! W and dW/dv = 6 sinc^5 sinc' (sinc6d)
+__device__ __forceinline__ void kernelWdW(float v, float& w, float& dw)
+{
+    float t  = v * v;
+    float s  = sincPoly(t);
+    float s2 = s * s;
+    float s4 = s2 * s2;
+    bool  in = v < 2.0f;
+    w        = in ? s4 * s2 : 0.0f;
+    dw       = in ? 6.0f * s4 * s * v * dsincPolyOverV(t) : 0.0f;
+}
+
+//! per-workgroup cluster bookkeeping
+struct Clu
+{
+    uint32_t        c, gw, i, iSafe, U;
+    bool            valid;
+    unsigned        cnt;
+    const uint32_t* un; // union of this cluster
+    const uint32_t* nl; // this lane's position words, stride 64
+    double          ox, oy, oz;
+    bool            pbc; // positions need the applyPBC rule after folding (tiny periodic boxes)
+};
+
+__device__ __forceinline__ float relc(double x, double o, const DevBox& b, int k) { return (float)foldPbc(x - o, b, k); }
+
+//! sets up the cluster and decides (workgroup-uniformly) whether folded coordinates are minimum-image for every
+//! neighbor pair: |x_i - o| + 2 h_i < L/2 on every periodic axis
+__device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
+{
+    Clu            cu;
+    const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    cu.c                = xcdBlock(blockIdx.x, gridDim.x);
+    cu.gw               = cu.c * kClusterWaves + wave;
+    const uint32_t c0   = a.first + cu.c * kCluster;
+    cu.i                = c0 + threadIdx.x;
+    cu.valid            = cu.gw < a.numGroups && cu.i < a.last;
+    cu.iSafe            = cu.valid ? cu.i : c0;
+    cu.cnt              = 0;
+    if (cu.valid)
+    {
+        unsigned c1 = a.nc[cu.i] - 1;
+        cu.cnt      = c1 < a.ngmax ? c1 : a.ngmax;
+    }
+    cu.U  = a.ucount[cu.c];
+    cu.un = a.uni + (size_t)cu.c * a.ucap;
+    cu.nl = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
+    const RecX o = a.rx[c0];
+    cu.ox = o.x, cu.oy = o.y, cu.oz = o.z;
+
+    const RecX r    = a.rx[cu.iSafe];
+    const float h2  = 2.0f * r.h;
+    float       ext = 0.0f;
+    if (a.box.pbc[0]) ext = fmaxf(ext, (fabsf(relc(r.x, cu.ox, a.box, 0)) + h2) * (float)a.box.il[0]);
+    if (a.box.pbc[1]) ext = fmaxf(ext, (fabsf(relc(r.y, cu.oy, a.box, 1)) + h2) * (float)a.box.il[1]);
+    if (a.box.pbc[2]) ext = fmaxf(ext, (fabsf(relc(r.z, cu.oz, a.box, 2)) + h2) * (float)a.box.il[2]);
+    ext = waveMax(ext);
+    if (lane == 0) s_red[wave] = ext;
+    __syncthreads();
+    float e = s_red[0];
+    for (int w = 1; w < kClusterWaves; ++w)
+        e = fmaxf(e, s_red[w]);
+    cu.pbc = __builtin_amdgcn_readfirstlane(e >= 0.49f ? 1 : 0);
+    return cu;
+}
+
+/*! Run body(p) over this lane's neighbors, p = LDS slot.  stage(j, slot) writes the record of particle j.
+ *  `resident` carries "the whole union is already in LDS" from a previous pass over the same records. */
+template<int CH, class Stage, class Body>
+__device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Body&& body, bool& resident)
+{
+    constexpr int S = (CH + kB - 1) / kB;
+    auto          fill = [&](uint32_t b0, uint32_t b1) {
+        uint32_t js[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+        {
+            const uint32_t u = b0 + threadIdx.x + s * kB;
+            js[s]            = u < b1 ? cu.un[u] : 0u;
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+        {
+            const uint32_t u = b0 + threadIdx.x + s * kB;
+            if (u < b1) stage(js[s], u - b0);
+        }
+    };
+
+    if (cu.U <= (uint32_t)CH)
+    {
+        if (!resident)
+        {
+            fill(0, cu.U);
+            __syncthreads();
+            resident = true;
+        }
+        const uint32_t  nw = (cu.cnt + 1) >> 1;
+        const uint32_t* nl = cu.nl;
+        uint32_t        q0 = 0 < nw ? nl[0] : 0u;
+        uint32_t        q1 = 1 < nw ? nl[kWave] : 0u;
+        uint32_t        q2 = 2 < nw ? nl[2 * kWave] : 0u;
+        uint32_t        q3 = 3 < nw ? nl[3 * kWave] : 0u;
+        for (uint32_t w = 0; w < nw; ++w)
+        {
+            const uint32_t cur = q0;
+            q0                 = q1;
+            q1                 = q2;
+            q2                 = q3;
+            q3                 = (w + 4 < nw) ? nl[(size_t)(w + 4) * kWave] : 0u;
+            body(cur & 0xffffu);
+            if (2 * w + 1 < cu.cnt) body(cur >> 16);
+        }
+    }
+    else
+    {
+        resident   = false;
+        uint32_t k = 0;
+        for (uint32_t b0 = 0; b0 < cu.U; b0 += CH)
+        {
+            const uint32_t b1 = min(cu.U, b0 + (uint32_t)CH);
+            __syncthreads();
+            fill(b0, b1);
+            __syncthreads();
+            while (k < cu.cnt)
+            {
+                const uint32_t w = cu.nl[(size_t)(k >> 1) * kWave];
+                const uint32_t p = (k & 1) ? (w >> 16) : (w & 0xffffu);
+                if (p >= b1) break;
+                body(p - b0);
+                ++k;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void pbcRule(const Clu& cu, const DevBox& b, float r, float& x, float& y, float& z)
+{
+    if (cu.pbc) applyPBC(b, r, x, y, z);
+}
+
+// ---- XMass: xmassJLoop (hydro_ve/xmass_kern.hpp:50-79) ----------------------------------------------------------
+template<int CH>
+__global__ __launch_bounds__(kB) void xmassKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH];
+    __shared__ float  s_red[kClusterWaves];
+    const Clu  cu = setup(a, s_red);
+    const RecX ri = a.rx[cu.iSafe];
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
+    float       rho0 = ri.m;
+    bool        res  = false;
+    neighborLoop<CH>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r = a.rx[j];
+            sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2), r.m);
+        },
+        [&](uint32_t p) {
+            const float4 q  = sP[p];
+            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+            rho0 += kernelW(dist * hInv) * q.w;
+        },
+        res);
+    if (cu.valid)
+    {
+        const float h3Inv = hInv * hInv * hInv;
+        a.xm[cu.i]        = (float)((double)ri.m / ((double)rho0 * a.K * (double)h3Inv));
+    }
+}
+
+// ---- VeDefGradh: veDefGradhJLoop (hydro_ve/ve_def_gradh_kern.hpp:43-90) -----------------------------------------
+template<int CH>
+__global__ __launch_bounds__(kB) void veDefGradhKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH];
+    __shared__ float  sX[CH];
+    __shared__ float  s_red[kClusterWaves];
+    const Clu   cu     = setup(a, s_red);
+    const RecX  ri     = a.rx[cu.iSafe];
+    const float xmassi = a.rt[cu.iSafe].xm;
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
+    float       kxi = xmassi, whomegai = -3.0f * xmassi, wrho0i = -3.0f * ri.m;
+    bool        res = false;
+    neighborLoop<CH>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r = a.rx[j];
+            sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2), r.m);
+            sX[slot] = a.rt[j].xm;
+        },
+        [&](uint32_t p) {
+            const float4 q      = sP[p];
+            const float  xmassj = sX[p];
+            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+            const float vloc = dist * hInv;
+            float       w, dw;
+            kernelWdW(vloc, w, dw);
+            const float dterh = -(3.0f * w + vloc * dw);
+            kxi += w * xmassj;
+            whomegai += dterh * xmassj;
+            wrho0i += dterh * q.w;
+        },
+        res);
+    if (cu.valid)
+    {
+        const double K     = a.K;
+        const float  h3Inv = hInv * hInv * hInv;
+        kxi                = (float)((double)kxi * (K * (double)h3Inv));
+        whomegai           = (float)((double)whomegai * (K * (double)h3Inv * (double)hInv));
+        wrho0i             = (float)((double)wrho0i * (K * (double)h3Inv * (double)hInv));
+        whomegai           = (float)((double)(whomegai * ri.m / xmassi) +
+                           ((double)kxi - K * (double)xmassi * (double)h3Inv) * (double)wrho0i);
+        const float rhoi   = kxi * ri.m / xmassi;
+        const float dhdrho = -ri.h / (rhoi * 3.0f);
+        a.kx[cu.i]         = kxi;
+        a.gradh[cu.i]      = 1.0f - dhdrho * whomegai;
+    }
+}
+
+// ---- IAD + divv/curlv: IADJLoop (iad_kern.hpp:43-109) + divV_curlVJLoop (divv_curlv_kern.hpp:43-123) -------------
+template<int CH>
+__global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH]; // x, y, z, vol = xm/kx
+    __shared__ float4 sV[CH]; // vx, vy, vz, xm
+    __shared__ float  s_red[kClusterWaves];
+    const Clu   cu  = setup(a, s_red);
+    const RecX  ri  = a.rx[cu.iSafe];
+    const RecV  vi  = a.rv[cu.iSafe];
+    const float kxi = a.rt[cu.iSafe].kx;
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hi = ri.h, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    auto        stage = [&](uint32_t j, uint32_t slot) {
+        const RecX r = a.rx[j];
+        const RecV v = a.rv[j];
+        const RecT t = a.rt[j];
+        sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
+                               t.xm / t.kx);
+        sV[slot]     = make_float4(v.vx, v.vy, v.vz, t.xm);
+    };
+    float t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
+    bool  res = false;
+    neighborLoop<CH>(
+        cu, stage,
+        [&](uint32_t p) {
+            const float4 q  = sP[p];
+            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
+            const float volj_w = q.w * kernelW(dist * hiInv);
+            t11 += rx * rx * volj_w;
+            t12 += rx * ry * volj_w;
+            t13 += rx * rz * volj_w;
+            t22 += ry * ry * volj_w;
+            t23 += ry * rz * volj_w;
+            t33 += rz * rz * volj_w;
+        },
+        res);
+    auto  getExp    = [](float v) { return v == 0.0f ? 0 : ilogbf(v); };
+    int   tauExpSum = getExp(t11) + getExp(t12) + getExp(t13) + getExp(t22) + getExp(t23) + getExp(t33);
+    float nrm       = ldexpf(1.0f, -tauExpSum / 6);
+    t11 *= nrm, t12 *= nrm, t13 *= nrm, t22 *= nrm, t23 *= nrm, t33 *= nrm;
+    const float det = t11 * t22 * t33 + 2.0f * t12 * t23 * t13 - t11 * t23 * t23 - t22 * t13 * t13 - t33 * t12 * t12;
+    const float factor = (float)((double)(nrm * (hi * hi * hi)) / ((double)det * a.K));
+    const float c11i   = (t22 * t33 - t23 * t23) * factor;
+    const float c12i   = (t13 * t23 - t33 * t12) * factor;
+    const float c13i   = (t12 * t23 - t22 * t13) * factor;
+    const float c22i   = (t11 * t33 - t13 * t13) * factor;
+    const float c23i   = (t13 * t12 - t11 * t23) * factor;
+    const float c33i   = (t11 * t22 - t12 * t12) * factor;
+
+    float dVx0 = 0, dVx1 = 0, dVx2 = 0, dVy0 = 0, dVy1 = 0, dVy2 = 0, dVz0 = 0, dVz1 = 0, dVz2 = 0;
+    neighborLoop<CH>(
+        cu, stage,
+        [&](uint32_t p) {
+            const float4 q  = sP[p];
+            const float4 v  = sV[p];
+            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
+            const float Wi   = kernelW(dist * hiInv);
+            const float tA0  = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
+            const float tA1  = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
+            const float tA2  = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
+            const float fx = (v.x - vi.vx) * v.w, fy = (v.y - vi.vy) * v.w, fz = (v.z - vi.vz) * v.w;
+            dVx0 += tA0 * fx;
+            dVx1 += tA1 * fx;
+            dVx2 += tA2 * fx;
+            dVy0 += tA0 * fy;
+            dVy1 += tA1 * fy;
+            dVy2 += tA2 * fy;
+            dVz0 += tA0 * fz;
+            dVz1 += tA1 * fz;
+            dVz2 += tA2 * fz;
+        },
+        res);
+    if (cu.valid)
+    {
+        const uint32_t i = cu.i;
+        a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
+        const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
+        a.divv[i]            = norm_kxi * (dVx0 + dVy1 + dVz2);
+        if (a.curlv)
+        {
+            const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
+            a.curlv[i]      = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
+        }
+    }
+}
+
+// ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
+template<int CH>
+__global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH]; // x, y, z, vol
+    __shared__ float4 sV[CH]; // vx, vy, vz, c
+    __shared__ float  sD[CH]; // divv
+    __shared__ float  s_red[kClusterWaves];
+    const Clu   cu  = setup(a, s_red);
+    const RecX  ri  = a.rx[cu.iSafe];
+    const RecV  vi  = a.rv[cu.iSafe];
+    const RecC  ci6 = a.rc[cu.iSafe];
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hi = ri.h, ci = vi.c, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    const float hiInv3K     = (float)a.K * (hiInv * hiInv * hiInv);
+    const float divv_i      = ci6.divv;
+    float       vijsignal_i = 1.e-40f * ci;
+    float       gx = 0, gy = 0, gz = 0;
+    bool        res = false;
+    neighborLoop<CH>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r = a.rx[j];
+            const RecV v = a.rv[j];
+            const RecT t = a.rt[j];
+            sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
+                                   relc(r.z, cu.oz, a.box, 2), t.xm / t.kx);
+            sV[slot]     = make_float4(v.vx, v.vy, v.vz, v.c);
+            sD[slot]     = a.rc[j].divv;
+        },
+        [&](uint32_t p) {
+            const float4 q  = sP[p];
+            const float4 v  = sV[p];
+            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float r2    = rx * rx + ry * ry + rz * rz;
+            const float rinv  = rsqrtf(r2);
+            const float dist  = r2 * rinv;
+            const float vx_ij = vi.vx - v.x, vy_ij = vi.vy - v.y, vz_ij = vi.vz - v.z;
+            const float rv    = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            const float vsig  = rv < 0.0f ? ci + v.w - 3.0f * rv * rinv : 0.0f;
+            vijsignal_i       = fmaxf(vijsignal_i, vsig);
+            const float Wi     = hiInv3K * kernelW(dist * hiInv);
+            const float termA1 = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
+            const float termA2 = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
+            const float termA3 = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
+            const float factor = q.w * (divv_i - sD[p]);
+            gx += factor * termA1;
+            gy += factor * termA2;
+            gz += factor * termA3;
+        },
+        res);
+    if (!cu.valid) return;
+    const float graddivv = sqrtf(gx * gx + gy * gy + gz * gz);
+    float       alphaloc = 0.0f;
+    if (divv_i < 0.0f)
+    {
+        const float a_const = hi * hi * graddivv;
+        alphaloc            = a.alphamax * a_const / (a_const + hi * fabsf(divv_i) + 0.05f * ci);
+    }
+    float alpha_i = a.rt[cu.i].alpha;
+    if (alphaloc >= alpha_i) { alpha_i = alphaloc; }
+    else
+    {
+        const float decay    = hi / (a.decay_constant * vijsignal_i);
+        const float alphadot = ((alphaloc >= a.alphamin) ? (alphaloc - alpha_i) : (a.alphamin - alpha_i)) / decay;
+        const double dt      = a.dtPtr ? *a.dtPtr : a.dt;
+        alpha_i              = (float)((double)alpha_i + (double)alphadot * dt);
+    }
+    a.alpha[cu.i] = alpha_i;
+}
+
+// ---- momentum + energy: momentumAndEnergyJLoop<avClean=false> (momentum_energy_kern.hpp:65-222) -------------------
+template<int CH>
+__global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH]; // x, y, z, 1/h
+    __shared__ float4 sV[CH]; // vx, vy, vz, c
+    __shared__ float4 sT[CH]; // m, log2(xm), rho, prho
+    __shared__ float4 sA[CH]; // alpha, c11, c12, c13
+    __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
+    __shared__ float  s_red[kClusterWaves];
+    const Clu   cu  = setup(a, s_red);
+    const RecX  ri  = a.rx[cu.iSafe];
+    const RecV  vi  = a.rv[cu.iSafe];
+    const RecT  ti  = a.rt[cu.iSafe];
+    const RecC  ci6 = a.rc[cu.iSafe];
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hi = ri.h, mi = ri.m, ci = vi.c, h2 = 2.0f * hi;
+    const float alpha_i = ti.alpha, xmassi = ti.xm, prhoi = ti.prho;
+    const float rhoi    = ti.kx * mi / xmassi;
+    const float rhoiInv = 1.0f / rhoi;
+    const float lxi     = __log2f(xmassi);
+    const float hiInv   = 1.0f / hi;
+    const float hiInv3  = hiInv * hiInv * hiInv;
+    const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp;
+    float       maxvsignali = 0.0f;
+    float       mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
+    bool        res = false;
+    neighborLoop<CH>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r   = a.rx[j];
+            const RecV v   = a.rv[j];
+            const RecT t   = a.rt[j];
+            const RecC c6  = a.rc[j];
+            const float rho = t.kx * r.m / t.xm;
+            sP[slot]        = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
+                                   relc(r.z, cu.oz, a.box, 2), 1.0f / r.h);
+            sV[slot]        = make_float4(v.vx, v.vy, v.vz, v.c);
+            sT[slot]        = make_float4(r.m, __log2f(t.xm), rho, t.prho);
+            sA[slot]        = make_float4(t.alpha, c6.c11, c6.c12, c6.c13);
+            sB[slot]        = make_float4(c6.c22, c6.c23, c6.c33, r.m / rho);
+        },
+        [&](uint32_t p) {
+            const float4 P = sP[p], V = sV[p], T = sT[p], A = sA[p], B = sB[p];
+            float        rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float r2     = rx * rx + ry * ry + rz * rz;
+            const float rinv   = rsqrtf(r2);
+            const float dist   = r2 * rinv;
+            const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
+            const float hjInv  = P.w;
+            const float hjInv3 = hjInv * hjInv * hjInv;
+            const float Wi     = hiInv3 * kernelW(dist * hiInv);
+            const float Wj     = hjInv3 * kernelW(dist * hjInv);
+            const float tA1i   = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
+            const float tA2i   = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
+            const float tA3i   = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
+            const float tA1j   = -(A.y * rx + A.z * ry + A.w * rz) * Wj;
+            const float tA2j   = -(A.z * rx + B.x * ry + B.y * rz) * Wj;
+            const float tA3j   = -(A.w * rx + B.y * ry + B.z * rz) * Wj;
+            const float mj = T.x, lxj = T.y, rhoj = T.z, cj = V.w;
+            const float rv  = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            const float wij = rv * rinv;
+            // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
+            const float vij_signal = (alpha_i + A.x) * 0.25f * (ci + cj) - 2.0f * wij;
+            const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
+            const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
+            maxvsignali            = fmaxf(maxvsignali, vijsignal);
+            // Atwood switch: sigma = 0 gives (xm_i^2, xm_j^2), sigma = 1 gives (xm_i xm_j, xm_i xm_j), the ramp
+            // in between xm_i^(2-s) xm_j^s: one branch-free exp2/log2 form for all three cases
+            const float Atwood = fabsf(rhoi - rhoj) * __frcp_rn(rhoi + rhoj);
+            const float sigma  = Atwood < Atmin ? 0.0f : (Atwood > Atmax ? 1.0f : ramp * (Atwood - Atmin));
+            const float dl     = lxj - lxi;
+            const float a_mom  = exp2f(fmaf(sigma, dl, 2.0f * lxi));
+            const float b_mom  = exp2f(fmaf(-sigma, dl, 2.0f * lxj));
+            const float a_visc   = mj * rhoiInv * halfVisc;
+            const float b_visc   = B.w * halfVisc;
+            const float a_visc_x = a_visc * tA1i + b_visc * tA1j;
+            const float a_visc_y = a_visc * tA2i + b_visc * tA2j;
+            const float a_visc_z = a_visc * tA3i + b_visc * tA3j;
+            a_visc_energy += a_visc_x * vx_ij + a_visc_y * vy_ij + a_visc_z * vz_ij;
+            energy += mj * a_mom * (vx_ij * tA1i + vy_ij * tA2i + vz_ij * tA3i);
+            const float momentum_i = mj * prhoi * a_mom;
+            const float momentum_j = mj * T.w * b_mom;
+            mx += momentum_i * tA1i + momentum_j * tA1j + a_visc_x;
+            my += momentum_i * tA2i + momentum_j * tA2j + a_visc_y;
+            mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
+        },
+        res);
+    float dt_lane = INFINITY;
+    if (cu.valid)
+    {
+        if (a_visc_energy < 0.0f) a_visc_energy = 0.0f;
+        a.du[cu.i] = a.K * (double)(prhoi * energy + 0.5f * a_visc_energy);
+        a.ax[cu.i] = (float)(-a.K * (double)mx);
+        a.ay[cu.i] = (float)(-a.K * (double)my);
+        a.az[cu.i] = (float)(-a.K * (double)mz);
+        dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+    }
+    // wave min -> workgroup min -> one atomic per cluster (momentum_energy_gpu.cu:94-118)
+    const float wmin = waveMin(dt_lane);
+    const int   wave = threadIdx.x >> 6;
+    if (a.groupDt != nullptr && (threadIdx.x & 63) == 0 && cu.gw < a.numGroups)
+    {
+        float old         = a.groupDt[cu.gw];
+        a.groupDt[cu.gw] = wmin < old ? wmin : old;
+    }
+    __syncthreads(); // s_red is reused
+    if ((threadIdx.x & 63) == 0) s_red[wave] = wmin;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        float m = s_red[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+            m = s_red[w] < m ? s_red[w] : m;
+        atomicMinPos(a.minDt, m);
+    }
+}
+
+// LDS capacity per kernel (records of 16 / 20 / 32 / 36 / 80 B): the momentum union fills the CU's 160 KiB with
+// one workgroup; the lighter kernels keep two or more workgroups per CU
+constexpr int kChXm = 2048, kChVd = 2048, kChIad = 2048, kChAv = 2048, kChMe = 2000;
+
+static inline unsigned clusters(const PairArgs& a) { return (a.numGroups + kClusterWaves - 1) / kClusterWaves; }
+
+void xmass(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) xmassKernel<kChXm><<<clusters(a), kB, 0, s>>>(a);
+}
+void veDefGradh(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) veDefGradhKernel<kChVd><<<clusters(a), kB, 0, s>>>(a);
+}
+void iadDivvCurlv(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) iadDivvCurlvKernel<kChIad><<<clusters(a), kB, 0, s>>>(a);
+}
+void avSwitches(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) avSwitchesKernel<kChAv><<<clusters(a), kB, 0, s>>>(a);
+}
+void momentumEnergy(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) momentumEnergyKernel<kChMe><<<clusters(a), kB, 0, s>>>(a);
+}
+
+} // namespace cluster
+} // namespace sx

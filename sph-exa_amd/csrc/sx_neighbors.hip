@@ -1,22 +1,31 @@
 /*! @file sx_neighbors.hip
- * @brief Neighbor search with the coupled h-nc iteration, one wavefront per 64-particle SFC block (gfx950).
+ * @brief Neighbor search with the coupled h-nc iteration, one 256-thread workgroup per 256-particle SFC cluster
+ *        (four wave64 groups) on gfx950.
  *
  * Replaces cstone::findNeighbors + sph::findNeighborsSph (cstone/findneighbors.hpp:95-188,
  * sph/find_neighbors.hpp:10-44) and the traversal inside xmassGpu (hydro_ve/xmass_gpu.cu:56-101).
  *
- * Per block (wave):
- *   1. wave reductions give the block's bounding box and max h;
- *   2. waveCollectLeaves (sx_traverse.hpp) gathers every leaf whose geometric box comes within 2*hmax of the
- *      block box (minimum image on periodic axes, inflated by the key-quantisation margin);
- *   3. each candidate leaf's particles (a contiguous SFC range) are loaded coalesced, one per lane, and broadcast
- *      lane by lane with v_readlane: every lane tests the candidate against its own particle with the reference CPU
- *      criterion, in double, without FMA contraction (this file is compiled -ffp-contract=off):
+ * Per cluster (workgroup):
+ *   1. wave + LDS reductions give the cluster's bounding box and max h;
+ *   2. wave 0 collects every leaf whose geometric box comes within 2*hmax of the cluster box (waveCollectLeaves,
+ *      sx_traverse.hpp; minimum image on periodic axes, inflated by the key-quantisation margin) and numbers the
+ *      particles of those leaves consecutively: the cluster's CANDIDATE SPACE (leaf cc's particles start at
+ *      s_cOff[cc]);
+ *   3. each wave independently streams the candidate leaves that one of its lanes can reach, in chunks of 64
+ *      particles loaded coalesced one per lane and broadcast lane by lane with v_readlane; every lane tests them
+ *      against its own particle with the reference CPU criterion, in double, without FMA contraction (this file is
+ *      compiled -ffp-contract=off):
  *          d2 = dx*dx + dy*dy + dz*dz  <  (double)(4.0f*h*h),   j != i,
- *      dx folded with rint() on periodic axes when the particle is within 2h of the box edge (findneighbors.hpp:118);
- *      hits are appended to the lane-interleaved list nidx[(block*ngmax + k)*64 + lane] (k < ngmax, counting on);
- *   4. lanes with nc = count+1 outside [ng0/4, ngmax+1] update h (updateH) and the block repeats, at most 10
+ *      dx folded with rint() on periodic axes when the particle is within 2h of the box edge (findneighbors.hpp:118).
+ *      Stored hits (the first ngmax, like the reference's capped list) are appended to the lane's list -- the global
+ *      index (nidx, gather kernels) or the u16 candidate index (cluster lists) -- and, for cluster lists, OR-ed into
+ *      an LDS bitmap over the candidate space (one atomic per chunk and wave; no workgroup barrier in the stream);
+ *   4. lanes with nc = count+1 outside [ng0/4, ngmax+1] update h (updateH) and the cluster repeats, at most 10
  *      updates per lane (the CPU loop's `iteration++ < 10`), so h, nc and the neighbor SET are identical to the
- *      CPU reference.
+ *      CPU reference;
+ *   5. cluster lists: a prefix popcount of the bitmap numbers the UNION of the cluster's neighbors (uni[], in
+ *      candidate order, i.e. leaf runs), and every lane rewrites its candidate indices as union positions -- still
+ *      ascending, which the chunked LDS staging of sx_hydro_cluster.hip relies on.
  */
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
@@ -24,58 +33,137 @@
 namespace sx
 {
 
-constexpr int kNsWaves = 4; // waves per workgroup
+constexpr int kCandSpace = 1 << 16; //!< candidate particles per cluster (u16 list entries)
+constexpr int kCandWords = kCandSpace / 32;
 
-__global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
+__device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t* pre, uint32_t idx)
 {
-    __shared__ int s_queue[kNsWaves][kQCap];
-    __shared__ int s_cand[kNsWaves][kCCap];
+    const uint32_t w = idx >> 5;
+    return pre[w] + __popc(bits[w] & ((1u << (idx & 31)) - 1u));
+}
 
-    const int      wave = threadIdx.x >> 6;
-    const int      lane = threadIdx.x & 63;
-    const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * kNsWaves + wave;
-    if (g >= a.numGroups) return; // whole wave, no block barrier in this kernel
-    int* queue = s_queue[wave];
-    int* cand  = s_cand[wave];
+__global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
+{
+    __shared__ int      s_queue[kQCap];
+    __shared__ int      s_cand[kCCap];
+    __shared__ uint32_t s_cOff[kCCap + 1];
+    __shared__ uint32_t s_bits[kCandWords];
+    __shared__ uint32_t s_pre[kCandWords];
+    __shared__ double   s_box[kClusterWaves][6];
+    __shared__ float    s_hmax[kClusterWaves];
+    __shared__ int      s_again[kClusterWaves];
+    __shared__ uint32_t s_wsum[kClusterWaves];
+    __shared__ float4   s_chunk[kClusterWaves][kWave];
+    __shared__ int      s_numCand;
 
-    const uint32_t i     = a.first + g * kGroupSize + lane;
-    const bool     valid = i < a.last;
-    const uint32_t iSafe = valid ? i : a.first + g * kGroupSize; // lane 0 of the block is always valid
+    const int      wave  = threadIdx.x >> 6;
+    const int      lane  = threadIdx.x & 63;
+    const uint32_t c     = xcdBlock(blockIdx.x, gridDim.x);
+    const uint32_t g     = c * kClusterWaves + wave;
+    const uint32_t c0    = a.first + c * kCluster;
+    const uint32_t i     = c0 + threadIdx.x;
+    const bool     valid = g < a.numGroups && i < a.last;
+    const uint32_t iSafe = valid ? i : c0; // the cluster's first particle is always valid
     const double   xi = a.x[iSafe], yi = a.y[iSafe], zi = a.z[iSafe];
+    const double   ox = a.x[c0], oy = a.y[c0], oz = a.z[c0]; // cluster origin of the float prefilter
     float          hi = a.h[iSafe];
 
-    uint32_t* nlist = a.nidx + (size_t)g * a.ngmax * kWave + lane;
+    const bool     local = a.localLists != 0;
+    uint32_t*      gl    = a.nidx + (size_t)g * a.ngmax * kWave + lane;
+    uint32_t*      ll    = local ? a.nloc + (size_t)g * nlocWords(a.ngmax) * kWave + lane : nullptr;
+    const uint64_t ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     const unsigned     ngmin      = a.ng0 / 4;
     int                iteration  = 0;
     bool               active     = valid;
     unsigned           count      = 0;
+    unsigned           stored     = 0;
     unsigned long long candTested = 0;
 
-    // block bounding box (positions do not change between iterations)
-    const double bx0 = waveMin(xi), bx1 = waveMax(xi);
-    const double by0 = waveMin(yi), by1 = waveMax(yi);
-    const double bz0 = waveMin(zi), bz1 = waveMax(zi);
+    // cluster bounding box (positions do not change between iterations)
+    {
+        const double wx0 = waveMin(xi), wx1 = waveMax(xi);
+        const double wy0 = waveMin(yi), wy1 = waveMax(yi);
+        const double wz0 = waveMin(zi), wz1 = waveMax(zi);
+        if (lane == 0)
+        {
+            s_box[wave][0] = wx0, s_box[wave][1] = wx1, s_box[wave][2] = wy0;
+            s_box[wave][3] = wy1, s_box[wave][4] = wz0, s_box[wave][5] = wz1;
+        }
+    }
+    __syncthreads();
+    double bx0 = s_box[0][0], bx1 = s_box[0][1], by0 = s_box[0][2], by1 = s_box[0][3], bz0 = s_box[0][4],
+           bz1 = s_box[0][5];
+    for (int w = 1; w < kClusterWaves; ++w)
+    {
+        bx0 = fmin(bx0, s_box[w][0]), bx1 = fmax(bx1, s_box[w][1]);
+        by0 = fmin(by0, s_box[w][2]), by1 = fmax(by1, s_box[w][3]);
+        bz0 = fmin(bz0, s_box[w][4]), bz1 = fmax(bz1, s_box[w][5]);
+    }
     const double gcx = 0.5 * (bx0 + bx1), gcy = 0.5 * (by0 + by1), gcz = 0.5 * (bz0 + bz1);
     const double gsx = 0.5 * (bx1 - bx0), gsy = 0.5 * (by1 - by0), gsz = 0.5 * (bz1 - bz0);
 
+    int numCand = 0;
     while (true)
     {
-        // ---- 2. candidate leaves for radius 2*hmax ----------------------------------------------------
-        const float  hmax = waveMax(valid ? hi : 0.0f);
-        const double R    = 2.0 * (double)hmax * (1.0 + 1e-6) + a.margin;
-        const double R2   = R * R;
-        bool         overflow;
-        const int    numCand = waveCollectLeaves(
-            a.childOffsets,
-            [&](int node) {
-                return boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, gcx, gcy, gcz, gsx, gsy, gsz,
-                                a.box) < R2;
-            },
-            queue, cand, lane, overflow);
-        if (overflow && lane == 0) atomicOr(&a.stats[0], 1u);
+        // ---- 2. candidate leaves for radius 2*hmax of the cluster, numbered into the candidate space -----
+        const float hmaxW = waveMax(valid ? hi : 0.0f);
+        if (lane == 0) s_hmax[wave] = hmaxW;
+        __syncthreads();
+        float hmax = s_hmax[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+            hmax = fmaxf(hmax, s_hmax[w]);
+        if (wave == 0)
+        {
+            const double R  = 2.0 * (double)hmax * (1.0 + 1e-6) + a.margin;
+            const double R2 = R * R;
+            bool         overflow;
+            const int    nCand = waveCollectLeaves(
+                a.childOffsets,
+                [&](int node) {
+                    return boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, gcx, gcy, gcz, gsx, gsy,
+                                    gsz, a.box) < R2;
+                },
+                s_queue, s_cand, lane, overflow);
+            // exclusive scan of the candidate leaf sizes
+            uint32_t run = 0;
+            for (int b = 0; b < nCand; b += kWave)
+            {
+                uint32_t sz = 0;
+                if (b + lane < nCand)
+                {
+                    const int leaf = a.internalToLeaf[s_cand[b + lane]];
+                    sz             = a.layout[leaf + 1] - a.layout[leaf];
+                }
+                uint32_t incl = sz;
+#pragma unroll
+                for (int o = 1; o < kWave; o <<= 1)
+                {
+                    uint32_t t = __shfl_up(incl, o, kWave);
+                    if (lane >= o) incl += t;
+                }
+                if (b + lane < nCand) s_cOff[b + lane] = run + incl - sz;
+                run += __shfl(incl, kWave - 1, kWave);
+            }
+            if (lane == 0)
+            {
+                s_cOff[nCand] = run;
+                if (local && run > (uint32_t)kCandSpace) overflow = true;
+                if (overflow) atomicOr(&a.stats[0], 1u);
+                s_numCand = overflow ? 0 : nCand;
+            }
+        }
+        __syncthreads();
+        numCand = s_numCand;
+        if (local)
+        {
+            const uint32_t nw = (s_cOff[numCand] + 31) / 32;
+            for (uint32_t w = threadIdx.x; w < nw; w += kCluster)
+                s_bits[w] = 0;
+            __syncthreads();
+        }
 
-        // ---- 3. test candidates against each lane's own particle --------------------------------------
+        // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f       = 4.0f * hi * hi;
         const double radSq     = (double)r2f;
         const double tw        = 2.0 * (double)hi;
@@ -85,20 +173,38 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
         const bool   usePbc    = a.box.anyPbc && !inside;
         const bool   anyPbcUse = __ballot(usePbc && valid) != 0;
         const double rr        = 2.0 * (double)(valid ? hi : 0.0f) * (1.0 + 1e-6) + a.margin;
-
-        count = 0;
-        for (int c = 0; c < numCand; ++c)
+        // float prefilter: cluster-relative minimum-image coordinates are exact displacements for every pair
+        // closer than 2h when |x_i - o| + 2h < L/2 on the periodic axes; rounding band tol on d2
+        const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
+                    zr = (float)foldPbc(zi - oz, a.box, 2);
+        bool safe = true;
+        for (int d = 0; d < 3; ++d)
         {
-            const int      node = __builtin_amdgcn_readfirstlane(cand[c]);
-            const int      leaf = a.internalToLeaf[node];
-            const uint32_t p0 = a.layout[leaf], p1 = a.layout[leaf + 1];
-            if (p0 == p1) continue;
-            // per-lane sphere-vs-leaf prune (conservative): skip the leaf if no lane can reach it
+            const float rd = d == 0 ? xr : (d == 1 ? yr : zr);
+            if (a.box.pbc[d] && (fabsf(rd) + 2.05f * hi) >= 0.49f * (float)a.box.l[d]) safe = false;
+        }
+        const bool  fastWave = __ballot(valid && !safe) == 0;
+        const float ext      = fmaxf(fabsf(xr), fmaxf(fabsf(yr), fabsf(zr))) + 2.0f * hi;
+        const float tol      = 7.62939453125e-06f * hi * (ext + hi) + 1e-30f; // 2^-17 h (E + h)
+        const float r2hi     = valid ? r2f + tol : -1.0f;
+        const float r2lo     = r2f - tol;
+
+        count         = 0;
+        stored        = 0;
+        uint32_t pend = 0; // low half of the next u16-pair word
+        for (int cc = 0; cc < numCand; ++cc)
+        {
+            const int node = s_cand[cc];
+            // per-lane sphere-vs-leaf prune (conservative): the wave tests the leaf only if one of its lanes can reach it
             const bool reach = valid && boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, xi, yi, zi,
                                                  0.0, 0.0, 0.0, a.box) < rr * rr;
             if (__ballot(reach) == 0) continue;
+            const int      leaf = a.internalToLeaf[node];
+            const uint32_t p0 = a.layout[leaf], p1 = a.layout[leaf + 1];
+            const uint32_t base = s_cOff[cc] - p0; // candidate index of particle j = base + j
             for (uint32_t s0 = p0; s0 < p1; s0 += kWave)
             {
+                const int      m  = (int)min<uint32_t>(kWave, p1 - s0);
                 const uint32_t jl = s0 + lane;
                 double         xj = 0, yj = 0, zj = 0;
                 if (jl < p1)
@@ -107,9 +213,66 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
                     yj = a.y[jl];
                     zj = a.z[jl];
                 }
-                const int m = (int)min<uint32_t>(kWave, p1 - s0);
                 candTested += m;
-                if (anyPbcUse)
+                uint64_t lm = 0; // this lane's stored hits in the chunk
+                if (fastWave)
+                {
+                    // float prefilter on cluster-relative, minimum-image coordinates; the rare candidates within the
+                    // rounding band of some lane's radius are decided by the exact double test
+                    s_chunk[wave][lane] = make_float4((float)foldPbc(xj - ox, a.box, 0), (float)foldPbc(yj - oy, a.box, 1),
+                                                      (float)foldPbc(zj - oz, a.box, 2), 0.0f);
+                    __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
+                    __builtin_amdgcn_wave_barrier();
+                    uint32_t hw[2] = {0u, 0u};
+#pragma unroll
+                    for (int half = 0; half < 2; ++half)
+                    {
+                        const int kEnd = min(m, 32 * (half + 1));
+                        uint32_t  bits = 0;
+                        for (int k = 32 * half; k < kEnd; ++k)
+                        {
+                            const float4 q  = s_chunk[wave][k];
+                            const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+                            const float  d2 = dx * dx + dy * dy + dz * dz;
+                            bool         hit = d2 < r2hi;
+                            if (__ballot(hit && d2 >= r2lo))
+                            {
+                                // exact reference criterion for this candidate (uniform address: scalar loads)
+                                const uint32_t j   = s0 + k;
+                                double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
+                                if (usePbc)
+                                {
+                                    ex = foldPbc(ex, a.box, 0);
+                                    ey = foldPbc(ey, a.box, 1);
+                                    ez = foldPbc(ez, a.box, 2);
+                                }
+                                hit = valid && (ex * ex + ey * ey + ez * ez < radSq);
+                            }
+                            if (hit) bits |= 1u << (k & 31);
+                        }
+                        hw[half] = bits;
+                    }
+                    uint64_t hm = ((uint64_t)hw[1] << 32) | hw[0];
+                    if (i >= s0 && i < s0 + (uint32_t)m) hm &= ~(1ull << (i - s0)); // j != i
+                    const unsigned nh = __popcll(hm);
+                    if (count + nh > a.ngmax)
+                    {
+                        // keep the first (ngmax - count) hits in stream order, like the capped CPU list
+                        unsigned keep = count < a.ngmax ? a.ngmax - count : 0u;
+                        uint64_t kept = 0;
+                        while (keep--)
+                        {
+                            const uint64_t low = hm & (~hm + 1ull);
+                            kept |= low;
+                            hm ^= low;
+                        }
+                        hm = kept;
+                    }
+                    count += nh;
+                    lm = hm;
+                    __builtin_amdgcn_wave_barrier(); // s_chunk is rewritten by the next chunk
+                }
+                else if (anyPbcUse)
                 {
                     for (int k = 0; k < m; ++k)
                     {
@@ -122,11 +285,10 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
                             dy = foldPbc(dy, a.box, 1);
                             dz = foldPbc(dz, a.box, 2);
                         }
-                        const uint32_t j   = s0 + k;
-                        const bool     hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && j != i;
+                        const bool hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i;
                         if (hit)
                         {
-                            if (count < a.ngmax) nlist[(size_t)count * kWave] = j;
+                            if (count < a.ngmax) lm |= 1ull << k;
                             count++;
                         }
                     }
@@ -135,38 +297,142 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
                 {
                     for (int k = 0; k < m; ++k)
                     {
-                        double         dx  = readlaneD(xj, k) - xi;
-                        double         dy  = readlaneD(yj, k) - yi;
-                        double         dz  = readlaneD(zj, k) - zi;
-                        const uint32_t j   = s0 + k;
-                        const bool     hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && j != i;
+                        double     dx  = readlaneD(xj, k) - xi;
+                        double     dy  = readlaneD(yj, k) - yi;
+                        double     dz  = readlaneD(zj, k) - zi;
+                        const bool hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i;
                         if (hit)
                         {
-                            if (count < a.ngmax) nlist[(size_t)count * kWave] = j;
+                            if (count < a.ngmax) lm |= 1ull << k;
                             count++;
                         }
                     }
                 }
+                if (local)
+                {
+                    const uint32_t b0 = base + s0; // candidate index of the chunk's first particle
+                    const uint64_t wm = waveOr64(lm);
+                    if (wm && lane < 3)
+                    {
+                        // bits [b0, b0+64) of the bitmap span up to three words
+                        const uint32_t sh = b0 & 31, w0 = b0 >> 5;
+                        uint32_t       part;
+                        if (lane == 0) part = (uint32_t)(wm << sh);
+                        else if (lane == 1) part = sh ? (uint32_t)(wm >> (32 - sh)) : (uint32_t)(wm >> 32);
+                        else part = sh ? (uint32_t)(wm >> (64 - sh)) : 0u;
+                        if (part) atomicOr(&s_bits[w0 + lane], part);
+                    }
+                    while (lm)
+                    {
+                        const uint32_t k = __builtin_ctzll(lm);
+                        lm &= lm - 1ull;
+                        const uint32_t idx = b0 + k;
+                        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend | (idx << 16);
+                        else pend = idx;
+                        stored++;
+                    }
+                }
+                else
+                {
+                    while (lm)
+                    {
+                        const int k = __builtin_ctzll(lm);
+                        lm &= lm - 1ull;
+                        gl[(size_t)stored * kWave] = s0 + k;
+                        stored++;
+                    }
+                }
             }
         }
+        if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
-        if (!a.iterateH) break;
-        const unsigned ncSph = count + 1;
-        const bool     bad   = active && (ngmin > ncSph || (ncSph - 1) > a.ngmax);
-        bool           again = false;
-        if (bad)
+        bool again = false;
+        if (a.iterateH)
         {
-            if (iteration < 10)
+            const unsigned ncSph = count + 1;
+            const bool     bad   = active && (ngmin > ncSph || (ncSph - 1) > a.ngmax);
+            if (bad)
             {
-                iteration++;
-                hi    = updateH(a.ng0, ncSph, hi, a.powTab);
-                again = true;
+                if (iteration < 10)
+                {
+                    iteration++;
+                    hi    = updateH(a.ng0, ncSph, hi, a.powTab);
+                    again = true;
+                }
+                else { iteration = 11; }
             }
-            else { iteration = 11; }
+            active = again;
         }
-        active = again;
-        if (__ballot(again) == 0) break;
+        const bool waveAgain = __ballot(again) != 0; // full-wave ballot, then one lane publishes it
+        if (lane == 0) s_again[wave] = waveAgain;
+        __syncthreads(); // also: every wave's bitmap updates are complete
+        int any = 0;
+        for (int w = 0; w < kClusterWaves; ++w)
+            any |= s_again[w];
+        if (!any) break;
+        __syncthreads(); // s_again / s_hmax / candidate space are rewritten by the next iteration
+    }
+
+    // ---- 5. cluster union: prefix popcount of the bitmap, union entries, list rewrite -----------------------
+    uint32_t ucnt = 0;
+    if (local)
+    {
+        const uint32_t nw  = (s_cOff[numCand] + 31) / 32;
+        const uint32_t per = (nw + kCluster - 1) / kCluster; // words per thread, consecutive
+        const uint32_t w0  = min(nw, threadIdx.x * per), w1 = min(nw, w0 + per);
+        uint32_t       sum = 0;
+        for (uint32_t w = w0; w < w1; ++w)
+            sum += __popc(s_bits[w]);
+        // workgroup exclusive scan of the per-thread sums
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1)
+        {
+            uint32_t t = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += t;
+        }
+        if (lane == kWave - 1) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int w = 0; w < wave; ++w)
+            off += s_wsum[w];
+        for (int w = 0; w < kClusterWaves; ++w)
+            ucnt += s_wsum[w];
+        uint32_t run = off + incl - sum;
+        for (uint32_t w = w0; w < w1; ++w)
+        {
+            s_pre[w] = run;
+            run += __popc(s_bits[w]);
+        }
+        // union entries: candidate index -> global index, through the leaf it belongs to
+        uint32_t* uni = a.uni + (size_t)c * a.ucap;
+        run           = off + incl - sum;
+        int cc        = 0;
+        for (uint32_t w = w0; w < w1; ++w)
+        {
+            uint32_t bits = s_bits[w];
+            while (bits)
+            {
+                const uint32_t idx = w * 32 + __builtin_ctz(bits);
+                bits &= bits - 1u;
+                while (s_cOff[cc + 1] <= idx)
+                    ++cc;
+                const int leaf = a.internalToLeaf[s_cand[cc]];
+                uni[run++]     = a.layout[leaf] + (idx - s_cOff[cc]);
+            }
+        }
+        __syncthreads();
+        // candidate indices -> union positions (ascending either way)
+        const uint32_t nwl = (stored + 1) >> 1;
+        for (uint32_t k = 0; k < nwl; ++k)
+        {
+            const uint32_t v  = ll[(size_t)k * kWave];
+            const uint32_t lo = bitRank(s_bits, s_pre, v & 0xffffu);
+            const uint32_t hp = (2 * k + 1 < stored) ? bitRank(s_bits, s_pre, v >> 16) : 0u;
+            ll[(size_t)k * kWave] = lo | (hp << 16);
+        }
+        if (threadIdx.x == 0) a.ucount[c] = ucnt;
     }
 
     if (valid)
@@ -178,27 +444,41 @@ __global__ __launch_bounds__(kNsWaves * 64) void findNeighborsKernel(NsArgs a)
     const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
     const unsigned           nfail  = waveSum(failed);
     const unsigned           maxCnt = waveMax(valid ? count : 0u);
-    const unsigned long long stored = waveSum((unsigned long long)(valid ? min(count, a.ngmax) : 0u));
+    const unsigned long long nstore = waveSum((unsigned long long)(valid ? stored : 0u));
     const unsigned long long tested = waveSum(valid ? candTested : 0ull);
     if (lane == 0)
     {
         if (nfail) atomicAdd(&a.stats[1], nfail);
         atomicMax(&a.stats[2], maxCnt);
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 4), stored);
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 4), nstore);
         atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 6), tested);
+        if (wave == 0 && local) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 8), (unsigned long long)ucnt);
     }
 }
 
-__global__ void exportKernel(const uint32_t* nidx, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
-                             uint32_t* out)
+//! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]
+__global__ void exportKernel(NsArgs a, uint32_t* out)
 {
-    uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= last) return;
-    uint32_t ni = i - first, g = ni / kGroupSize, lane = ni % kGroupSize;
-    uint32_t c  = nc[i] - 1;
-    c           = c < ngmax ? c : ngmax;
-    for (uint32_t k = 0; k < ngmax; ++k)
-        out[(size_t)ni * ngmax + k] = k < c ? nidx[((size_t)g * ngmax + k) * kWave + lane] : 0u;
+    uint32_t i = a.first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.last) return;
+    uint32_t ni = i - a.first, g = ni / kGroupSize, lane = ni % kGroupSize, c = ni / kCluster;
+    uint32_t cnt = a.nc[i] - 1;
+    cnt          = cnt < a.ngmax ? cnt : a.ngmax;
+    const uint32_t W = nlocWords(a.ngmax);
+    for (uint32_t k = 0; k < a.ngmax; ++k)
+    {
+        uint32_t j = 0;
+        if (k < cnt)
+        {
+            if (a.localLists)
+            {
+                uint32_t w = a.nloc[((size_t)g * W + k / 2) * kWave + lane];
+                j          = a.uni[(size_t)c * a.ucap + ((k & 1) ? (w >> 16) : (w & 0xffffu))];
+            }
+            else { j = a.nidx[((size_t)g * a.ngmax + k) * kWave + lane]; }
+        }
+        out[(size_t)ni * a.ngmax + k] = j;
+    }
 }
 
 __global__ void importKernel(uint32_t* nidx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in)
@@ -213,16 +493,15 @@ __global__ void importKernel(uint32_t* nidx, uint32_t first, uint32_t last, uint
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
-    unsigned blocks = (a.numGroups + kNsWaves - 1) / kNsWaves;
-    findNeighborsKernel<<<blocks, kNsWaves * 64, 0, s>>>(a);
+    unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    findNeighborsKernel<<<clusters, kCluster, 0, s>>>(a);
     return hipGetLastError();
 }
 
-hipError_t exportNeighbors(const uint32_t* nidx, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
-                           uint32_t* out, hipStream_t s)
+hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s)
 {
-    uint32_t n = last - first;
-    if (n) exportKernel<<<(n + 255) / 256, 256, 0, s>>>(nidx, nc, first, last, ngmax, out);
+    uint32_t n = a.last - a.first;
+    if (n) exportKernel<<<(n + 255) / 256, 256, 0, s>>>(a, out);
     return hipGetLastError();
 }
 

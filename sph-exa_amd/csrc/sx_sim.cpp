@@ -356,7 +356,7 @@ struct sx_sim
     RecV*     rv;
     RecT*     rt;
     RecC*     rc;
-    uint32_t* nidx;
+    NbLists   nb;
     uint32_t* stats;
     uint32_t* statsHost;
     Scalars*  sc;
@@ -451,10 +451,9 @@ void allocFields(sx_sim* s, size_t cap)
     spare(s->dum1, "du_m1");
     spare(s->alpha, "alpha");
     spare(s->id, "id");
-    size_t groups = (cap + kGroupSize - 1) / kGroupSize;
-    s->nidx       = a.get<uint32_t>("nidx", groups * s->p.ngmax * kWave);
-    s->stats      = a.get<uint32_t>("stats", 8);
-    s->statsHost  = a.pinned<uint32_t>("statsHost", 8);
+    s->nb.reserve(a, 0, (uint32_t)cap, s->p.ngmax, true);
+    s->stats      = a.get<uint32_t>("stats", kStatsWords);
+    s->statsHost  = a.pinned<uint32_t>("statsHost", kStatsWords);
     s->sc         = a.get<Scalars>("scalars", 1);
     s->scHost     = a.pinned<Scalars>("scalarsHost", 1);
 }
@@ -466,7 +465,12 @@ PairArgs simPairArgs(sx_sim* s)
     a.last           = (uint32_t)s->last;
     a.numGroups      = (uint32_t)((s->last - s->first + kGroupSize - 1) / kGroupSize);
     a.ngmax          = s->p.ngmax;
-    a.nidx           = s->nidx;
+    a.localLists     = s->nb.local;
+    a.nidx           = s->nb.nidx;
+    a.nloc           = s->nb.nloc;
+    a.uni            = s->nb.uni;
+    a.ucount         = s->nb.ucount;
+    a.ucap           = s->nb.ucap;
     a.nc             = s->nc;
     a.rx             = s->rx;
     a.rv             = s->rv;
@@ -963,7 +967,8 @@ extern "C"
             na.z              = s->z;
             na.h              = s->h;
             na.nc             = s->nc;
-            na.nidx           = s->nidx;
+            if (!s->nb.reserve(s->mem, (uint32_t)s->first, (uint32_t)s->last, s->p.ngmax, true)) return SX_ERR_NOMEM;
+            na.setLists(s->nb);
             na.childOffsets   = s->tree.childOffsets;
             na.internalToLeaf = s->tree.internalToLeaf;
             na.layout         = s->tree.layout;
@@ -973,10 +978,10 @@ extern "C"
             na.margin         = quantMargin(s->dbox);
             na.stats          = s->stats;
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
-            SIM_HIP(hipMemsetAsync(s->stats, 0, 32, st));
+            SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(findNeighbors(na, st));
-            SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, 32, hipMemcpyDeviceToHost, st));
+            SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
             if (!dist) break;
             // halo sufficiency: every local particle's final h within its chunk's request margin
             const size_t nl  = s->last - s->first;
@@ -1072,6 +1077,7 @@ extern "C"
         s->lastStats.maxNeighbors  = s->statsHost[2];
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
+        s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         if (s->statsHost[0] & 1u) return SX_ERR_TRAVERSAL;
         return SX_OK;
     }

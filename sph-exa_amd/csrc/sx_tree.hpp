@@ -114,6 +114,41 @@ struct DevTree
     }
 };
 
+//! the neighbor lists of one search over [first, last): global u32 lists or cluster unions + u16 positions
+struct NbLists
+{
+    int       local{0};
+    uint32_t  first{0}, last{0}, ngmax{0}, ucap{0};
+    uint32_t* nidx{nullptr};
+    uint32_t* nloc{nullptr};
+    uint32_t* uni{nullptr};
+    uint32_t* ucount{nullptr};
+
+    size_t groups() const { return (size_t(last - first) + kGroupSize - 1) / kGroupSize; }
+    size_t clusters() const { return (size_t(last - first) + kCluster - 1) / kCluster; }
+    //! cluster-local u16 positions need unions below 2^16 entries
+    static bool localPossible(uint32_t ngmax) { return unionCap(ngmax) <= 65536u; }
+    bool reserve(Arena& a, uint32_t f, uint32_t l, uint32_t ng, bool wantLocal)
+    {
+        first = f, last = l, ngmax = ng;
+        local = (wantLocal && localPossible(ng)) ? 1 : 0;
+        size_t gr = std::max<size_t>(1, groups()), cl = std::max<size_t>(1, clusters());
+        if (local)
+        {
+            ucap   = unionCap(ng);
+            nloc   = a.get<uint32_t>("nb.nloc", gr * nlocWords(ng) * kWave);
+            uni    = a.get<uint32_t>("nb.uni", cl * ucap);
+            ucount = a.get<uint32_t>("nb.ucount", cl);
+            return nloc && uni && ucount;
+        }
+        nidx = a.get<uint32_t>("nb.nidx", gr * ng * kWave);
+        return nidx != nullptr;
+    }
+};
+
+constexpr int kStatsWords = 12; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
+                                //!< neighbors, [6] candidates tested, [8] union entries
+
 //! neighbor-search arguments (sx_neighbors.hip)
 struct NsArgs
 {
@@ -122,7 +157,15 @@ struct NsArgs
     const double *  x, *y, *z;
     float*          h;
     uint32_t*       nc;
-    uint32_t*       nidx;
+    uint32_t*       nidx; // global lists [group][k][lane] (localLists == 0)
+    // cluster lists (localLists == 1): per 256-particle cluster c, the union of its targets' neighbors
+    // uni[c*ucap + u] (global indices, stream order), ucount[c] = U, and per target the u16 positions into that
+    // union, two per word: nloc[(group*nlocWords + k/2)*64 + lane]
+    int             localLists;
+    uint32_t*       nloc;
+    uint32_t*       uni;
+    uint32_t*       ucount;
+    uint32_t        ucap;
     // tree (OctreeNsView)
     const int32_t*  childOffsets;
     const int32_t*  internalToLeaf;
@@ -132,7 +175,17 @@ struct NsArgs
     DevBox          box;
     double          margin; // node-box inflation covering key quantisation round-off
     const float*    powTab; // glibc powf(1 + 1023*ng0/nc, 0.1f) by nc (updateH)
-    uint32_t*       stats;  // [0] error flags, [1] failures, [2] max count, [3] pad, [4..5] sum nbrs (u64), [6..7] sum cand
+    uint32_t*       stats;  // kStatsWords words, see above
+
+    void setLists(const NbLists& L)
+    {
+        localLists = L.local;
+        nidx       = L.nidx;
+        nloc       = L.nloc;
+        uni        = L.uni;
+        ucount     = L.ucount;
+        ucap       = L.ucap;
+    }
 };
 
 hipError_t launchSfcKeys(const double* x, const double* y, const double* z, uint64_t* keys, size_t n,
@@ -155,8 +208,8 @@ void       packC(size_t n, const float* c11, const float* c12, const float* c13,
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
-hipError_t exportNeighbors(const uint32_t* nidx, const uint32_t* nc, uint32_t first, uint32_t last, uint32_t ngmax,
-                           uint32_t* out, hipStream_t s);
+//! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
+hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);
 hipError_t importNeighbors(uint32_t* nidx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in,
                            hipStream_t s);
 

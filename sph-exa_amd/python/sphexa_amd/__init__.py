@@ -64,7 +64,7 @@ class SxOctree(C.Structure):
 
 class SxNbStats(C.Structure):
     _fields_ = [("sumNeighbors", C.c_uint64), ("maxNeighbors", C.c_uint32), ("numFailed", C.c_uint32),
-                ("sumCandidates", C.c_uint64)]
+                ("sumCandidates", C.c_uint64), ("sumUnion", C.c_uint64)]
 
 
 # field dtypes (sph::SphTypes, sph/types.hpp:39-46)
@@ -418,7 +418,7 @@ class Sim:
         s = SxNbStats()
         self.L.sx_sim_last_stats(self.h, C.byref(s))
         return dict(sumNeighbors=s.sumNeighbors, maxNeighbors=s.maxNeighbors, numFailed=s.numFailed,
-                    sumCandidates=s.sumCandidates)
+                    sumCandidates=s.sumCandidates, sumUnion=s.sumUnion)
 
     def close(self):
         if self.h:

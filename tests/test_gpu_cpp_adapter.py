@@ -61,6 +61,8 @@ def test_cpp_adapter_compute_forces(tmp_path):
         scale = np.abs(b)
         if k in ("c12", "c13", "c23"):
             scale = np.maximum(np.abs(ref.c11), np.abs(ref.c22)).astype(np.float64)
-        tol = 2e-5 * scale + 1e-5 * np.max(np.abs(b))
+        # curlv is pure cancellation noise on the symmetric Sedov lattice: scale it by the velocity-gradient size
+        field_max = np.max(np.abs(ref.divv)) if k == "curlv" else np.max(np.abs(b))
+        tol = 2e-5 * scale + 1e-5 * field_max
         assert np.all(np.abs(a - b) <= tol), (k, np.max(np.abs(a - b) / (scale + 1e-300)))
     assert mdt == pytest.approx(rdt, rel=1e-6)
