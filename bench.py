@@ -21,8 +21,28 @@ sys.path.insert(0, os.path.join(ROOT, "sph-exa_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (packed) peak
 MOM_OWN_BYTES = 108    # momentum kernel own record R+W
 MOM_EDGE_BYTES = 4 + 88  # index + neighbor record per edge
+MOM_FLOP_PER_PAIR = 150  # SURVEY.md 8(d) secondary VALU figure
+# compulsory HBM bytes of one momentum launch per target, as implemented: own packed records 96 B,
+# nc 4 B, outputs 20 B, u16 neighbor positions 2 B/neighbor, union index 4 B per union entry
+MOM_COMPULSORY_OWN = 96 + 4 + 20
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 --pmc summary (scripts/gpu_pmc.sh +
+    scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k, v in d.items():
+        if kernel_prefix in k and "hbm_read_bytes_est" in v and "hbm_write_bytes_est" in v:
+            return v["hbm_read_bytes_est"] + v["hbm_write_bytes_est"]
+    return None
 
 
 def parse():
@@ -103,12 +123,14 @@ def main():
 
     ctx.sync()
     barrier()
-    stage_sum = {}
+    stage_sum, kern_sum = {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sim.step()
         for k, v in sim.stage_times().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
+        for k, v in sim.kernel_times().items():
+            kern_sum[k] = kern_sum.get(k, 0.0) + v
     ctx.sync()
     barrier()
     el = time.perf_counter() - t0
@@ -122,9 +144,12 @@ def main():
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
     ng = stats["sumNeighbors"] / max(1, n_local)
-    mom_ms = stage_sum.get("MomentumEnergy", float("nan")) / args.steps
+    mom_ms = kern_sum.get("momentumEnergy", float("nan")) / args.steps
     mom_bytes = n_local * (MOM_OWN_BYTES + ng * MOM_EDGE_BYTES)
     achieved = mom_bytes / (mom_ms * 1e-3) / 1e9
+    union_pp = stats["sumUnion"] / max(1, n_local)
+    comp_bytes = n_local * (MOM_COMPULSORY_OWN + 2 * ng + 4 * union_pp)
+    mom_tflops = n_local * ng * MOM_FLOP_PER_PAIR / (mom_ms * 1e-3) / 1e12
     sc = sim.scalars()
     out = {
         "metric": "particle-updates/sec (whole node), Sedov -n 400, 1/2/4/8 MI355X + HBM roofline %",
@@ -146,9 +171,16 @@ def main():
                    "halos_per_gpu": sim.layout()["n"] - n_local,
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
         "roofline": {"bound": "hbm", "kernel": "momentumEnergyKernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("momentumEnergyKernel"),
                      "algorithmic_bytes_per_launch": mom_bytes, "avg_launch_ms": mom_ms,
-                     "model": f"edge model: {MOM_OWN_BYTES} B own + {ng:.1f} neighbors x {MOM_EDGE_BYTES} B"},
+                     "model": f"edge model (SURVEY.md 8(d)): {MOM_OWN_BYTES} B own + {ng:.1f} neighbors x "
+                              f"{MOM_EDGE_BYTES} B; effective bandwidth, neighbor records come from LDS",
+                     "compulsory_bytes_per_launch": comp_bytes,
+                     "compulsory_frac": comp_bytes / (mom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "valu": {"flop_per_pair": MOM_FLOP_PER_PAIR, "achieved_tflops": mom_tflops,
+                              "peak_tflops": FP32_PEAK_TFLOPS, "frac": mom_tflops / FP32_PEAK_TFLOPS},
+                     "traffic_source": os.path.relpath(PMC_FILE, ROOT)},
+        "kernels_ms": {k: v / args.steps for k, v in kern_sum.items()},
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
         "neighbors_per_particle": ng,
         "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),

@@ -165,6 +165,9 @@ const char* sx_last_error(sx_ctx* ctx);
  *  order); 0 (default): FMA-contracted kernels. */
 int    sx_set_exact(sx_ctx* ctx, int exact);
 double sx_kernel_constant(void); /* K of the sinc^6 kernel, particles_data.hpp:366 */
+/*! host evaluation of the register-resident kernel W(v), dW/dv of the fast pair kernels (sx_kernel_poly.hpp), for
+ *  checking it against the reference tables */
+int    sx_kernel_poly(const float* v, size_t n, float* w, float* dw);
 int    sx_copy_tables(sx_ctx* ctx, float* wh_host, float* whd_host); /* 20000-entry f32 tables */
 int    sx_synchronize(sx_ctx* ctx);
 
@@ -269,6 +272,9 @@ int    sx_sim_scalars(sx_sim* sim, double out[5]);
 /*! per-stage device time of the last step (ms) measured with HIP events, names in stage order */
 int    sx_sim_stage_times(sx_sim* sim, float* ms, int cap, const char** names);
 int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);
+/*! device time (ms) of each hot kernel alone in the last step (HIP events on the launch stream, bracketing just the
+ *  launch): findNeighbors, xmass, veDefGradh, iadDivvCurlv, avSwitches, momentumEnergy */
+int    sx_sim_kernel_times(sx_sim* sim, float* ms, int cap, const char** names);
 
 #ifdef __cplusplus
 }

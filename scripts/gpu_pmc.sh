@@ -7,7 +7,7 @@ OUT=gpurun_out/pmc
 mkdir -p $OUT
 ARGS=${ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
 i=0
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES"; do
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" "SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"; do
   i=$((i+1))
   echo "== pass $i: $pmc"; date
   timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d $OUT/p$i -o pmc -- python bench.py $ARGS > $OUT/p$i.log 2>&1 || { rc=$?; tail -5 $OUT/p$i.log; exit $rc; }

@@ -13,6 +13,7 @@
 
 #include "../../include/sphexa_hip.h"
 #include "sx_hydro.hpp"
+#include "sx_kernel_poly.hpp"
 #include "sx_tree.hpp"
 
 using namespace sx;
@@ -170,6 +171,13 @@ extern "C"
     int           sx_ctx_exact_internal(sx_ctx* c) { return c->exact ? 1 : 0; }
     const float2* sx_ctx_table_internal(sx_ctx* c, int which) { return which ? c->whd : c->wh; }
     const float*  sx_ctx_powtab_internal(sx_ctx* c, uint32_t ng0) { return ensurePowTab(c, ng0); }
+
+    int sx_kernel_poly(const float* v, size_t n, float* w, float* dw)
+    {
+        for (size_t k = 0; k < n; ++k)
+            kernelWdW(v[k], w[k], dw[k]);
+        return SX_OK;
+    }
 
     double sx_kernel_constant(void)
     {

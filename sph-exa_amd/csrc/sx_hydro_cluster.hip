@@ -22,6 +22,7 @@
  * the tolerance).  Bit-reproducible results come from the exact variant (sx_hydro.hip, -ffp-contract=off).
  */
 #include "sx_hydro.hpp"
+#include "sx_kernel_poly.hpp"
 #include "sx_traverse.hpp"
 
 namespace sx
@@ -31,71 +32,58 @@ namespace cluster
 
 constexpr int kB = kCluster; // threads per workgroup
 
-//! sinc(pi v / 2) as a polynomial in t = v^2 on [0, 2] (least squares, sx_hydro_cluster.hip header)
-__device__ __forceinline__ float sincPoly(float t)
-{
-    float s = 3.08339593857454e-08f;
-    s       = fmaf(s, t, -2.262898533444968e-06f);
-    s       = fmaf(s, t, 0.00010206655861111358f);
-    s       = fmaf(s, t, -0.0029803994111716747f);
-    s       = fmaf(s, t, 0.050733841955661774f);
-    s       = fmaf(s, t, -0.411233514547348f);
-    return fmaf(s, t, 1.0f);
-}
-//! (d/dv sinc(pi v / 2)) / v as a polynomial in t = v^2
-__device__ __forceinline__ float dsincPolyOverV(float t)
-{
-    float s = 5.004272196629245e-08f;
-    s       = fmaf(s, t, -2.7139270741827204e-07f);
-    s       = fmaf(s, t, -1.9479362890706398e-05f);
-    s       = fmaf(s, t, 0.0008091478957794607f);
-    s       = fmaf(s, t, -0.01787404529750347f);
-    s       = fmaf(s, t, 0.20293137431144714f);
-    return fmaf(s, t, -0.8224664926528931f);
-}
-//! W(v) = sinc6 (sph_kernel_tables.hpp:27-40); 0 beyond the support like lt::lookup's last interval
-__device__ __forceinline__ float kernelW(float v)
-{
-    float s  = sincPoly(v * v);
-    float s2 = s * s;
-    return v < 2.0f ? s2 * s2 * s2 : 0.0f;
-}
-//! W and dW/dv = 6 sinc^5 sinc' (sinc6d)
-__device__ __forceinline__ void kernelWdW(float v, float& w, float& dw)
-{
-    float t  = v * v;
-    float s  = sincPoly(t);
-    float s2 = s * s;
-    float s4 = s2 * s2;
-    bool  in = v < 2.0f;
-    w        = in ? s4 * s2 : 0.0f;
-    dw       = in ? 6.0f * s4 * s * v * dsincPolyOverV(t) : 0.0f;
-}
-
 //! per-workgroup cluster bookkeeping
 struct Clu
 {
     uint32_t        c, gw, i, iSafe, U;
     bool            valid;
-    unsigned        cnt;
-    const uint32_t* un; // union of this cluster
-    const uint32_t* nl; // this lane's position words, stride 64
+    unsigned        cnt;        // this target's stored neighbors
+    uint32_t        wBeg, wEnd; // this wave's share of the target's list words (split-K over the wave's part)
+    int             part;       // which share: 0 .. SPLIT-1
+    int             tid;        // target slot within the cluster: 0 .. 255
+    const uint32_t* un;         // union of this cluster
+    const uint32_t* nl;         // this lane's position words, stride 64
     double          ox, oy, oz;
     bool            pbc; // positions need the applyPBC rule after folding (tiny periodic boxes)
+};
+
+//! LDS neighbor records as loaded by the pipelined loop
+struct Rec5
+{
+    float4 a;
+    float  s;
+};
+struct Rec8
+{
+    float4 a, b;
+};
+struct Rec9
+{
+    float4 a, b;
+    float  s;
+};
+struct Rec20
+{
+    float4 p, v, t, a, b;
 };
 
 __device__ __forceinline__ float relc(double x, double o, const DevBox& b, int k) { return (float)foldPbc(x - o, b, k); }
 
 //! sets up the cluster and decides (workgroup-uniformly) whether folded coordinates are minimum-image for every
-//! neighbor pair: |x_i - o| + 2 h_i < L/2 on every periodic axis
+//! neighbor pair: |x_i - o| + 2 h_i < L/2 on every periodic axis.  With SPLIT > 1 the workgroup has SPLIT waves per
+//! group: wave w serves group w % 4 and takes the words [wBeg, wEnd) of share w / 4 of every lane's list.
+template<int SPLIT>
 __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
 {
     Clu            cu;
     const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int      sub  = wave & (kClusterWaves - 1);
+    cu.part             = wave / kClusterWaves;
+    cu.tid              = sub * kWave + lane;
     cu.c                = xcdBlock(blockIdx.x, gridDim.x);
-    cu.gw               = cu.c * kClusterWaves + wave;
+    cu.gw               = cu.c * kClusterWaves + sub;
     const uint32_t c0   = a.first + cu.c * kCluster;
-    cu.i                = c0 + threadIdx.x;
+    cu.i                = c0 + cu.tid;
     cu.valid            = cu.gw < a.numGroups && cu.i < a.last;
     cu.iSafe            = cu.valid ? cu.i : c0;
     cu.cnt              = 0;
@@ -104,10 +92,13 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
         unsigned c1 = a.nc[cu.i] - 1;
         cu.cnt      = c1 < a.ngmax ? c1 : a.ngmax;
     }
-    cu.U  = a.ucount[cu.c];
-    cu.un = a.uni + (size_t)cu.c * a.ucap;
-    cu.nl = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
-    const RecX o = a.rx[c0];
+    const uint32_t nw = (cu.cnt + 1) >> 1;
+    cu.wBeg           = nw * cu.part / SPLIT;
+    cu.wEnd           = nw * (cu.part + 1) / SPLIT;
+    cu.U              = a.ucount[cu.c];
+    cu.un             = a.uni + (size_t)cu.c * a.ucap;
+    cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
+    const RecX o      = a.rx[c0];
     cu.ox = o.x, cu.oy = o.y, cu.oz = o.z;
 
     const RecX r    = a.rx[cu.iSafe];
@@ -120,30 +111,62 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     if (lane == 0) s_red[wave] = ext;
     __syncthreads();
     float e = s_red[0];
-    for (int w = 1; w < kClusterWaves; ++w)
+    for (int w = 1; w < kClusterWaves * SPLIT; ++w)
         e = fmaxf(e, s_red[w]);
     cu.pbc = __builtin_amdgcn_readfirstlane(e >= 0.49f ? 1 : 0);
     return cu;
 }
 
-/*! Run body(p) over this lane's neighbors, p = LDS slot.  stage(j, slot) writes the record of particle j.
- *  `resident` carries "the whole union is already in LDS" from a previous pass over the same records. */
-template<int CH, class Stage, class Body>
-__device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Body&& body, bool& resident)
+/*! Partial sums of the SPLIT shares of each target -> every share (same order everywhere, so all shares agree).
+ *  v[f] is summed (or max-ed where bit f of maxMask is set); scratch holds NV * SPLIT * 256 floats. */
+template<int SPLIT, int NV>
+__device__ __forceinline__ void combineShares(const Clu& cu, float (&v)[NV], float* scratch, unsigned maxMask = 0,
+                                              bool scratchAliasesRecords = false)
 {
-    constexpr int S = (CH + kB - 1) / kB;
+    if constexpr (SPLIT > 1)
+    {
+        constexpr int T = SPLIT * kCluster;
+        if (scratchAliasesRecords) __syncthreads(); // every share is done reading the staged records
+#pragma unroll
+        for (int f = 0; f < NV; ++f)
+            scratch[f * T + cu.part * kCluster + cu.tid] = v[f];
+        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < NV; ++f)
+        {
+            float acc = scratch[f * T + cu.tid];
+            for (int q = 1; q < SPLIT; ++q)
+            {
+                const float x = scratch[f * T + q * kCluster + cu.tid];
+                acc           = ((maxMask >> f) & 1u) ? fmaxf(acc, x) : acc + x;
+            }
+            v[f] = acc;
+        }
+    }
+}
+
+/*! Run compute(load(p)) over this lane's share of its neighbors, p = LDS slot.  stage(j, slot) writes the record
+ *  of particle j.  `resident` carries "the whole union is already in LDS" from a previous pass over the same records.
+ *  With the union resident the loop is software-pipelined: the LDS records of the next two neighbors (one list
+ *  word) are read while the current two are computed, and list words are prefetched four ahead. */
+template<int CH, int SPLIT, class Stage, class Load, class Compute>
+__device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&& load, Compute&& compute,
+                                             bool& resident)
+{
+    constexpr int NT = kB * SPLIT;
+    constexpr int S  = (CH + NT - 1) / NT;
     auto          fill = [&](uint32_t b0, uint32_t b1) {
         uint32_t js[S];
 #pragma unroll
         for (int s = 0; s < S; ++s)
         {
-            const uint32_t u = b0 + threadIdx.x + s * kB;
+            const uint32_t u = b0 + threadIdx.x + s * NT;
             js[s]            = u < b1 ? cu.un[u] : 0u;
         }
 #pragma unroll
         for (int s = 0; s < S; ++s)
         {
-            const uint32_t u = b0 + threadIdx.x + s * kB;
+            const uint32_t u = b0 + threadIdx.x + s * NT;
             if (u < b1) stage(js[s], u - b0);
         }
     };
@@ -156,39 +179,49 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Body&
             __syncthreads();
             resident = true;
         }
-        const uint32_t  nw = (cu.cnt + 1) >> 1;
+        const uint32_t wBeg = cu.wBeg, wEnd = cu.wEnd;
+        if (wBeg >= wEnd) return;
         const uint32_t* nl = cu.nl;
-        uint32_t        q0 = 0 < nw ? nl[0] : 0u;
-        uint32_t        q1 = 1 < nw ? nl[kWave] : 0u;
-        uint32_t        q2 = 2 < nw ? nl[2 * kWave] : 0u;
-        uint32_t        q3 = 3 < nw ? nl[3 * kWave] : 0u;
-        for (uint32_t w = 0; w < nw; ++w)
+        auto            ld = [&](uint32_t w) { return w < wEnd ? nl[(size_t)w * kWave] : 0u; };
+        uint32_t        q0 = ld(wBeg + 1), q1 = ld(wBeg + 2), q2 = ld(wBeg + 3), q3 = ld(wBeg + 4);
+        const uint32_t  w0 = nl[(size_t)wBeg * kWave];
+        auto            ra = load(w0 & 0xffffu); // slot 0 for a missing odd partner: valid, never computed
+        auto            rb = load(w0 >> 16);
+        for (uint32_t w = wBeg; w < wEnd; ++w)
         {
-            const uint32_t cur = q0;
-            q0                 = q1;
-            q1                 = q2;
-            q2                 = q3;
-            q3                 = (w + 4 < nw) ? nl[(size_t)(w + 4) * kWave] : 0u;
-            body(cur & 0xffffu);
-            if (2 * w + 1 < cu.cnt) body(cur >> 16);
+            const auto ca = ra;
+            const auto cb = rb;
+            if (w + 1 < wEnd)
+            {
+                const uint32_t nx = q0;
+                q0                = q1;
+                q1                = q2;
+                q2                = q3;
+                q3                = ld(w + 5);
+                ra                = load(nx & 0xffffu);
+                rb                = load(nx >> 16);
+            }
+            compute(ca);
+            if (2 * w + 1 < cu.cnt) compute(cb);
         }
     }
     else
     {
-        resident   = false;
-        uint32_t k = 0;
+        resident         = false;
+        uint32_t       k    = 2 * cu.wBeg;
+        const uint32_t kEnd = min(cu.cnt, 2 * cu.wEnd);
         for (uint32_t b0 = 0; b0 < cu.U; b0 += CH)
         {
             const uint32_t b1 = min(cu.U, b0 + (uint32_t)CH);
             __syncthreads();
             fill(b0, b1);
             __syncthreads();
-            while (k < cu.cnt)
+            while (k < kEnd)
             {
                 const uint32_t w = cu.nl[(size_t)(k >> 1) * kWave];
                 const uint32_t p = (k & 1) ? (w >> 16) : (w & 0xffffu);
                 if (p >= b1) break;
-                body(p - b0);
+                compute(load(p - b0));
                 ++k;
             }
         }
@@ -201,63 +234,67 @@ __device__ __forceinline__ void pbcRule(const Clu& cu, const DevBox& b, float r,
 }
 
 // ---- XMass: xmassJLoop (hydro_ve/xmass_kern.hpp:50-79) ----------------------------------------------------------
-template<int CH>
-__global__ __launch_bounds__(kB) void xmassKernel(PairArgs a)
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)
 {
     __shared__ float4 sP[CH];
-    __shared__ float  s_red[kClusterWaves];
-    const Clu  cu = setup(a, s_red);
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    const Clu  cu = setup<SPLIT>(a, s_red);
     const RecX ri = a.rx[cu.iSafe];
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
     const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
-    float       rho0 = ri.m;
+    float       rho0 = cu.part == 0 ? ri.m : 0.0f;
     bool        res  = false;
-    neighborLoop<CH>(
+    neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r = a.rx[j];
             sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2), r.m);
         },
-        [&](uint32_t p) {
-            const float4 q  = sP[p];
-            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+        [&](uint32_t p) { return sP[p]; },
+        [&](const float4& q) {
+            float rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
             rho0 += kernelW(dist * hInv) * q.w;
         },
         res);
-    if (cu.valid)
+    float v[1] = {rho0};
+    combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 0u, true);
+    if (cu.valid && cu.part == 0)
     {
         const float h3Inv = hInv * hInv * hInv;
-        a.xm[cu.i]        = (float)((double)ri.m / ((double)rho0 * a.K * (double)h3Inv));
+        a.xm[cu.i]        = (float)((double)ri.m / ((double)v[0] * a.K * (double)h3Inv));
     }
 }
 
 // ---- VeDefGradh: veDefGradhJLoop (hydro_ve/ve_def_gradh_kern.hpp:43-90) -----------------------------------------
-template<int CH>
-__global__ __launch_bounds__(kB) void veDefGradhKernel(PairArgs a)
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
 {
     __shared__ float4 sP[CH];
     __shared__ float  sX[CH];
-    __shared__ float  s_red[kClusterWaves];
-    const Clu   cu     = setup(a, s_red);
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    const Clu   cu     = setup<SPLIT>(a, s_red);
     const RecX  ri     = a.rx[cu.iSafe];
     const float xmassi = a.rt[cu.iSafe].xm;
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
     const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
-    float       kxi = xmassi, whomegai = -3.0f * xmassi, wrho0i = -3.0f * ri.m;
+    const bool  own = cu.part == 0; // the self terms go to share 0
+    float       kxi = own ? xmassi : 0.0f, whomegai = own ? -3.0f * xmassi : 0.0f, wrho0i = own ? -3.0f * ri.m : 0.0f;
     bool        res = false;
-    neighborLoop<CH>(
+    neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r = a.rx[j];
             sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2), r.m);
             sX[slot] = a.rt[j].xm;
         },
-        [&](uint32_t p) {
-            const float4 q      = sP[p];
-            const float  xmassj = sX[p];
-            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+        [&](uint32_t p) { return Rec5{sP[p], sX[p]}; },
+        [&](const Rec5& r) {
+            const float4& q      = r.a;
+            const float   xmassj = r.s;
+            float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
             const float vloc = dist * hInv;
@@ -269,7 +306,12 @@ __global__ __launch_bounds__(kB) void veDefGradhKernel(PairArgs a)
             wrho0i += dterh * q.w;
         },
         res);
-    if (cu.valid)
+    {
+        float v[3] = {kxi, whomegai, wrho0i};
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 0u, true);
+        kxi = v[0], whomegai = v[1], wrho0i = v[2];
+    }
+    if (cu.valid && cu.part == 0)
     {
         const double K     = a.K;
         const float  h3Inv = hInv * hInv * hInv;
@@ -286,13 +328,14 @@ __global__ __launch_bounds__(kB) void veDefGradhKernel(PairArgs a)
 }
 
 // ---- IAD + divv/curlv: IADJLoop (iad_kern.hpp:43-109) + divV_curlVJLoop (divv_curlv_kern.hpp:43-123) -------------
-template<int CH>
-__global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, vol = xm/kx
     __shared__ float4 sV[CH]; // vx, vy, vz, xm
-    __shared__ float  s_red[kClusterWaves];
-    const Clu   cu  = setup(a, s_red);
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    __shared__ float  s_scr[SPLIT > 1 ? 9 * SPLIT * kCluster : 1];
+    const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
     const float kxi = a.rt[cu.iSafe].kx;
@@ -308,11 +351,10 @@ __global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
     };
     float t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
     bool  res = false;
-    neighborLoop<CH>(
-        cu, stage,
-        [&](uint32_t p) {
-            const float4 q  = sP[p];
-            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+    neighborLoop<CH, SPLIT>(
+        cu, stage, [&](uint32_t p) { return sP[p]; },
+        [&](const float4& q) {
+            float rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
             const float volj_w = q.w * kernelW(dist * hiInv);
@@ -324,6 +366,11 @@ __global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
             t33 += rz * rz * volj_w;
         },
         res);
+    {
+        float v[6] = {t11, t12, t13, t22, t23, t33};
+        combineShares<SPLIT>(cu, v, s_scr);
+        t11 = v[0], t12 = v[1], t13 = v[2], t22 = v[3], t23 = v[4], t33 = v[5];
+    }
     auto  getExp    = [](float v) { return v == 0.0f ? 0 : ilogbf(v); };
     int   tauExpSum = getExp(t11) + getExp(t12) + getExp(t13) + getExp(t22) + getExp(t23) + getExp(t33);
     float nrm       = ldexpf(1.0f, -tauExpSum / 6);
@@ -338,12 +385,12 @@ __global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
     const float c33i   = (t11 * t22 - t12 * t12) * factor;
 
     float dVx0 = 0, dVx1 = 0, dVx2 = 0, dVy0 = 0, dVy1 = 0, dVy2 = 0, dVz0 = 0, dVz1 = 0, dVz2 = 0;
-    neighborLoop<CH>(
-        cu, stage,
-        [&](uint32_t p) {
-            const float4 q  = sP[p];
-            const float4 v  = sV[p];
-            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+    neighborLoop<CH, SPLIT>(
+        cu, stage, [&](uint32_t p) { return Rec8{sP[p], sV[p]}; },
+        [&](const Rec8& r) {
+            const float4& q  = r.a;
+            const float4& v  = r.b;
+            float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
             const float Wi   = kernelW(dist * hiInv);
@@ -362,7 +409,14 @@ __global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
             dVz2 += tA2 * fz;
         },
         res);
-    if (cu.valid)
+    {
+        float v[9] = {dVx0, dVx1, dVx2, dVy0, dVy1, dVy2, dVz0, dVz1, dVz2};
+        __syncthreads(); // s_scr still holds the tau shares being read
+        combineShares<SPLIT>(cu, v, s_scr);
+        dVx0 = v[0], dVx1 = v[1], dVx2 = v[2], dVy0 = v[3], dVy1 = v[4], dVy2 = v[5], dVz0 = v[6], dVz1 = v[7],
+        dVz2 = v[8];
+    }
+    if (cu.valid && cu.part == 0)
     {
         const uint32_t i = cu.i;
         a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
@@ -377,14 +431,14 @@ __global__ __launch_bounds__(kB) void iadDivvCurlvKernel(PairArgs a)
 }
 
 // ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
-template<int CH>
-__global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, vol
     __shared__ float4 sV[CH]; // vx, vy, vz, c
     __shared__ float  sD[CH]; // divv
-    __shared__ float  s_red[kClusterWaves];
-    const Clu   cu  = setup(a, s_red);
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
     const RecC  ci6 = a.rc[cu.iSafe];
@@ -395,7 +449,7 @@ __global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
     float       vijsignal_i = 1.e-40f * ci;
     float       gx = 0, gy = 0, gz = 0;
     bool        res = false;
-    neighborLoop<CH>(
+    neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r = a.rx[j];
@@ -406,10 +460,11 @@ __global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
             sV[slot]     = make_float4(v.vx, v.vy, v.vz, v.c);
             sD[slot]     = a.rc[j].divv;
         },
-        [&](uint32_t p) {
-            const float4 q  = sP[p];
-            const float4 v  = sV[p];
-            float        rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+        [&](uint32_t p) { return Rec9{sP[p], sV[p], sD[p]}; },
+        [&](const Rec9& r) {
+            const float4& q  = r.a;
+            const float4& v  = r.b;
+            float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float r2    = rx * rx + ry * ry + rz * rz;
             const float rinv  = rsqrtf(r2);
@@ -422,13 +477,18 @@ __global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
             const float termA1 = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
             const float termA2 = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
             const float termA3 = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
-            const float factor = q.w * (divv_i - sD[p]);
+            const float factor = q.w * (divv_i - r.s);
             gx += factor * termA1;
             gy += factor * termA2;
             gz += factor * termA3;
         },
         res);
-    if (!cu.valid) return;
+    {
+        float v[4] = {gx, gy, gz, vijsignal_i};
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 8u, true);
+        gx = v[0], gy = v[1], gz = v[2], vijsignal_i = v[3];
+    }
+    if (!cu.valid || cu.part != 0) return;
     const float graddivv = sqrtf(gx * gx + gy * gy + gz * gz);
     float       alphaloc = 0.0f;
     if (divv_i < 0.0f)
@@ -449,16 +509,16 @@ __global__ __launch_bounds__(kB) void avSwitchesKernel(PairArgs a)
 }
 
 // ---- momentum + energy: momentumAndEnergyJLoop<avClean=false> (momentum_energy_kern.hpp:65-222) -------------------
-template<int CH>
-__global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, 1/h
     __shared__ float4 sV[CH]; // vx, vy, vz, c
     __shared__ float4 sT[CH]; // m, log2(xm), rho, prho
     __shared__ float4 sA[CH]; // alpha, c11, c12, c13
     __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
-    __shared__ float  s_red[kClusterWaves];
-    const Clu   cu  = setup(a, s_red);
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
     const RecT  ti  = a.rt[cu.iSafe];
@@ -475,7 +535,7 @@ __global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
     float       maxvsignali = 0.0f;
     float       mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
     bool        res = false;
-    neighborLoop<CH>(
+    neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r   = a.rx[j];
@@ -490,9 +550,10 @@ __global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
             sA[slot]        = make_float4(t.alpha, c6.c11, c6.c12, c6.c13);
             sB[slot]        = make_float4(c6.c22, c6.c23, c6.c33, r.m / rho);
         },
-        [&](uint32_t p) {
-            const float4 P = sP[p], V = sV[p], T = sT[p], A = sA[p], B = sB[p];
-            float        rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
+        [&](uint32_t p) { return Rec20{sP[p], sV[p], sT[p], sA[p], sB[p]}; },
+        [&](const Rec20& r) {
+            const float4 &P = r.p, &V = r.v, &T = r.t, &A = r.a, &B = r.b;
+            float         rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float r2     = rx * rx + ry * ry + rz * rz;
             const float rinv   = rsqrtf(r2);
@@ -537,8 +598,13 @@ __global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
             mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
         },
         res);
+    {
+        float v[6] = {mx, my, mz, energy, a_visc_energy, maxvsignali};
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 32u, true);
+        mx = v[0], my = v[1], mz = v[2], energy = v[3], a_visc_energy = v[4], maxvsignali = v[5];
+    }
     float dt_lane = INFINITY;
-    if (cu.valid)
+    if (cu.valid && cu.part == 0)
     {
         if (a_visc_energy < 0.0f) a_visc_energy = 0.0f;
         a.du[cu.i] = a.K * (double)(prhoi * energy + 0.5f * a_visc_energy);
@@ -550,7 +616,7 @@ __global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
     // wave min -> workgroup min -> one atomic per cluster (momentum_energy_gpu.cu:94-118)
     const float wmin = waveMin(dt_lane);
     const int   wave = threadIdx.x >> 6;
-    if (a.groupDt != nullptr && (threadIdx.x & 63) == 0 && cu.gw < a.numGroups)
+    if (a.groupDt != nullptr && (threadIdx.x & 63) == 0 && cu.part == 0 && cu.gw < a.numGroups)
     {
         float old         = a.groupDt[cu.gw];
         a.groupDt[cu.gw] = wmin < old ? wmin : old;
@@ -561,37 +627,56 @@ __global__ __launch_bounds__(kB) void momentumEnergyKernel(PairArgs a)
     if (threadIdx.x == 0)
     {
         float m = s_red[0];
-        for (int w = 1; w < kClusterWaves; ++w)
+        for (int w = 1; w < kClusterWaves * SPLIT; ++w)
             m = s_red[w] < m ? s_red[w] : m;
         atomicMinPos(a.minDt, m);
     }
 }
 
 // LDS capacity per kernel (records of 16 / 20 / 32 / 36 / 80 B): the momentum union fills the CU's 160 KiB with
-// one workgroup; the lighter kernels keep two or more workgroups per CU
-constexpr int kChXm = 2048, kChVd = 2048, kChIad = 2048, kChAv = 2048, kChMe = 2000;
+// one workgroup; the lighter kernels keep two or more workgroups per CU.  SPLIT waves share each group's lists so a
+// CU holds enough waves to reach the VALU's two-cycle issue (one wave alone issues every four cycles).
+#ifndef SX_CH_ME
+#define SX_CH_ME 2000
+#endif
+#ifndef SX_SPLIT_XM
+#define SX_SPLIT_XM 2
+#endif
+#ifndef SX_SPLIT_VD
+#define SX_SPLIT_VD 2
+#endif
+#ifndef SX_SPLIT_IAD
+#define SX_SPLIT_IAD 2
+#endif
+#ifndef SX_SPLIT_AV
+#define SX_SPLIT_AV 2
+#endif
+#ifndef SX_SPLIT_ME
+#define SX_SPLIT_ME 2
+#endif
+constexpr int kChXm = 2048, kChVd = 2048, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME;
 
 static inline unsigned clusters(const PairArgs& a) { return (a.numGroups + kClusterWaves - 1) / kClusterWaves; }
 
 void xmass(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) xmassKernel<kChXm><<<clusters(a), kB, 0, s>>>(a);
+    if (a.numGroups) xmassKernel<kChXm, SX_SPLIT_XM><<<clusters(a), kB * SX_SPLIT_XM, 0, s>>>(a);
 }
 void veDefGradh(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) veDefGradhKernel<kChVd><<<clusters(a), kB, 0, s>>>(a);
+    if (a.numGroups) veDefGradhKernel<kChVd, SX_SPLIT_VD><<<clusters(a), kB * SX_SPLIT_VD, 0, s>>>(a);
 }
 void iadDivvCurlv(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) iadDivvCurlvKernel<kChIad><<<clusters(a), kB, 0, s>>>(a);
+    if (a.numGroups) iadDivvCurlvKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
 }
 void avSwitches(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) avSwitchesKernel<kChAv><<<clusters(a), kB, 0, s>>>(a);
+    if (a.numGroups) avSwitchesKernel<kChAv, SX_SPLIT_AV><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
 }
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) momentumEnergyKernel<kChMe><<<clusters(a), kB, 0, s>>>(a);
+    if (a.numGroups) momentumEnergyKernel<kChMe, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
 
 } // namespace cluster

@@ -33,6 +33,14 @@
 namespace sx
 {
 
+#ifndef SX_NS_LOOP
+#define SX_NS_LOOP 1 // 1: prefilter loop in groups of kNsGroup candidates; 0: one candidate per iteration
+#endif
+#ifndef SX_NS_GROUP
+#define SX_NS_GROUP 4
+#endif
+constexpr int kNsGroup = SX_NS_GROUP;
+
 constexpr int kCandSpace = 1 << 16; //!< candidate particles per cluster (u16 list entries)
 constexpr int kCandWords = kCandSpace / 32;
 
@@ -42,11 +50,17 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
     return pre[w] + __popc(bits[w] & ((1u << (idx & 31)) - 1u));
 }
 
-__global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
+#ifndef SX_NS_WAVES_PER_EU
+#define SX_NS_WAVES_PER_EU 3
+#endif
+
+__global__ __launch_bounds__(kCluster) __attribute__((amdgpu_waves_per_eu(SX_NS_WAVES_PER_EU))) void
+findNeighborsKernel(NsArgs a)
 {
     __shared__ int      s_queue[kQCap];
     __shared__ int      s_cand[kCCap];
     __shared__ uint32_t s_cOff[kCCap + 1];
+    __shared__ uint32_t s_p0[kCCap]; // first particle of candidate leaf cc
     __shared__ uint32_t s_bits[kCandWords];
     __shared__ uint32_t s_pre[kCandWords];
     __shared__ double   s_box[kClusterWaves][6];
@@ -132,8 +146,10 @@ __global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
                 uint32_t sz = 0;
                 if (b + lane < nCand)
                 {
-                    const int leaf = a.internalToLeaf[s_cand[b + lane]];
-                    sz             = a.layout[leaf + 1] - a.layout[leaf];
+                    const int      leaf = a.internalToLeaf[s_cand[b + lane]];
+                    const uint32_t q0   = a.layout[leaf];
+                    sz                  = a.layout[leaf + 1] - q0;
+                    s_p0[b + lane]      = q0;
                 }
                 uint32_t incl = sz;
 #pragma unroll
@@ -199,8 +215,7 @@ __global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
             const bool reach = valid && boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, xi, yi, zi,
                                                  0.0, 0.0, 0.0, a.box) < rr * rr;
             if (__ballot(reach) == 0) continue;
-            const int      leaf = a.internalToLeaf[node];
-            const uint32_t p0 = a.layout[leaf], p1 = a.layout[leaf + 1];
+            const uint32_t p0 = s_p0[cc], p1 = p0 + (s_cOff[cc + 1] - s_cOff[cc]);
             const uint32_t base = s_cOff[cc] - p0; // candidate index of particle j = base + j
             for (uint32_t s0 = p0; s0 < p1; s0 += kWave)
             {
@@ -219,10 +234,55 @@ __global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
                 {
                     // float prefilter on cluster-relative, minimum-image coordinates; the rare candidates within the
                     // rounding band of some lane's radius are decided by the exact double test
-                    s_chunk[wave][lane] = make_float4((float)foldPbc(xj - ox, a.box, 0), (float)foldPbc(yj - oy, a.box, 1),
-                                                      (float)foldPbc(zj - oz, a.box, 2), 0.0f);
+                    // slots past the leaf end hold a far-away point: never a hit, never ambiguous
+                    const bool in = jl < p1;
+                    s_chunk[wave][lane] =
+                        make_float4(in ? (float)foldPbc(xj - ox, a.box, 0) : 3e18f, in ? (float)foldPbc(yj - oy, a.box, 1) : 0.f,
+                                    in ? (float)foldPbc(zj - oz, a.box, 2) : 0.f, 0.0f);
                     __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
                     __builtin_amdgcn_wave_barrier();
+#if SX_NS_LOOP == 1
+                    uint64_t  hm  = 0;
+                    const int ng4 = (m + kNsGroup - 1) / kNsGroup;
+                    for (int g4 = 0; g4 < ng4; ++g4)
+                    {
+                        // kNsGroup candidates straight-line (their LDS broadcasts in flight together), branch-free bits
+                        uint32_t b4  = 0;
+                        bool     amb = false;
+#pragma unroll
+                        for (int u = 0; u < kNsGroup; ++u)
+                        {
+                            const float4 q  = s_chunk[wave][g4 * kNsGroup + u];
+                            const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+                            const float  d2 = dx * dx + dy * dy + dz * dz;
+                            b4 |= (d2 < r2hi ? 1u : 0u) << u;
+                            amb = amb | ((d2 < r2hi) & (d2 >= r2lo));
+                        }
+                        if (__ballot(amb))
+                        {
+                            // rare: within the rounding band of some lane's radius; decide those candidates exactly
+                            for (int u = 0; u < kNsGroup; ++u)
+                            {
+                                const int    k  = g4 * kNsGroup + u;
+                                const float4 q  = s_chunk[wave][k];
+                                const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+                                const float  d2 = dx * dx + dy * dy + dz * dz;
+                                if (__ballot(d2 < r2hi && d2 >= r2lo) == 0) continue;
+                                const uint32_t j  = s0 + k; // uniform: scalar loads
+                                double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
+                                if (usePbc)
+                                {
+                                    ex = foldPbc(ex, a.box, 0);
+                                    ey = foldPbc(ey, a.box, 1);
+                                    ez = foldPbc(ez, a.box, 2);
+                                }
+                                const bool hit = valid && (ex * ex + ey * ey + ez * ez < radSq);
+                                b4             = hit ? (b4 | (1u << u)) : (b4 & ~(1u << u));
+                            }
+                        }
+                        hm |= (uint64_t)b4 << (g4 * kNsGroup);
+                    }
+#else
                     uint32_t hw[2] = {0u, 0u};
 #pragma unroll
                     for (int half = 0; half < 2; ++half)
@@ -253,6 +313,7 @@ __global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
                         hw[half] = bits;
                     }
                     uint64_t hm = ((uint64_t)hw[1] << 32) | hw[0];
+#endif
                     if (i >= s0 && i < s0 + (uint32_t)m) hm &= ~(1ull << (i - s0)); // j != i
                     const unsigned nh = __popcll(hm);
                     if (count + nh > a.ngmax)
@@ -418,8 +479,7 @@ __global__ __launch_bounds__(kCluster) void findNeighborsKernel(NsArgs a)
                 bits &= bits - 1u;
                 while (s_cOff[cc + 1] <= idx)
                     ++cc;
-                const int leaf = a.internalToLeaf[s_cand[cc]];
-                uni[run++]     = a.layout[leaf] + (idx - s_cOff[cc]);
+                uni[run++] = s_p0[cc] + (idx - s_cOff[cc]);
             }
         }
         __syncthreads();

@@ -379,6 +379,9 @@ struct sx_sim
 
     std::vector<hipEvent_t>  ev;
     std::vector<std::string> stageNames;
+    std::vector<hipEvent_t>  kev; // begin/end pairs around the hot kernels alone
+    std::vector<std::string> kernelNames;
+    std::vector<float>       kernelMs;
     std::vector<float>       stageMs;
     sx_nbstats               lastStats{};
     int                      haloRetries{0};
@@ -789,6 +792,12 @@ extern "C"
         for (auto& e : s->ev)
             (void)hipEventCreate(&e);
         s->stageMs.assign(s->stageNames.size(), 0.f);
+        const char* knames[] = {"findNeighbors", "xmass", "veDefGradh", "iadDivvCurlv", "avSwitches", "momentumEnergy"};
+        s->kernelNames.assign(std::begin(knames), std::end(knames));
+        s->kev.resize(2 * s->kernelNames.size());
+        for (auto& e : s->kev)
+            (void)hipEventCreate(&e);
+        s->kernelMs.assign(s->kernelNames.size(), 0.f);
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
         (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
@@ -800,6 +809,8 @@ extern "C"
         if (!s) return;
         (void)hipDeviceSynchronize();
         for (auto& e : s->ev)
+            (void)hipEventDestroy(e);
+        for (auto& e : s->kev)
             (void)hipEventDestroy(e);
         delete s;
     }
@@ -980,7 +991,9 @@ extern "C"
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
+            SIM_HIP(hipEventRecord(s->kev[0], st));
             SIM_HIP(findNeighbors(na, st));
+            SIM_HIP(hipEventRecord(s->kev[1], st));
             SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
             if (!dist) break;
             // halo sufficiency: every local particle's final h within its chunk's request margin
@@ -1007,12 +1020,16 @@ extern "C"
         PairArgs     pa = simPairArgs(s);
         // ---- XMass
         packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+        SIM_HIP(hipEventRecord(s->kev[2], st));
         H.xmass(pa, st);
+        SIM_HIP(hipEventRecord(s->kev[3], st));
         if (int e = haloExchange(s, {{s->xm, 4}}, st)) return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- VeDefGradh
         packT(n, s->xm, nullptr, nullptr, nullptr, s->rt, st);
+        SIM_HIP(hipEventRecord(s->kev[4], st));
         H.veDefGradh(pa, st);
+        SIM_HIP(hipEventRecord(s->kev[5], st));
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- EOS, then the v/prho/c/kx halo exchange
         EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
@@ -1024,7 +1041,9 @@ extern "C"
         // ---- IAD + divv/curlv, rho time-step, then the c_ij/divv exchange
         packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
         packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
+        SIM_HIP(hipEventRecord(s->kev[6], st));
         H.iadDivvCurlv(pa, st);
+        SIM_HIP(hipEventRecord(s->kev[7], st));
         SIM_HIP(maxFloat(s->divv, (uint32_t)s->first, (uint32_t)s->last, &s->sc->maxDivvU, st));
         if (int e = haloExchange(
                 s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}}, st))
@@ -1032,12 +1051,16 @@ extern "C"
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- AV switches, then the alpha exchange
         packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, s->divv, s->rc, st);
+        SIM_HIP(hipEventRecord(s->kev[8], st));
         H.avSwitches(pa, st);
+        SIM_HIP(hipEventRecord(s->kev[9], st));
         if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- momentum + energy
         packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
+        SIM_HIP(hipEventRecord(s->kev[10], st));
         H.momentumEnergy(pa, st);
+        SIM_HIP(hipEventRecord(s->kev[11], st));
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- integrate: global time-step, positions, h
         dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease);
@@ -1073,6 +1096,8 @@ extern "C"
 
         for (size_t k = 0; k < s->stageMs.size(); ++k)
             (void)hipEventElapsedTime(&s->stageMs[k], s->ev[k], s->ev[k + 1]);
+        for (size_t k = 0; k < s->kernelMs.size(); ++k)
+            (void)hipEventElapsedTime(&s->kernelMs[k], s->kev[2 * k], s->kev[2 * k + 1]);
         s->lastStats.numFailed     = s->statsHost[1];
         s->lastStats.maxNeighbors  = s->statsHost[2];
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);
@@ -1093,6 +1118,17 @@ extern "C"
         out[3] = s->scHost->minDtCourant;
         out[4] = s->scHost->minDtRho;
         return SX_OK;
+    }
+
+    int sx_sim_kernel_times(sx_sim* s, float* ms, int cap, const char** names)
+    {
+        int k = 0;
+        for (; k < cap && k < (int)s->kernelMs.size(); ++k)
+        {
+            ms[k] = s->kernelMs[k];
+            if (names) names[k] = s->kernelNames[k].c_str();
+        }
+        return k;
     }
 
     int sx_sim_stage_times(sx_sim* s, float* ms, int cap, const char** names)

@@ -12,7 +12,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(os.path.dirname(HERE))          # .../sph-exa_amd
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libsphexa_hip.so")
+# SPHEXA_AMD_LIB selects another in-tree build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("SPHEXA_AMD_LIB") or os.path.join(PKG, "lib", "libsphexa_hip.so")
 HEADER = os.path.join(ROOT, "include", "sphexa_hip.h")
 
 SX_OK, SX_ERR_TRAVERSAL, SX_ERR_NOT_CONVERGED, SX_ERR_HIP, SX_ERR_ARG, SX_ERR_NOMEM = range(6)
@@ -104,6 +105,7 @@ def lib():
         "sx_set_exact": (C.c_int, [vp, C.c_int]),
         "sx_kernel_constant": (C.c_double, []),
         "sx_copy_tables": (C.c_int, [vp, vp, vp]),
+        "sx_kernel_poly": (C.c_int, [vp, C.c_size_t, vp, vp]),
         "sx_synchronize": (C.c_int, [vp]),
         "sx_device_alloc": (vp, [vp, sz]),
         "sx_device_free": (C.c_int, [vp, vp]),
@@ -148,6 +150,7 @@ def lib():
         "sx_sim_scalars": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sx_sim_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_last_stats": (C.c_int, [vp, C.POINTER(SxNbStats)]),
+        "sx_sim_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_set_comm": (C.c_int, [vp, vp]),
         "sx_sim_init_sedov_rank": (C.c_int, [vp, u32, C.c_int, C.c_int]),
         "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
@@ -412,6 +415,12 @@ class Sim:
         ms = (C.c_float * 16)()
         names = (C.c_char_p * 16)()
         k = self.L.sx_sim_stage_times(self.h, ms, 16, names)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def kernel_times(self):
+        ms = (C.c_float * 16)()
+        names = (C.c_char_p * 16)()
+        k = self.L.sx_sim_kernel_times(self.h, ms, 16, names)
         return {names[i].decode(): ms[i] for i in range(k)}
 
     def stats(self):

@@ -28,6 +28,35 @@ def test_kernel_constant_and_tables_match_oracle():
     assert np.array_equal(wh, ora.wh) and np.array_equal(whd, ora.whd)
 
 
+def test_kernel_poly_matches_sinc6_and_tables():
+    """The fast pair kernels evaluate W = sinc(pi v/2)^6 and dW/dv by a degree-6 polynomial in v^2
+    (sx_kernel_poly.hpp) instead of the 20000-point tables; its error is of the order of the tables' own."""
+    L = sx.lib()
+    v = np.linspace(0.0, 2.1, 400001).astype(np.float32)
+    w = np.zeros_like(v)
+    dw = np.zeros_like(v)
+    assert L.sx_kernel_poly(v.ctypes.data, v.size, w.ctypes.data, dw.ctypes.data) == 0
+    x = np.pi / 2 * v.astype(np.float64)
+    s = np.where(x > 0, np.sin(x) / np.where(x > 0, x, 1.0), 1.0)
+    ds = np.where(x > 0, np.pi / 2 * (np.cos(x) / np.where(x > 0, x, 1.0) - np.sin(x) / np.where(x > 0, x, 1.0) ** 2),
+                  0.0)
+    inside = v < 2.0
+    w_ex = np.where(inside, s ** 6, 0.0)
+    dw_ex = np.where(inside, 6 * s ** 5 * ds, 0.0)
+    assert np.max(np.abs(w - w_ex)) < 4e-7  # tables: 1.1e-7 (float interpolation of float samples)
+    assert np.max(np.abs(dw - dw_ex)) < 1e-6  # tables: 2.2e-7
+    # the reference tables (linear interpolation, lt::lookup) differ from the exact function by the same order
+    wh = np.zeros(sx.KTABLE, np.float32)
+    whd = np.zeros(sx.KTABLE, np.float32)
+    L.sx_copy_tables(None, wh.ctypes.data, whd.ctypes.data)
+    dx = np.float32(2.0) / np.float32(sx.KTABLE - 1)
+    idx = (v[inside] * (np.float32(1.0) / dx)).astype(np.int64)
+    ok = idx < sx.KTABLE - 1
+    vi, ii = v[inside][ok], idx[ok]
+    lut = wh[ii] + (wh[ii + 1] - wh[ii]) / dx * (vi - ii.astype(np.float32) * dx)
+    assert np.max(np.abs(lut - w[inside][ok])) < 4e-7
+
+
 def test_update_h_needs_glibc_powf_table():
     """updateH calls std::pow(float,float) = glibc powf, which is not correctly rounded: on nc = 1..2e5 (ng0=100) it
     differs from a correctly rounded pow for 100+ values (first at nc=488).  This is why the device takes the factor
