@@ -33,9 +33,6 @@
 namespace sx
 {
 
-#ifndef SX_NS_LOOP
-#define SX_NS_LOOP 1 // 1: prefilter loop in groups of kNsGroup candidates; 0: one candidate per iteration
-#endif
 #ifndef SX_NS_GROUP
 #define SX_NS_GROUP 4
 #endif
@@ -60,7 +57,8 @@ findNeighborsKernel(NsArgs a)
     __shared__ int      s_queue[kQCap];
     __shared__ int      s_cand[kCCap];
     __shared__ uint32_t s_cOff[kCCap + 1];
-    __shared__ uint32_t s_p0[kCCap]; // first particle of candidate leaf cc
+    __shared__ uint32_t s_p0[kCCap];    // first particle of candidate leaf cc
+    __shared__ uint8_t  s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
     __shared__ uint32_t s_bits[kCandWords];
     __shared__ uint32_t s_pre[kCandWords];
     __shared__ double   s_box[kClusterWaves][6];
@@ -118,8 +116,14 @@ findNeighborsKernel(NsArgs a)
     const double gsx = 0.5 * (bx1 - bx0), gsy = 0.5 * (by1 - by0), gsz = 0.5 * (bz1 - bz0);
 
     int numCand = 0;
+#ifdef SX_NS_PROFILE
+    uint64_t prof[5] = {0, 0, 0, 0, 0}; // cycles: candidates+scan, stream, tests, -, union+rewrite
+#endif
     while (true)
     {
+#ifdef SX_NS_PROFILE
+        const uint64_t tB = __builtin_readcyclecounter();
+#endif
         // ---- 2. candidate leaves for radius 2*hmax of the cluster, numbered into the candidate space -----
         const float hmaxW = waveMax(valid ? hi : 0.0f);
         if (lane == 0) s_hmax[wave] = hmaxW;
@@ -171,14 +175,37 @@ findNeighborsKernel(NsArgs a)
         }
         __syncthreads();
         numCand = s_numCand;
+        // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
+        // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
+        for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
+        {
+            const int node = s_cand[cc];
+            uint32_t  bits = 0;
+            for (int w = 0; w < kClusterWaves; ++w)
+            {
+                const float hw = s_hmax[w];
+                if (hw <= 0.0f) continue; // no valid lane
+                const double R  = 2.0 * (double)hw * (1.0 + 1e-6) + a.margin;
+                const double d2 = boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node,
+                                           0.5 * (s_box[w][0] + s_box[w][1]), 0.5 * (s_box[w][2] + s_box[w][3]),
+                                           0.5 * (s_box[w][4] + s_box[w][5]), 0.5 * (s_box[w][1] - s_box[w][0]),
+                                           0.5 * (s_box[w][3] - s_box[w][2]), 0.5 * (s_box[w][5] - s_box[w][4]), a.box);
+                if (d2 < R * R) bits |= 1u << w;
+            }
+            s_reach[cc] = (uint8_t)bits;
+        }
         if (local)
         {
             const uint32_t nw = (s_cOff[numCand] + 31) / 32;
             for (uint32_t w = threadIdx.x; w < nw; w += kCluster)
                 s_bits[w] = 0;
-            __syncthreads();
         }
+        __syncthreads();
 
+#ifdef SX_NS_PROFILE
+        prof[0] += __builtin_readcyclecounter() - tB;
+        const uint64_t tS = __builtin_readcyclecounter();
+#endif
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f       = 4.0f * hi * hi;
         const double radSq     = (double)r2f;
@@ -188,7 +215,6 @@ findNeighborsKernel(NsArgs a)
                             (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
         const bool   usePbc    = a.box.anyPbc && !inside;
         const bool   anyPbcUse = __ballot(usePbc && valid) != 0;
-        const double rr        = 2.0 * (double)(valid ? hi : 0.0f) * (1.0 + 1e-6) + a.margin;
         // float prefilter: cluster-relative minimum-image coordinates are exact displacements for every pair
         // closer than 2h when |x_i - o| + 2h < L/2 on the periodic axes; rounding band tol on d2
         const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
@@ -208,28 +234,55 @@ findNeighborsKernel(NsArgs a)
         count         = 0;
         stored        = 0;
         uint32_t pend = 0; // low half of the next u16-pair word
-        for (int cc = 0; cc < numCand; ++cc)
-        {
-            const int node = s_cand[cc];
-            // per-lane sphere-vs-leaf prune (conservative): the wave tests the leaf only if one of its lanes can reach it
-            const bool reach = valid && boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, xi, yi, zi,
-                                                 0.0, 0.0, 0.0, a.box) < rr * rr;
-            if (__ballot(reach) == 0) continue;
-            const uint32_t p0 = s_p0[cc], p1 = p0 + (s_cOff[cc + 1] - s_cOff[cc]);
-            const uint32_t base = s_cOff[cc] - p0; // candidate index of particle j = base + j
-            for (uint32_t s0 = p0; s0 < p1; s0 += kWave)
+        // this wave's chunks in stream order: (leaf cc, first particle s0), next one's coordinates prefetched
+        const uint32_t wbit  = 1u << wave;
+        auto           after = [&](int cc, uint32_t s0, int& ncc, uint32_t& ns0) {
+            // the chunk following (cc, s0); ncc = numCand when none is left
+            if (cc >= 0)
             {
-                const int      m  = (int)min<uint32_t>(kWave, p1 - s0);
-                const uint32_t jl = s0 + lane;
-                double         xj = 0, yj = 0, zj = 0;
-                if (jl < p1)
+                const uint32_t p1 = s_p0[cc] + (s_cOff[cc + 1] - s_cOff[cc]);
+                if (s0 + kWave < p1)
                 {
-                    xj = a.x[jl];
-                    yj = a.y[jl];
-                    zj = a.z[jl];
+                    ncc = cc, ns0 = s0 + kWave;
+                    return;
+                }
+            }
+            for (++cc; cc < numCand; ++cc)
+                if ((s_reach[cc] & wbit) && s_cOff[cc + 1] > s_cOff[cc]) break;
+            ncc = cc, ns0 = cc < numCand ? s_p0[cc] : 0u;
+        };
+        int      cc = 0;
+        uint32_t s0 = 0;
+        after(-1, 0, cc, s0);
+        double xn = 0, yn = 0, zn = 0; // coordinates of the chunk at (cc, s0)
+        if (cc < numCand)
+        {
+            const uint32_t p1 = s_p0[cc] + (s_cOff[cc + 1] - s_cOff[cc]);
+            if (s0 + lane < p1) xn = a.x[s0 + lane], yn = a.y[s0 + lane], zn = a.z[s0 + lane];
+        }
+        while (cc < numCand)
+        {
+            {
+                const uint32_t p0 = s_p0[cc], p1 = p0 + (s_cOff[cc + 1] - s_cOff[cc]);
+                const uint32_t base = s_cOff[cc] - p0; // candidate index of particle j = base + j
+                const int      m    = (int)min<uint32_t>(kWave, p1 - s0);
+                const uint32_t jl   = s0 + lane;
+                const double   xj = xn, yj = yn, zj = zn;
+                // prefetch the next chunk while this one is tested
+                int      ncc;
+                uint32_t ns0;
+                after(cc, s0, ncc, ns0);
+                xn = yn = zn = 0;
+                if (ncc < numCand)
+                {
+                    const uint32_t np1 = s_p0[ncc] + (s_cOff[ncc + 1] - s_cOff[ncc]);
+                    if (ns0 + lane < np1) xn = a.x[ns0 + lane], yn = a.y[ns0 + lane], zn = a.z[ns0 + lane];
                 }
                 candTested += m;
                 uint64_t lm = 0; // this lane's stored hits in the chunk
+#ifdef SX_NS_PROFILE
+                uint64_t tP = 0;
+#endif
                 if (fastWave)
                 {
                     // float prefilter on cluster-relative, minimum-image coordinates; the rare candidates within the
@@ -241,7 +294,9 @@ findNeighborsKernel(NsArgs a)
                                     in ? (float)foldPbc(zj - oz, a.box, 2) : 0.f, 0.0f);
                     __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
                     __builtin_amdgcn_wave_barrier();
-#if SX_NS_LOOP == 1
+#ifdef SX_NS_PROFILE
+                    const uint64_t tT = __builtin_readcyclecounter();
+#endif
                     uint64_t  hm  = 0;
                     const int ng4 = (m + kNsGroup - 1) / kNsGroup;
                     for (int g4 = 0; g4 < ng4; ++g4)
@@ -282,37 +337,9 @@ findNeighborsKernel(NsArgs a)
                         }
                         hm |= (uint64_t)b4 << (g4 * kNsGroup);
                     }
-#else
-                    uint32_t hw[2] = {0u, 0u};
-#pragma unroll
-                    for (int half = 0; half < 2; ++half)
-                    {
-                        const int kEnd = min(m, 32 * (half + 1));
-                        uint32_t  bits = 0;
-                        for (int k = 32 * half; k < kEnd; ++k)
-                        {
-                            const float4 q  = s_chunk[wave][k];
-                            const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
-                            const float  d2 = dx * dx + dy * dy + dz * dz;
-                            bool         hit = d2 < r2hi;
-                            if (__ballot(hit && d2 >= r2lo))
-                            {
-                                // exact reference criterion for this candidate (uniform address: scalar loads)
-                                const uint32_t j   = s0 + k;
-                                double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
-                                if (usePbc)
-                                {
-                                    ex = foldPbc(ex, a.box, 0);
-                                    ey = foldPbc(ey, a.box, 1);
-                                    ez = foldPbc(ez, a.box, 2);
-                                }
-                                hit = valid && (ex * ex + ey * ey + ez * ez < radSq);
-                            }
-                            if (hit) bits |= 1u << (k & 31);
-                        }
-                        hw[half] = bits;
-                    }
-                    uint64_t hm = ((uint64_t)hw[1] << 32) | hw[0];
+#ifdef SX_NS_PROFILE
+                    tP = __builtin_readcyclecounter();
+                    prof[2] += tP - tT;
 #endif
                     if (i >= s0 && i < s0 + (uint32_t)m) hm &= ~(1ull << (i - s0)); // j != i
                     const unsigned nh = __popcll(hm);
@@ -383,14 +410,29 @@ findNeighborsKernel(NsArgs a)
                         else part = sh ? (uint32_t)(wm >> (64 - sh)) : 0u;
                         if (part) atomicOr(&s_bits[w0 + lane], part);
                     }
-                    while (lm)
+                    // append two hits per iteration (one u16-pair word per iteration), 32-bit halves
+#pragma unroll
+                    for (int half = 0; half < 2; ++half)
                     {
-                        const uint32_t k = __builtin_ctzll(lm);
-                        lm &= lm - 1ull;
-                        const uint32_t idx = b0 + k;
-                        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend | (idx << 16);
-                        else pend = idx;
-                        stored++;
+                        uint32_t       hb   = half ? (uint32_t)(lm >> 32) : (uint32_t)lm;
+                        const uint32_t hb0  = b0 + 32u * half;
+                        while (hb)
+                        {
+                            const uint32_t e1 = hb0 + __builtin_ctz(hb);
+                            hb &= hb - 1u;
+                            const bool     two = hb != 0u;
+                            const uint32_t e2  = hb0 + (two ? __builtin_ctz(hb) : 0u);
+                            if (two) hb &= hb - 1u;
+                            uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
+                            if (stored & 1u)
+                            {
+                                *dst = pend | (e1 << 16);
+                                pend = e2;
+                            }
+                            else if (two) { *dst = e1 | (e2 << 16); }
+                            else { pend = e1; }
+                            stored += two ? 2u : 1u;
+                        }
                     }
                 }
                 else
@@ -403,10 +445,17 @@ findNeighborsKernel(NsArgs a)
                         stored++;
                     }
                 }
+#ifdef SX_NS_PROFILE
+                if (fastWave) prof[3] += __builtin_readcyclecounter() - tP;
+#endif
+                cc = ncc, s0 = ns0;
             }
         }
         if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
+#ifdef SX_NS_PROFILE
+        prof[1] += __builtin_readcyclecounter() - tS;
+#endif
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -435,6 +484,9 @@ findNeighborsKernel(NsArgs a)
         __syncthreads(); // s_again / s_hmax / candidate space are rewritten by the next iteration
     }
 
+#ifdef SX_NS_PROFILE
+    const uint64_t tU = __builtin_readcyclecounter();
+#endif
     // ---- 5. cluster union: prefix popcount of the bitmap, union entries, list rewrite -----------------------
     uint32_t ucnt = 0;
     if (local)
@@ -479,7 +531,9 @@ findNeighborsKernel(NsArgs a)
                 bits &= bits - 1u;
                 while (s_cOff[cc + 1] <= idx)
                     ++cc;
-                uni[run++] = s_p0[cc] + (idx - s_cOff[cc]);
+                if (run < a.ucap) uni[run] = s_p0[cc] + (idx - s_cOff[cc]);
+                else atomicOr(&a.stats[0], 1u); // union larger than its capacity: reported as a traversal error
+                ++run;
             }
         }
         __syncthreads();
@@ -495,6 +549,12 @@ findNeighborsKernel(NsArgs a)
         if (threadIdx.x == 0) a.ucount[c] = ucnt;
     }
 
+#ifdef SX_NS_PROFILE
+    prof[4] = __builtin_readcyclecounter() - tU;
+    if (lane == 0)
+        for (int q = 0; q < 5; ++q)
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 12 + 2 * q), (unsigned long long)prof[q]);
+#endif
     if (valid)
     {
         a.nc[i] = count + 1;

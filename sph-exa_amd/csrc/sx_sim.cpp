@@ -21,6 +21,8 @@
  * then vx,vy,vz,prho,c,kx, then c11..c33,divv, then alpha.
  */
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -1103,6 +1105,14 @@ extern "C"
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
+#ifdef SX_NS_PROFILE
+        {
+            const uint64_t* pr = reinterpret_cast<const uint64_t*>(s->statsHost + 12);
+            const double nwv = (double)((s->last - s->first) / 64);
+            fprintf(stderr, "nsprof cycles/wave: candidates %.0f stream %.0f tests %.0f post-test %.0f union %.0f\n",
+                    pr[0] / nwv, pr[1] / nwv, pr[2] / nwv, pr[3] / nwv, pr[4] / nwv);
+        }
+#endif
         if (s->statsHost[0] & 1u) return SX_ERR_TRAVERSAL;
         return SX_OK;
     }
