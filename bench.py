@@ -31,15 +31,20 @@ MOM_COMPULSORY_OWN = 96 + 4 + 20
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 --pmc summary (scripts/gpu_pmc.sh +
-    scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None."""
+def pmc_traffic(kernel_prefix, particles):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 --pmc summary of the same workload
+    (scripts/gpu_pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None
+    when the summary was taken on another particle count."""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
+    if d.get("_meta", {}).get("particles_per_gpu") != particles:
+        return None
     for k, v in d.items():
+        if k == "_meta":
+            continue
         if kernel_prefix in k and "hbm_read_bytes_est" in v and "hbm_write_bytes_est" in v:
             return v["hbm_read_bytes_est"] + v["hbm_write_bytes_est"]
     return None
@@ -104,14 +109,34 @@ def main():
 
     side = args.side or int(round(200 * n_gpus ** (1.0 / 3.0)))
     n_total = side ** 3
-    ctx = sx.Context(0 if args.backend == "host" else local, exact=args.exact)
+    device = 0
+    if args.backend != "host":
+        import torch  # device_count() does not initialise the GPU runtime
+
+        device = local % max(1, torch.cuda.device_count())
+    ctx = sx.Context(device, exact=args.exact)
     box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
     # capacity: the rank's share plus halos (surface layer of the SFC domain) with headroom
     cap = n_total if world == 1 else int(1.6 * n_total / world) + 65536
     sim = sx.Sim(ctx, cap, box, bucket=args.bucket)
     comm = None
+    transport = args.backend
     if world > 1:
-        comm = sx.Comm(args.backend)
+        try:
+            comm = sx.Comm(args.backend)
+            ok = 1
+        except sx.SxError as e:  # e.g. RCCL refusing the node's topology: keep the run alive on the staged path
+            print(f"rank {rank}: {e}; falling back to the host-staged transport", file=sys.stderr)
+            ok = 0
+        import torch
+
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank must use the same transport
+        if int(flag.item()) == 0:
+            if comm is not None:
+                comm.close()
+            comm = sx.Comm("host")
+            transport = f"host (fallback: {args.backend} communicator creation failed)"
         sim.set_comm(comm)
     sim.init_sedov(side, rank, world)
     for _ in range(args.warmup):
@@ -167,11 +192,11 @@ def main():
         "config": {"workload": f"Sedov -n {side} ({side ** 3} particles), VE propagator, {args.steps} steps",
                    "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
                    "parallelism": "1 GPU" if world == 1 else
-                   f"{world} GPUs: SFC domain decomposition, RCCL halo + particle exchange ({args.backend})",
+                   f"{world} GPUs: SFC domain decomposition, halo + particle exchange over {transport}",
                    "halos_per_gpu": sim.layout()["n"] - n_local,
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
         "roofline": {"bound": "hbm", "kernel": "momentumEnergyKernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("momentumEnergyKernel"),
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("momentumEnergyKernel", n_local),
                      "algorithmic_bytes_per_launch": mom_bytes, "avg_launch_ms": mom_ms,
                      "model": f"edge model (SURVEY.md 8(d)): {MOM_OWN_BYTES} B own + {ng:.1f} neighbors x "
                               f"{MOM_EDGE_BYTES} B; effective bandwidth, neighbor records come from LDS",

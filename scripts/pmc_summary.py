@@ -28,11 +28,22 @@ for k, cs in acc.items():
     if dur.get(k):
         d["profiled_ms"] = sum(dur[k]) / len(dur[k])
     out[k] = d
-keys = sorted(out, key=lambda k: -out[k].get("profiled_ms", 0))
+keys = sorted((k for k in out if k != "_meta"), key=lambda k: -out[k].get("profiled_ms", 0))
 for k in keys[:10]:
     d = out[k]
     print(f"{k[:40]:40s} ms={d.get('profiled_ms', 0):7.3f} rd={d.get('hbm_read_bytes_est', 0)/1e9:7.3f}GB "
           f"wr={d.get('hbm_write_bytes_est', 0)/1e9:6.3f}GB L2hit={d.get('l2_hit_rate', 0):.3f} "
           f"vmem_rd={d.get('SQ_INSTS_VMEM_RD', 0):.3g} valu={d.get('SQ_INSTS_VALU', 0):.3g}")
 if len(sys.argv) > 2:
+    # the workload the passes ran (bench.py's JSON line of the last pass), so bench.py only reuses matching traffic
+    meta = {}
+    for lf in sorted(glob.glob(os.path.join(root, "p*.log")))[-1:]:
+        for line in open(lf):
+            if line.startswith("{"):
+                try:
+                    d = json.loads(line)
+                    meta = {"particles_per_gpu": d["config"]["particles_per_gpu"], "workload": d["config"]["workload"]}
+                except (ValueError, KeyError):
+                    pass
+    out["_meta"] = meta
     json.dump(out, open(sys.argv[2], "w"), indent=1)
