@@ -383,6 +383,8 @@ extern "C"
         a.margin         = quantMargin(a.box);
         a.stats          = c->stats;
         a.powTab         = ensurePowTab(c, p->ng0);
+        a.numLeaves      = tree->numLeafNodes;
+        a.qrel           = c->arena.get<float>("ns.qrel", qrelFloats(f->n));
         if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);

@@ -47,6 +47,51 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
     return pre[w] + __popc(bits[w] & ((1u << (idx & 31)) - 1u));
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+constexpr int kDCap = kCandWords * 4 / 16; //!< leaf frames cached in LDS (aliasing s_pre)
+
+/*! Frame of a candidate leaf for the float prefilter: d = fold(anchor - o) with anchor = the leaf's first particle
+ *  (the frame of the qrel records, leafFrameKernel), o = the cluster origin; .w = Qd + 2|d| (Qd = diagonal of
+ *  the leaf box inflated by the key-quantisation margin, bounding |x_j - anchor|), or -1 when on some periodic
+ *  axis |d| + width reaches L/2 (the records might then sit in another image than the fold picks). */
+__device__ __forceinline__ float4 leafFrame(const NsArgs& a, int node, uint32_t p0, double ox, double oy, double oz)
+{
+    const double dx = foldPbc(a.x[p0] - ox, a.box, 0), dy = foldPbc(a.y[p0] - oy, a.box, 1),
+                 dz = foldPbc(a.z[p0] - oz, a.box, 2);
+    const double wx = 2.0 * (a.sizes[3 * (size_t)node] + a.margin),
+                 wy = 2.0 * (a.sizes[3 * (size_t)node + 1] + a.margin),
+                 wz = 2.0 * (a.sizes[3 * (size_t)node + 2] + a.margin);
+    bool ok = true;
+    if (a.box.pbc[0] && fabs(dx) + wx >= 0.499 * a.box.l[0]) ok = false;
+    if (a.box.pbc[1] && fabs(dy) + wy >= 0.499 * a.box.l[1]) ok = false;
+    if (a.box.pbc[2] && fabs(dz) + wz >= 0.499 * a.box.l[2]) ok = false;
+    const double E0 = (sqrt(wx * wx + wy * wy + wz * wz) + 2.0 * sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-5);
+    return make_float4((float)dx, (float)dy, (float)dz, ok ? (float)E0 : -1.0f);
+}
+
+//! per-particle records of the float prefilter in pair layout: pair p = particles (2p, 2p+1) holds
+//! {qx_a, qx_b, qy_a, qy_b, qz_a, qz_b, qw_a, qw_b} with q = x - anchor(leaf) in f32 and qw = |q|^2; one wave per leaf
+__global__ void leafFrameKernel(const uint32_t* __restrict__ layout, int numLeaves, const double* __restrict__ x,
+                                const double* __restrict__ y, const double* __restrict__ z, float* __restrict__ q)
+{
+    const int L    = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (L >= numLeaves) return;
+    const uint32_t p0 = layout[L], p1 = layout[L + 1];
+    if (p1 <= p0) return;
+    const double ax = x[p0], ay = y[p0], az = z[p0];
+    for (uint32_t j = p0 + lane; j < p1; j += 64)
+    {
+        const float qx = (float)(x[j] - ax), qy = (float)(y[j] - ay), qz = (float)(z[j] - az);
+        float*      P  = q + (size_t)(j >> 1) * 8 + (j & 1);
+        P[0]           = qx;
+        P[2]           = qy;
+        P[4]           = qz;
+        P[6]           = qx * qx + qy * qy + qz * qz;
+    }
+}
+
 #ifndef SX_NS_WAVES_PER_EU
 #define SX_NS_WAVES_PER_EU 3
 #endif
@@ -67,6 +112,8 @@ findNeighborsKernel(NsArgs a)
     __shared__ uint32_t s_wsum[kClusterWaves];
     __shared__ float4   s_chunk[kClusterWaves][kWave];
     __shared__ int      s_numCand;
+    // leaf frames of the first kDCap candidate leaves; s_pre is only used after the last stream
+    float4* const s_d = reinterpret_cast<float4*>(s_pre);
 
     const int      wave  = threadIdx.x >> 6;
     const int      lane  = threadIdx.x & 63;
@@ -193,6 +240,7 @@ findNeighborsKernel(NsArgs a)
                 if (d2 < R * R) bits |= 1u << w;
             }
             s_reach[cc] = (uint8_t)bits;
+            if (cc < kDCap && a.qrel) s_d[cc] = leafFrame(a, node, s_p0[cc], ox, oy, oz);
         }
         if (local)
         {
@@ -214,9 +262,8 @@ findNeighborsKernel(NsArgs a)
                             (zi - tw >= a.box.lim[4]) && (xi + tw <= a.box.lim[1]) &&
                             (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
         const bool   usePbc    = a.box.anyPbc && !inside;
-        const bool   anyPbcUse = __ballot(usePbc && valid) != 0;
         // float prefilter: cluster-relative minimum-image coordinates are exact displacements for every pair
-        // closer than 2h when |x_i - o| + 2h < L/2 on the periodic axes; rounding band tol on d2
+        // closer than 2h when |x_i - o| + 2h < L/2 on the periodic axes
         const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
                     zr = (float)foldPbc(zi - oz, a.box, 2);
         bool safe = true;
@@ -225,231 +272,241 @@ findNeighborsKernel(NsArgs a)
             const float rd = d == 0 ? xr : (d == 1 ? yr : zr);
             if (a.box.pbc[d] && (fabsf(rd) + 2.05f * hi) >= 0.49f * (float)a.box.l[d]) safe = false;
         }
-        const bool  fastWave = __ballot(valid && !safe) == 0;
-        const float ext      = fmaxf(fabsf(xr), fmaxf(fabsf(yr), fabsf(zr))) + 2.0f * hi;
-        const float tol      = 7.62939453125e-06f * hi * (ext + hi) + 1e-30f; // 2^-17 h (E + h)
-        const float r2hi     = valid ? r2f + tol : -1.0f;
-        const float r2lo     = r2f - tol;
+        const bool  fastWave = a.qrel != nullptr && __ballot(valid && !safe) == 0;
+        const float thr      = valid ? r2f : -1e30f; // invalid lanes: t ~ +1e30, never a hit, never ambiguous
+        const float rn2      = 2.0f * sqrtf(xr * xr + yr * yr + zr * zr);
+
+        // the reference criterion in double for candidates [s0, s0 + m): this lane's hits as bits from s0
+        auto exactChunk = [&](uint32_t s0, int m) -> uint64_t {
+            double xj = 0, yj = 0, zj = 0;
+            if (lane < m) xj = a.x[s0 + lane], yj = a.y[s0 + lane], zj = a.z[s0 + lane];
+            uint64_t hm = 0;
+            for (int k = 0; k < m; ++k)
+            {
+                double dx = readlaneD(xj, k) - xi;
+                double dy = readlaneD(yj, k) - yi;
+                double dz = readlaneD(zj, k) - zi;
+                if (usePbc)
+                {
+                    dx = foldPbc(dx, a.box, 0);
+                    dy = foldPbc(dy, a.box, 1);
+                    dz = foldPbc(dz, a.box, 2);
+                }
+                if (valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i) hm |= 1ull << k;
+            }
+            return hm;
+        };
 
         count         = 0;
         stored        = 0;
         uint32_t pend = 0; // low half of the next u16-pair word
-        // this wave's chunks in stream order: (leaf cc, first particle s0), next one's coordinates prefetched
-        const uint32_t wbit  = 1u << wave;
-        auto           after = [&](int cc, uint32_t s0, int& ncc, uint32_t& ns0) {
-            // the chunk following (cc, s0); ncc = numCand when none is left
-            if (cc >= 0)
+        // chunk sequence of this wave: (candidate leaf cc, even start s0a) in stream order, chunks of 64 candidate
+        // slots aligned to particle pairs; the next chunk's leaf-frame pairs are prefetched into registers.
+        // Reachable non-empty leaves are found 64 at a time: lane l of the window holds leaf wb + l, a ballot gives
+        // the window's reachable set (wave-uniform scalar iteration, no dependent LDS reads per leaf)
+        const uint32_t wbit = 1u << wave;
+        struct Chunk
+        {
+            int      cc;
+            uint32_t s0a, p0, p1, base;
+        };
+        int      wb  = -kWave;
+        uint64_t rm  = 0;
+        uint32_t wp0 = 0, wcnt = 0, wco = 0;
+        auto     advance = [&](Chunk& q) {
+            if (q.cc >= 0 && q.cc < numCand && q.s0a + kWave < q.p1)
             {
-                const uint32_t p1 = s_p0[cc] + (s_cOff[cc + 1] - s_cOff[cc]);
-                if (s0 + kWave < p1)
+                q.s0a += kWave;
+                return;
+            }
+            while (rm == 0)
+            {
+                wb += kWave;
+                if (wb >= numCand)
                 {
-                    ncc = cc, ns0 = s0 + kWave;
+                    q.cc = numCand;
                     return;
                 }
+                const int l = wb + lane;
+                wp0 = 0, wcnt = 0, wco = 0;
+                bool r = false;
+                if (l < numCand)
+                {
+                    wp0  = s_p0[l];
+                    wco  = s_cOff[l];
+                    wcnt = s_cOff[l + 1] - wco;
+                    r    = (s_reach[l] & wbit) && wcnt > 0;
+                }
+                rm = __ballot(r);
             }
-            for (++cc; cc < numCand; ++cc)
-                if ((s_reach[cc] & wbit) && s_cOff[cc + 1] > s_cOff[cc]) break;
-            ncc = cc, ns0 = cc < numCand ? s_p0[cc] : 0u;
+            const int k = __builtin_ctzll(rm);
+            rm &= rm - 1ull;
+            q.cc   = wb + k;
+            q.p0   = __builtin_amdgcn_readlane(wp0, k);
+            q.p1   = q.p0 + __builtin_amdgcn_readlane(wcnt, k);
+            q.base = __builtin_amdgcn_readlane(wco, k) - q.p0;
+            q.s0a  = q.p0 & ~1u;
         };
-        int      cc = 0;
-        uint32_t s0 = 0;
-        after(-1, 0, cc, s0);
-        double xn = 0, yn = 0, zn = 0; // coordinates of the chunk at (cc, s0)
-        if (cc < numCand)
-        {
-            const uint32_t p1 = s_p0[cc] + (s_cOff[cc + 1] - s_cOff[cc]);
-            if (s0 + lane < p1) xn = a.x[s0 + lane], yn = a.y[s0 + lane], zn = a.z[s0 + lane];
-        }
-        while (cc < numCand)
-        {
+        auto fetchPairs = [&](const Chunk& q) -> float4 {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (fastWave && q.cc < numCand)
             {
-                const uint32_t p0 = s_p0[cc], p1 = p0 + (s_cOff[cc + 1] - s_cOff[cc]);
-                const uint32_t base = s_cOff[cc] - p0; // candidate index of particle j = base + j
-                const int      m    = (int)min<uint32_t>(kWave, p1 - s0);
-                const uint32_t jl   = s0 + lane;
-                const double   xj = xn, yj = yn, zj = zn;
-                // prefetch the next chunk while this one is tested
-                int      ncc;
-                uint32_t ns0;
-                after(cc, s0, ncc, ns0);
-                xn = yn = zn = 0;
-                if (ncc < numCand)
-                {
-                    const uint32_t np1 = s_p0[ncc] + (s_cOff[ncc + 1] - s_cOff[ncc]);
-                    if (ns0 + lane < np1) xn = a.x[ns0 + lane], yn = a.y[ns0 + lane], zn = a.z[ns0 + lane];
-                }
-                candTested += m;
-                uint64_t lm = 0; // this lane's stored hits in the chunk
-#ifdef SX_NS_PROFILE
-                uint64_t tP = 0;
-#endif
-                if (fastWave)
-                {
-                    // float prefilter on cluster-relative, minimum-image coordinates; the rare candidates within the
-                    // rounding band of some lane's radius are decided by the exact double test
-                    // slots past the leaf end hold a far-away point: never a hit, never ambiguous
-                    const bool in = jl < p1;
-                    s_chunk[wave][lane] =
-                        make_float4(in ? (float)foldPbc(xj - ox, a.box, 0) : 3e18f, in ? (float)foldPbc(yj - oy, a.box, 1) : 0.f,
-                                    in ? (float)foldPbc(zj - oz, a.box, 2) : 0.f, 0.0f);
-                    __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
-                    __builtin_amdgcn_wave_barrier();
-#ifdef SX_NS_PROFILE
-                    const uint64_t tT = __builtin_readcyclecounter();
-#endif
-                    uint64_t  hm  = 0;
-                    const int ng4 = (m + kNsGroup - 1) / kNsGroup;
-                    for (int g4 = 0; g4 < ng4; ++g4)
-                    {
-                        // kNsGroup candidates straight-line (their LDS broadcasts in flight together), branch-free bits
-                        uint32_t b4  = 0;
-                        bool     amb = false;
-#pragma unroll
-                        for (int u = 0; u < kNsGroup; ++u)
-                        {
-                            const float4 q  = s_chunk[wave][g4 * kNsGroup + u];
-                            const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
-                            const float  d2 = dx * dx + dy * dy + dz * dz;
-                            b4 |= (d2 < r2hi ? 1u : 0u) << u;
-                            amb = amb | ((d2 < r2hi) & (d2 >= r2lo));
-                        }
-                        if (__ballot(amb))
-                        {
-                            // rare: within the rounding band of some lane's radius; decide those candidates exactly
-                            for (int u = 0; u < kNsGroup; ++u)
-                            {
-                                const int    k  = g4 * kNsGroup + u;
-                                const float4 q  = s_chunk[wave][k];
-                                const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
-                                const float  d2 = dx * dx + dy * dy + dz * dz;
-                                if (__ballot(d2 < r2hi && d2 >= r2lo) == 0) continue;
-                                const uint32_t j  = s0 + k; // uniform: scalar loads
-                                double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
-                                if (usePbc)
-                                {
-                                    ex = foldPbc(ex, a.box, 0);
-                                    ey = foldPbc(ey, a.box, 1);
-                                    ez = foldPbc(ez, a.box, 2);
-                                }
-                                const bool hit = valid && (ex * ex + ey * ey + ez * ez < radSq);
-                                b4             = hit ? (b4 | (1u << u)) : (b4 & ~(1u << u));
-                            }
-                        }
-                        hm |= (uint64_t)b4 << (g4 * kNsGroup);
-                    }
-#ifdef SX_NS_PROFILE
-                    tP = __builtin_readcyclecounter();
-                    prof[2] += tP - tT;
-#endif
-                    if (i >= s0 && i < s0 + (uint32_t)m) hm &= ~(1ull << (i - s0)); // j != i
-                    const unsigned nh = __popcll(hm);
-                    if (count + nh > a.ngmax)
-                    {
-                        // keep the first (ngmax - count) hits in stream order, like the capped CPU list
-                        unsigned keep = count < a.ngmax ? a.ngmax - count : 0u;
-                        uint64_t kept = 0;
-                        while (keep--)
-                        {
-                            const uint64_t low = hm & (~hm + 1ull);
-                            kept |= low;
-                            hm ^= low;
-                        }
-                        hm = kept;
-                    }
-                    count += nh;
-                    lm = hm;
-                    __builtin_amdgcn_wave_barrier(); // s_chunk is rewritten by the next chunk
-                }
-                else if (anyPbcUse)
-                {
-                    for (int k = 0; k < m; ++k)
-                    {
-                        double dx = readlaneD(xj, k) - xi;
-                        double dy = readlaneD(yj, k) - yi;
-                        double dz = readlaneD(zj, k) - zi;
-                        if (usePbc)
-                        {
-                            dx = foldPbc(dx, a.box, 0);
-                            dy = foldPbc(dy, a.box, 1);
-                            dz = foldPbc(dz, a.box, 2);
-                        }
-                        const bool hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i;
-                        if (hit)
-                        {
-                            if (count < a.ngmax) lm |= 1ull << k;
-                            count++;
-                        }
-                    }
-                }
-                else
-                {
-                    for (int k = 0; k < m; ++k)
-                    {
-                        double     dx  = readlaneD(xj, k) - xi;
-                        double     dy  = readlaneD(yj, k) - yi;
-                        double     dz  = readlaneD(zj, k) - zi;
-                        const bool hit = valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i;
-                        if (hit)
-                        {
-                            if (count < a.ngmax) lm |= 1ull << k;
-                            count++;
-                        }
-                    }
-                }
-                if (local)
-                {
-                    const uint32_t b0 = base + s0; // candidate index of the chunk's first particle
-                    const uint64_t wm = waveOr64(lm);
-                    if (wm && lane < 3)
-                    {
-                        // bits [b0, b0+64) of the bitmap span up to three words
-                        const uint32_t sh = b0 & 31, w0 = b0 >> 5;
-                        uint32_t       part;
-                        if (lane == 0) part = (uint32_t)(wm << sh);
-                        else if (lane == 1) part = sh ? (uint32_t)(wm >> (32 - sh)) : (uint32_t)(wm >> 32);
-                        else part = sh ? (uint32_t)(wm >> (64 - sh)) : 0u;
-                        if (part) atomicOr(&s_bits[w0 + lane], part);
-                    }
-                    // append two hits per iteration (one u16-pair word per iteration), 32-bit halves
-#pragma unroll
-                    for (int half = 0; half < 2; ++half)
-                    {
-                        uint32_t       hb   = half ? (uint32_t)(lm >> 32) : (uint32_t)lm;
-                        const uint32_t hb0  = b0 + 32u * half;
-                        while (hb)
-                        {
-                            const uint32_t e1 = hb0 + __builtin_ctz(hb);
-                            hb &= hb - 1u;
-                            const bool     two = hb != 0u;
-                            const uint32_t e2  = hb0 + (two ? __builtin_ctz(hb) : 0u);
-                            if (two) hb &= hb - 1u;
-                            uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
-                            if (stored & 1u)
-                            {
-                                *dst = pend | (e1 << 16);
-                                pend = e2;
-                            }
-                            else if (two) { *dst = e1 | (e2 << 16); }
-                            else { pend = e1; }
-                            stored += two ? 2u : 1u;
-                        }
-                    }
-                }
-                else
-                {
-                    while (lm)
-                    {
-                        const int k = __builtin_ctzll(lm);
-                        lm &= lm - 1ull;
-                        gl[(size_t)stored * kWave] = s0 + k;
-                        stored++;
-                    }
-                }
-#ifdef SX_NS_PROFILE
-                if (fastWave) prof[3] += __builtin_readcyclecounter() - tP;
-#endif
-                cc = ncc, s0 = ns0;
+                const uint32_t e = min(q.s0a + kWave, q.p1);
+                if ((uint32_t)lane < 2 * ((e - q.s0a + 1) >> 1))
+                    v = reinterpret_cast<const float4*>(a.qrel)[(size_t)(q.s0a >> 1) * 2 + lane];
             }
+            return v;
+        };
+        Chunk cur{-1, 0, 0, 0, 0};
+        advance(cur);
+        Chunk nxt = cur;
+        advance(nxt);
+        float4 pf = fetchPairs(cur), pfn = fetchPairs(nxt);
+        while (cur.cc < numCand)
+        {
+            const int      cc = cur.cc;
+            const uint32_t p0 = cur.p0, p1 = cur.p1, s0a = cur.s0a;
+            const uint32_t base = cur.base; // candidate index of particle j = base + j
+            const uint32_t s0 = max(s0a, p0), e = min(s0a + kWave, p1);
+            const int      m  = (int)(e - s0);
+            const float4   chunk = pf;
+            cur                  = nxt;
+            advance(nxt);
+            pf  = pfn;
+            pfn = fetchPairs(nxt);
+            candTested += m;
+
+            // leaf frame: d = fold(anchor - o) (anchor = the leaf's first particle), w = error-bound extent, < 0 when
+            // the leaf may straddle a periodic image
+            float4 dd = make_float4(0.f, 0.f, 0.f, -1.f);
+            if (fastWave) dd = cc < kDCap ? s_d[cc] : leafFrame(a, s_cand[cc], p0, ox, oy, oz);
+            uint64_t hm;
+            bool     exact = !(fastWave && dd.w >= 0.0f);
+            if (!exact)
+            {
+                // t = |q - r'|^2 - 4h^2 = qw + (r'.r' - 4h^2) - 2 q.r' per candidate pair (packed f32, q from LDS);
+                // hit = sign bit of t, gathered by v_alignbit; |t| < tol (error bound) defers the chunk to the exact
+                // double test
+                const float rx = xr - dd.x, ry = yr - dd.y, rz = zr - dd.z;
+                const float c  = fmaf(rx, rx, fmaf(ry, ry, fmaf(rz, rz, -thr)));
+                const float E  = dd.w + rn2;
+                const float tol = valid ? 0x1p-19f * fmaf(E, E, thr) : 0.0f;
+                const v2f   mrx = {-2.0f * rx, -2.0f * rx}, mry = {-2.0f * ry, -2.0f * ry},
+                          mrz = {-2.0f * rz, -2.0f * rz}, c2 = {c, c};
+                float4* sc = s_chunk[wave];
+                sc[lane]   = chunk;
+                __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
+                __builtin_amdgcn_wave_barrier();
+#ifdef SX_NS_PROFILE
+                const uint64_t tT = __builtin_readcyclecounter();
+#endif
+                const int ng = (int)((e - s0a + 7) >> 3); // groups of 8 candidates (4 pairs)
+                uint32_t  acc = 0, wlo = 0, whi = 0;
+                float     am  = 3.0e38f;
+                for (int g = 0; g < ng; ++g)
+                {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                    {
+                        const float4 A = sc[(g * 4 + u) * 2], B = sc[(g * 4 + u) * 2 + 1];
+                        const v2f    qx = {A.x, A.y}, qy = {A.z, A.w}, qz = {B.x, B.y}, qw = {B.z, B.w};
+                        v2f          t  = qw + c2;
+                        t               = __builtin_elementwise_fma(qz, mrz, t);
+                        t               = __builtin_elementwise_fma(qy, mry, t);
+                        t               = __builtin_elementwise_fma(qx, mrx, t);
+                        acc             = __builtin_amdgcn_alignbit(acc, __float_as_uint(t.x), 31);
+                        acc             = __builtin_amdgcn_alignbit(acc, __float_as_uint(t.y), 31);
+                        am              = fminf(am, fminf(fabsf(t.x), fabsf(t.y)));
+                    }
+                    if (g == 3) wlo = __builtin_bitreverse32(acc), acc = 0;
+                }
+                // candidate k of a half sits at bit (n-1-k) of acc: reverse, then drop the unused low bits
+                if (ng < 4) wlo = __builtin_bitreverse32(acc) >> (32 - 8 * ng);
+                else if (ng > 4) whi = __builtin_bitreverse32(acc) >> (32 - 8 * (ng - 4));
+                __builtin_amdgcn_wave_barrier(); // s_chunk is rewritten by the next chunk
+#ifdef SX_NS_PROFILE
+                prof[2] += __builtin_readcyclecounter() - tT;
+#endif
+                if (__ballot(am < tol)) exact = true;
+                else
+                {
+                    hm = ((uint64_t)wlo | ((uint64_t)whi << 32)) >> (s0 - s0a);
+                    if (m < 64) hm &= (1ull << m) - 1ull;
+                    if (i >= s0 && i < e) hm &= ~(1ull << (i - s0)); // j != i
+                }
+            }
+            if (exact) hm = exactChunk(s0, m);
+#ifdef SX_NS_PROFILE
+            const uint64_t tP = __builtin_readcyclecounter();
+#endif
+            const unsigned nh = __popcll(hm);
+            if (count + nh > a.ngmax)
+            {
+                // keep the first (ngmax - count) hits in stream order, like the capped CPU list
+                unsigned keep = count < a.ngmax ? a.ngmax - count : 0u;
+                uint64_t kept = 0;
+                while (keep--)
+                {
+                    const uint64_t low = hm & (~hm + 1ull);
+                    kept |= low;
+                    hm ^= low;
+                }
+                hm = kept;
+            }
+            count += nh;
+            uint64_t lm = hm;
+            if (local)
+            {
+                const uint32_t b0 = base + s0; // candidate index of the chunk's first particle
+                const uint64_t wm = waveOr64(lm);
+                if (wm && lane < 3)
+                {
+                    // bits [b0, b0+64) of the bitmap span up to three words
+                    const uint32_t sh = b0 & 31, w0 = b0 >> 5;
+                    uint32_t       part;
+                    if (lane == 0) part = (uint32_t)(wm << sh);
+                    else if (lane == 1) part = sh ? (uint32_t)(wm >> (32 - sh)) : (uint32_t)(wm >> 32);
+                    else part = sh ? (uint32_t)(wm >> (64 - sh)) : 0u;
+                    if (part) atomicOr(&s_bits[w0 + lane], part);
+                }
+                // append two hits per iteration (one u16-pair word per iteration), 32-bit halves
+#pragma unroll
+                for (int half = 0; half < 2; ++half)
+                {
+                    uint32_t       hb  = half ? (uint32_t)(lm >> 32) : (uint32_t)lm;
+                    const uint32_t hb0 = b0 + 32u * half;
+                    while (hb)
+                    {
+                        const uint32_t e1 = hb0 + __builtin_ctz(hb);
+                        hb &= hb - 1u;
+                        const bool     two = hb != 0u;
+                        const uint32_t e2  = hb0 + (two ? __builtin_ctz(hb) : 0u);
+                        if (two) hb &= hb - 1u;
+                        uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
+                        if (stored & 1u)
+                        {
+                            *dst = pend | (e1 << 16);
+                            pend = e2;
+                        }
+                        else if (two) { *dst = e1 | (e2 << 16); }
+                        else { pend = e1; }
+                        stored += two ? 2u : 1u;
+                    }
+                }
+            }
+            else
+            {
+                while (lm)
+                {
+                    const int k = __builtin_ctzll(lm);
+                    lm &= lm - 1ull;
+                    gl[(size_t)stored * kWave] = s0 + k;
+                    stored++;
+                }
+            }
+#ifdef SX_NS_PROFILE
+            prof[3] += __builtin_readcyclecounter() - tP;
+#endif
         }
         if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
@@ -614,6 +671,8 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
     unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    if (a.qrel && a.numLeaves > 0)
+        leafFrameKernel<<<(a.numLeaves + 3) / 4, 256, 0, s>>>(a.layout, a.numLeaves, a.x, a.y, a.z, a.qrel);
     findNeighborsKernel<<<clusters, kCluster, 0, s>>>(a);
     return hipGetLastError();
 }

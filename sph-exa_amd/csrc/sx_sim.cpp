@@ -991,6 +991,9 @@ extern "C"
             na.margin         = quantMargin(s->dbox);
             na.stats          = s->stats;
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
+            na.numLeaves      = s->tree.numLeaves;
+            na.qrel           = s->mem.get<float>("ns.qrel", qrelFloats(s->n));
+            if (!na.qrel) return SX_ERR_NOMEM;
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));

@@ -175,6 +175,10 @@ struct NsArgs
     DevBox          box;
     double          margin; // node-box inflation covering key quantisation round-off
     const float*    powTab; // glibc powf(1 + 1023*ng0/nc, 0.1f) by nc (updateH)
+    // float prefilter records (leafFrameKernel, pair layout, qrelFloats(n) floats, written by findNeighbors); nullptr
+    // selects the exact double test for every candidate
+    int             numLeaves;
+    float*          qrel;
     uint32_t*       stats;  // kStatsWords words, see above
 
     void setLists(const NbLists& L)
@@ -207,6 +211,8 @@ void       packC(size_t n, const float* c11, const float* c12, const float* c13,
                  const float* c33, const float* divv, RecC* out, hipStream_t s);
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
+//! floats of the prefilter record buffer for n particles (pairs of 8 floats + one padded chunk)
+inline size_t qrelFloats(size_t n) { return ((n + 1) / 2 + 64) * 8; }
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
 //! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);
