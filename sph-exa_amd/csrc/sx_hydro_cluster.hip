@@ -183,26 +183,35 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
         if (wBeg >= wEnd) return;
         const uint32_t* nl = cu.nl;
         auto            ld = [&](uint32_t w) { return w < wEnd ? nl[(size_t)w * kWave] : 0u; };
-        uint32_t        q0 = ld(wBeg + 1), q1 = ld(wBeg + 2), q2 = ld(wBeg + 3), q3 = ld(wBeg + 4);
+        // two record buffers used alternately (2x unrolled, no register copies); list words prefetched ahead
+        uint32_t        q0 = ld(wBeg + 1), q1 = ld(wBeg + 2), q2 = ld(wBeg + 3);
         const uint32_t  w0 = nl[(size_t)wBeg * kWave];
-        auto            ra = load(w0 & 0xffffu); // slot 0 for a missing odd partner: valid, never computed
-        auto            rb = load(w0 >> 16);
-        for (uint32_t w = wBeg; w < wEnd; ++w)
+        auto            a0 = load(w0 & 0xffffu); // slot 0 for a missing odd partner: valid, never computed
+        auto            b0 = load(w0 >> 16);
+        decltype(a0)    a1, b1;
+        uint32_t        w = wBeg;
+        while (true)
         {
-            const auto ca = ra;
-            const auto cb = rb;
             if (w + 1 < wEnd)
             {
-                const uint32_t nx = q0;
-                q0                = q1;
-                q1                = q2;
-                q2                = q3;
-                q3                = ld(w + 5);
-                ra                = load(nx & 0xffffu);
-                rb                = load(nx >> 16);
+                a1 = load(q0 & 0xffffu);
+                b1 = load(q0 >> 16);
+                q0 = ld(w + 4);
             }
-            compute(ca);
-            if (2 * w + 1 < cu.cnt) compute(cb);
+            compute(a0);
+            if (2 * w + 1 < cu.cnt) compute(b0);
+            if (++w >= wEnd) break;
+            if (w + 1 < wEnd)
+            {
+                a0 = load(q1 & 0xffffu);
+                b0 = load(q1 >> 16);
+                q1 = ld(w + 4);
+            }
+            compute(a1);
+            if (2 * w + 1 < cu.cnt) compute(b1);
+            if (++w >= wEnd) break;
+            const uint32_t t = q0;
+            q0 = q2, q2 = q1, q1 = t;
         }
     }
     else
@@ -509,12 +518,29 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
 }
 
 // ---- momentum + energy: momentumAndEnergyJLoop<avClean=false> (momentum_energy_kern.hpp:65-222) -------------------
+//! Atwood-ramped momentum weights (momentum_energy_kern.hpp:178-195): xm_i^(2-s) xm_j^s and xm_j^(2-s) xm_i^s with
+//! s = 0 below Atmin, 1 above Atmax (both exact products) and the ramp in between (exp2/log2 form)
+__device__ __forceinline__ void atwoodWeights(float Atwood, float Atmin, float Atmax, float ramp, float xmi, float lxi,
+                                              float xmj, float& a_mom, float& b_mom)
+{
+    if (Atwood < Atmin) { a_mom = xmi * xmi, b_mom = xmj * xmj; }
+    else if (Atwood > Atmax) { a_mom = xmi * xmj, b_mom = a_mom; }
+    else
+    {
+        const float sigma = ramp * (Atwood - Atmin);
+        const float lxj   = __log2f(xmj);
+        const float dl    = lxj - lxi;
+        a_mom             = exp2f(fmaf(sigma, dl, 2.0f * lxi));
+        b_mom             = exp2f(fmaf(-sigma, dl, 2.0f * lxj));
+    }
+}
+
 template<int CH, int SPLIT>
 __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, 1/h
     __shared__ float4 sV[CH]; // vx, vy, vz, c
-    __shared__ float4 sT[CH]; // m, log2(xm), rho, prho
+    __shared__ float4 sT[CH]; // m, xm, rho, m*prho
     __shared__ float4 sA[CH]; // alpha, c11, c12, c13
     __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
     __shared__ float  s_red[kClusterWaves * SPLIT];
@@ -529,12 +555,13 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     const float rhoi    = ti.kx * mi / xmassi;
     const float rhoiInv = 1.0f / rhoi;
     const float lxi     = __log2f(xmassi);
+    const float xmi2    = xmassi * xmassi;
     const float hiInv   = 1.0f / hi;
     const float hiInv3  = hiInv * hiInv * hiInv;
     const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp;
-    float       maxvsignali = 0.0f;
-    float       mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
-    bool        res = false;
+    float maxvsignali = 0.0f;
+    float mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
+    bool  res = false;
     neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
@@ -546,7 +573,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             sP[slot]        = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
                                    relc(r.z, cu.oz, a.box, 2), 1.0f / r.h);
             sV[slot]        = make_float4(v.vx, v.vy, v.vz, v.c);
-            sT[slot]        = make_float4(r.m, __log2f(t.xm), rho, t.prho);
+            sT[slot]        = make_float4(r.m, t.xm, rho, r.m * t.prho);
             sA[slot]        = make_float4(t.alpha, c6.c11, c6.c12, c6.c13);
             sB[slot]        = make_float4(c6.c22, c6.c23, c6.c33, r.m / rho);
         },
@@ -569,7 +596,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float tA1j   = -(A.y * rx + A.z * ry + A.w * rz) * Wj;
             const float tA2j   = -(A.z * rx + B.x * ry + B.y * rz) * Wj;
             const float tA3j   = -(A.w * rx + B.y * ry + B.z * rz) * Wj;
-            const float mj = T.x, lxj = T.y, rhoj = T.z, cj = V.w;
+            const float mj = T.x, rhoj = T.z, cj = V.w;
             const float rv  = rx * vx_ij + ry * vy_ij + rz * vz_ij;
             const float wij = rv * rinv;
             // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
@@ -577,13 +604,14 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
             const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
             maxvsignali            = fmaxf(maxvsignali, vijsignal);
-            // Atwood switch: sigma = 0 gives (xm_i^2, xm_j^2), sigma = 1 gives (xm_i xm_j, xm_i xm_j), the ramp
-            // in between xm_i^(2-s) xm_j^s: one branch-free exp2/log2 form for all three cases
             const float Atwood = fabsf(rhoi - rhoj) * __frcp_rn(rhoi + rhoj);
-            const float sigma  = Atwood < Atmin ? 0.0f : (Atwood > Atmax ? 1.0f : ramp * (Atwood - Atmin));
-            const float dl     = lxj - lxi;
-            const float a_mom  = exp2f(fmaf(sigma, dl, 2.0f * lxi));
-            const float b_mom  = exp2f(fmaf(-sigma, dl, 2.0f * lxj));
+            float       a_mom, b_mom;
+            if (__ballot(Atwood >= Atmin) == 0)
+            {
+                a_mom = xmi2; // the common case: below Atmin in every lane
+                b_mom = T.y * T.y;
+            }
+            else atwoodWeights(Atwood, Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
             const float a_visc   = mj * rhoiInv * halfVisc;
             const float b_visc   = B.w * halfVisc;
             const float a_visc_x = a_visc * tA1i + b_visc * tA1j;
@@ -592,7 +620,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             a_visc_energy += a_visc_x * vx_ij + a_visc_y * vy_ij + a_visc_z * vz_ij;
             energy += mj * a_mom * (vx_ij * tA1i + vy_ij * tA2i + vz_ij * tA3i);
             const float momentum_i = mj * prhoi * a_mom;
-            const float momentum_j = mj * T.w * b_mom;
+            const float momentum_j = T.w * b_mom;
             mx += momentum_i * tA1i + momentum_j * tA1j + a_visc_x;
             my += momentum_i * tA2i + momentum_j * tA2j + a_visc_y;
             mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
