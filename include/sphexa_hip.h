@@ -241,6 +241,16 @@ int  sx_comm_create_rccl(sx_comm** comm, int rank, int size, const void* id128);
 int  sx_comm_create_host(sx_comm** comm, int rank, int size, sx_alltoallv_cb a2a, sx_allreduce_cb ar, void* user);
 void sx_comm_destroy(sx_comm* comm);
 
+/* ---- host-side decisions of the SFC domain decomposition (sph-exa_amd/csrc/sx_domain.cpp) -------------- */
+/*! equal-count SFC splitters from the all-reduced histogram of 2^histBits key bins (bin = key >> (63-histBits)):
+ *  rank q owns keys [split[q], split[q+1]); split has nranks+1 entries.  Replaces cstone::makeSfcAssignment,
+ *  domain/include/cstone/domain/domaindecomp.hpp:120. */
+int sx_domain_splitters(const uint32_t* hist, uint32_t histBits, int nranks, uint64_t* split);
+/*! halo receive layout [lower ranks | numLocal locals | higher ranks] (domain.hpp:196-244): recvOff[q] for each
+ *  peer (0 for rank itself), out = {first local, last local, total}. */
+int sx_domain_halo_layout(const uint64_t* recvCounts, int nranks, int rank, uint64_t numLocal, uint64_t* recvOff,
+                          uint64_t out[3]);
+
 /* ---- device-resident simulation: one HydroVeProp step per call ----------------------------------------- */
 typedef struct sx_sim sx_sim;
 /*! Sedov lattice (sedov_init.hpp:48-130) of side^3 particles; with nranks > 1 only this rank's SFC share. */

@@ -593,23 +593,8 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     std::vector<uint32_t> hb(nb);
     SIM_HIP(hipMemcpyAsync(hb.data(), bins, nb * 4, hipMemcpyDeviceToHost, st));
     SIM_HIP(hipStreamSynchronize(st));
-    uint64_t total = 0;
-    for (auto v : hb)
-        total += v;
     std::vector<uint64_t> split(P + 1, 0);
-    split[P] = uint64_t(1) << 63;
-    {
-        uint64_t acc = 0;
-        int      q   = 1;
-        for (size_t b = 0; b < nb && q < P; ++b)
-        {
-            while (q < P && acc >= (total * q) / P)
-                split[q++] = uint64_t(b) << (63 - kHistBits);
-            acc += hb[b];
-        }
-        while (q < P)
-            split[q++] = uint64_t(1) << 63;
-    }
+    if (int e = sx_domain_splitters(hb.data(), kHistBits, P, split.data())) return e;
 
     // --- 3. particle exchange
     uint64_t* dsplit = s->work.get<uint64_t>("dom.split", P + 1);
@@ -724,12 +709,8 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     if (nLow + nl + nHigh > s->cap) return SX_ERR_NOMEM;
     s->haloRecvOff.assign(P, 0);
     {
-        uint64_t lo = 0, hi = nLow + nl;
-        for (int q = 0; q < P; ++q)
-        {
-            if (q < r) { s->haloRecvOff[q] = lo, lo += s->haloRecv[q]; }
-            else if (q > r) { s->haloRecvOff[q] = hi, hi += s->haloRecv[q]; }
-        }
+        uint64_t lay[3];
+        if (int e = sx_domain_halo_layout(s->haloRecv.data(), P, r, nl, s->haloRecvOff.data(), lay)) return e;
     }
     s->numHalos = nLow + nHigh;
 

@@ -158,6 +158,8 @@ def lib():
         "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
         "sx_comm_destroy": (None, [vp]),
+        "sx_domain_splitters": (C.c_int, [vp, u32, C.c_int, vp]),
+        "sx_domain_halo_layout": (C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -165,6 +167,29 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def domain_splitters(hist, hist_bits, nranks):
+    """equal-count SFC splitters (nranks+1 keys) from an all-reduced key histogram (sx_domain_splitters)"""
+    h = np.ascontiguousarray(hist, dtype=np.uint32)
+    if h.size != 1 << hist_bits:
+        raise ValueError("histogram size must be 2^hist_bits")
+    out = np.zeros(nranks + 1, np.uint64)
+    rc = lib().sx_domain_splitters(h.ctypes.data, hist_bits, nranks, out.ctypes.data)
+    if rc != SX_OK:
+        raise SxError(f"sx_domain_splitters failed: {rc}")
+    return out
+
+
+def halo_layout(recv_counts, rank, num_local):
+    """halo receive offsets [lower ranks | locals | higher ranks] and (first, last, total) (sx_domain_halo_layout)"""
+    rc_ = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+    off = np.zeros(rc_.size, np.uint64)
+    out = np.zeros(3, np.uint64)
+    rc = lib().sx_domain_halo_layout(rc_.ctypes.data, rc_.size, rank, num_local, off.ctypes.data, out.ctypes.data)
+    if rc != SX_OK:
+        raise SxError(f"sx_domain_halo_layout failed: {rc}")
+    return off, tuple(int(v) for v in out)
 
 
 def default_params(K=None, ngmax=150, ng0=100):

@@ -1,0 +1,57 @@
+"""Worker of the CPU multi-rank tests (tests/test_dist_cpu.py): gloo process group on 127.0.0.1, one rank of the
+decomposed oracle (oracle/dist_oracle.py) over an index slab of a lattice IC, K steps, locals written to
+DIR/rank<r>.npz.
+
+  python tests/dist_cpu_worker.py --rank R --size P --port X --out DIR [--ic sedov|noh] [--side S] [--steps K]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sph-exa_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--size", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--ic", default="sedov")
+    ap.add_argument("--side", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=2)
+    args = ap.parse_args()
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{args.port}", rank=args.rank,
+                            world_size=args.size)
+    import dist_oracle as do
+    import pyoracle as po
+
+    st, box = po.sedov_state(args.side) if args.ic == "sedov" else po.noh_state(args.side)
+    f, l = st.n * args.rank // args.size, st.n * (args.rank + 1) // args.size
+    local = po.HostState(l - f)
+    for k in po.CONSERVED:
+        local.arrays[k][:] = st.arrays[k][f:l]
+    local.minDt, local.minDt_m1 = st.minDt, st.minDt_m1
+    d = do.DistOracle(po.load_oracle(), box, local)
+    out = {}
+    for s in range(args.steps):
+        loc = d.step()
+        for k in ("id", "nc", "h", "x", "y", "z", "vx", "vy", "vz", "temp", "du", "ax", "ay", "az", "alpha",
+                  "xm", "kx", "prho", "c", "divv"):
+            out[f"s{s}_{k}"] = loc.arrays[k].copy()
+        out[f"s{s}_scalars"] = np.array([loc.minDt, loc.minDt_m1, loc.ttot])
+        out[f"s{s}_layout"] = np.array([d.first, d.last, d.total, d.halo_retries])
+        out[f"s{s}_split"] = d.split.astype(np.uint64)
+    np.savez(os.path.join(args.out, f"rank{args.rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

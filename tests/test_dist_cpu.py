@@ -1,0 +1,116 @@
+"""The multi-rank path on the CPU (no GPU): world_size 2 and 3 over gloo.
+
+* the host-side decisions of the decomposition that the GPU path calls (sx_domain_splitters,
+  sx_domain_halo_layout in libsphexa_hip.so) against a numpy restatement;
+* the decomposed VE step (oracle/dist_oracle.py: SFC assignment from the all-reduced key histogram through
+  sx_domain_splitters, particle exchange, halo discovery, the five halo exchanges, global dt) against the
+  single-domain oracle: after step 1 nc and h exact, floats within the full-step tolerance of
+  tests/test_gpu_parity.py (neighbor sums run in another order), identical dt on every rank.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+import sphexa_amd as sx
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ["x", "y", "z", "vx", "vy", "vz", "temp", "du", "ax", "ay", "az", "alpha", "xm", "kx", "prho", "c", "divv"]
+
+
+def test_splitters_equal_counts():
+    rng = np.random.default_rng(3)
+    bits = 12
+    for P in (1, 2, 3, 8):
+        hist = rng.integers(0, 50, 1 << bits).astype(np.uint32)
+        split = sx.domain_splitters(hist, bits, P)
+        assert split[0] == 0 and split[P] == 1 << 63 and np.all(np.diff(split.astype(np.float64)) >= 0)
+        # restatement: rank q starts at the first bin b with cumsum(hist[:b]) >= q*total/P
+        cum = np.concatenate([[0], np.cumsum(hist.astype(np.int64))])
+        total = int(cum[-1])
+        for q in range(1, P):
+            b = int(np.argmax(cum >= (total * q) // P))
+            assert split[q] == np.uint64(b) << np.uint64(63 - bits)
+        owned = [int(cum[int(split[q + 1] >> np.uint64(63 - bits)) if q + 1 < P else -1] -
+                     cum[int(split[q] >> np.uint64(63 - bits))]) for q in range(P)]
+        assert sum(owned) == total and max(owned) - min(owned) <= 2 * int(hist.max())
+
+
+def test_halo_layout():
+    off, (first, last, total) = sx.halo_layout([3, 0, 5, 2], 1, 10)
+    assert (first, last, total) == (3, 13, 20)
+    assert list(off) == [0, 0, 13, 18]
+    off, lay = sx.halo_layout([0], 0, 7)
+    assert lay == (0, 7, 7)
+    with pytest.raises(sx.SxError):
+        sx.halo_layout([1, 2], 2, 5)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_ranks(tmp_path, nproc, side, steps, ic="sedov"):
+    port = _free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="2", MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_cpu_worker.py"), "--rank", str(r),
+                               "--size", str(nproc), "--port", str(port), "--out", str(tmp_path), "--ic", ic,
+                               "--side", str(side), "--steps", str(steps)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(nproc)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+    return [dict(np.load(os.path.join(tmp_path, f"rank{q}.npz"))) for q in range(nproc)]
+
+
+def merged(ranks, s):
+    out = {k: np.concatenate([d[f"s{s}_{k}"] for d in ranks]) for k in ["id", "nc", "h"] + FIELDS}
+    o = np.argsort(out["id"])
+    return {k: v[o] for k, v in out.items()}
+
+
+@pytest.mark.parametrize("nproc,ic,side", [(2, "sedov", 16), (3, "sedov", 14), (2, "noh", 18)])
+def test_decomposed_steps_match_single_domain(tmp_path, nproc, ic, side):
+    steps = 2
+    ranks = run_ranks(tmp_path, nproc, side, steps, ic)
+    st, obox = po.sedov_state(side) if ic == "sedov" else po.noh_state(side)
+    ora = po.load_oracle()
+    ref = st.copy()
+    for s in range(steps):
+        ora.step(ref, obox)
+        got = merged(ranks, s)
+        assert got["id"].size == st.n and np.array_equal(got["id"], np.arange(st.n))
+        o = np.argsort(ref.id)
+        if s == 0:
+            assert np.array_equal(got["nc"], ref.nc[o])
+            assert np.array_equal(got["h"], ref.h[o])
+        for k in FIELDS:
+            a = got[k].astype(np.float64)
+            b = ref.arrays[k][o].astype(np.float64)
+            tol = 1e-4 * np.abs(b) + 1e-5 * np.max(np.abs(b))
+            assert np.all(np.abs(a - b) <= tol), (s, k, np.max(np.abs(a - b) / (np.abs(b) + 1e-300)))
+        dts = {tuple(d[f"s{s}_scalars"]) for d in ranks}
+        assert len(dts) == 1
+        assert list(dts)[0][0] == pytest.approx(ref.minDt, rel=1e-6)
+        # equal-count SFC shares, every rank holding halos
+        sizes = [int(d[f"s{s}_layout"][1] - d[f"s{s}_layout"][0]) for d in ranks]
+        assert max(sizes) - min(sizes) <= 0.1 * st.n / nproc + 64
+        for d in ranks:
+            first, last, total, _ = d[f"s{s}_layout"]
+            assert last > first and total > last - first
