@@ -163,16 +163,24 @@ __device__ __forceinline__ T waveSum(T v)
     return v;
 }
 
+//! OR over the wave (all lanes active), wave-uniform result: DPP quad/row steps + row broadcasts, no LDS traffic
+//! (quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror, row_mirror, row_bcast15 into rows 1,3, row_bcast31 into
+//! rows 2,3: lane 63 ends up with the OR of all 64 lanes)
+__device__ __forceinline__ uint32_t waveOrU32(uint32_t v)
+{
+    int x = (int)v;
+    x |= __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+    x |= __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+
 __device__ __forceinline__ uint64_t waveOr64(uint64_t v)
 {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-    {
-        lo |= (uint32_t)__shfl_xor((int)lo, o, kWave);
-        hi |= (uint32_t)__shfl_xor((int)hi, o, kWave);
-    }
-    return ((uint64_t)hi << 32) | lo;
+    return ((uint64_t)waveOrU32((uint32_t)(v >> 32)) << 32) | waveOrU32((uint32_t)v);
 }
 
 __device__ __forceinline__ double readlaneD(double v, int k)

@@ -110,7 +110,7 @@ findNeighborsKernel(NsArgs a)
     __shared__ float    s_hmax[kClusterWaves];
     __shared__ int      s_again[kClusterWaves];
     __shared__ uint32_t s_wsum[kClusterWaves];
-    __shared__ float4   s_chunk[kClusterWaves][kWave];
+    __shared__ float4   s_chunk[kClusterWaves][2][kWave]; // per wave: double-buffered leaf-frame pair records
     __shared__ int      s_numCand;
     // leaf frames of the first kDCap candidate leaves; s_pre is only used after the last stream
     float4* const s_d = reinterpret_cast<float4*>(s_pre);
@@ -164,7 +164,7 @@ findNeighborsKernel(NsArgs a)
 
     int numCand = 0;
 #ifdef SX_NS_PROFILE
-    uint64_t prof[5] = {0, 0, 0, 0, 0}; // cycles: candidates+scan, stream, tests, -, union+rewrite
+    uint64_t prof[6] = {0, 0, 0, 0, 0, 0}; // cycles: candidates+scan, stream, tests, post-test, union; chunks
 #endif
     while (true)
     {
@@ -357,11 +357,18 @@ findNeighborsKernel(NsArgs a)
             }
             return v;
         };
+        // software pipeline: chunk k is tested from LDS buffer k%2 while chunk k+1 (loaded into registers during
+        // chunk k-1) is staged into the other buffer, and the load of chunk k+2 is issued before chunk k's list
+        // stores (vmcnt also counts stores: a load issued after them would make its wait cover them too)
         Chunk cur{-1, 0, 0, 0, 0};
         advance(cur);
         Chunk nxt = cur;
         advance(nxt);
-        float4 pf = fetchPairs(cur), pfn = fetchPairs(nxt);
+        int buf = 0;
+        s_chunk[wave][0][lane] = fetchPairs(cur);
+        float4 pfn             = fetchPairs(nxt);
+        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
         while (cur.cc < numCand)
         {
             const int      cc = cur.cc;
@@ -369,11 +376,6 @@ findNeighborsKernel(NsArgs a)
             const uint32_t base = cur.base; // candidate index of particle j = base + j
             const uint32_t s0 = max(s0a, p0), e = min(s0a + kWave, p1);
             const int      m  = (int)(e - s0);
-            const float4   chunk = pf;
-            cur                  = nxt;
-            advance(nxt);
-            pf  = pfn;
-            pfn = fetchPairs(nxt);
             candTested += m;
 
             // leaf frame: d = fold(anchor - o) (anchor = the leaf's first particle), w = error-bound extent, < 0 when
@@ -393,10 +395,7 @@ findNeighborsKernel(NsArgs a)
                 const float tol = valid ? 0x1p-19f * fmaf(E, E, thr) : 0.0f;
                 const v2f   mrx = {-2.0f * rx, -2.0f * rx}, mry = {-2.0f * ry, -2.0f * ry},
                           mrz = {-2.0f * rz, -2.0f * rz}, c2 = {c, c};
-                float4* sc = s_chunk[wave];
-                sc[lane]   = chunk;
-                __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the wave's LDS stores have landed
-                __builtin_amdgcn_wave_barrier();
+                const float4* sc = s_chunk[wave][buf];
 #ifdef SX_NS_PROFILE
                 const uint64_t tT = __builtin_readcyclecounter();
 #endif
@@ -423,7 +422,6 @@ findNeighborsKernel(NsArgs a)
                 // candidate k of a half sits at bit (n-1-k) of acc: reverse, then drop the unused low bits
                 if (ng < 4) wlo = __builtin_bitreverse32(acc) >> (32 - 8 * ng);
                 else if (ng > 4) whi = __builtin_bitreverse32(acc) >> (32 - 8 * (ng - 4));
-                __builtin_amdgcn_wave_barrier(); // s_chunk is rewritten by the next chunk
 #ifdef SX_NS_PROFILE
                 prof[2] += __builtin_readcyclecounter() - tT;
 #endif
@@ -435,9 +433,16 @@ findNeighborsKernel(NsArgs a)
                     if (i >= s0 && i < e) hm &= ~(1ull << (i - s0)); // j != i
                 }
             }
-            if (exact) hm = exactChunk(s0, m);
+            if (exact) hm = exactChunk(s0, m); // (its loads complete before the prefetch below is issued)
+            // stage chunk k+1, issue the load of chunk k+2
+            __builtin_amdgcn_wave_barrier();
+            s_chunk[wave][buf ^ 1][lane] = pfn;
+            cur                          = nxt;
+            advance(nxt);
+            pfn = fetchPairs(nxt);
 #ifdef SX_NS_PROFILE
             const uint64_t tP = __builtin_readcyclecounter();
+            prof[5] += (exact ? (1ull << 32) : 0ull) + 1ull;
 #endif
             const unsigned nh = __popcll(hm);
             if (count + nh > a.ngmax)
@@ -507,6 +512,9 @@ findNeighborsKernel(NsArgs a)
 #ifdef SX_NS_PROFILE
             prof[3] += __builtin_readcyclecounter() - tP;
 #endif
+            buf ^= 1;
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
+            __builtin_amdgcn_wave_barrier();
         }
         if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
@@ -609,7 +617,7 @@ findNeighborsKernel(NsArgs a)
 #ifdef SX_NS_PROFILE
     prof[4] = __builtin_readcyclecounter() - tU;
     if (lane == 0)
-        for (int q = 0; q < 5; ++q)
+        for (int q = 0; q < 6; ++q)
             atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 12 + 2 * q), (unsigned long long)prof[q]);
 #endif
     if (valid)

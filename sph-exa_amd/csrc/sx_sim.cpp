@@ -1093,8 +1093,11 @@ extern "C"
         {
             const uint64_t* pr = reinterpret_cast<const uint64_t*>(s->statsHost + 12);
             const double nwv = (double)((s->last - s->first) / 64);
-            fprintf(stderr, "nsprof cycles/wave: candidates %.0f stream %.0f tests %.0f post-test %.0f union %.0f\n",
-                    pr[0] / nwv, pr[1] / nwv, pr[2] / nwv, pr[3] / nwv, pr[4] / nwv);
+            fprintf(stderr,
+                    "nsprof cycles/wave: candidates %.0f stream %.0f tests %.0f post-test %.0f union %.0f; chunks/wave "
+                    "%.1f exact %.2f%%\n",
+                    pr[0] / nwv, pr[1] / nwv, pr[2] / nwv, pr[3] / nwv, pr[4] / nwv, (pr[5] & 0xffffffffu) / nwv,
+                    100.0 * (pr[5] >> 32) / std::max(1.0, (double)(pr[5] & 0xffffffffu)));
         }
 #endif
         if (s->statsHost[0] & 1u) return SX_ERR_TRAVERSAL;

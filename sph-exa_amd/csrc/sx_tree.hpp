@@ -146,8 +146,8 @@ struct NbLists
     }
 };
 
-constexpr int kStatsWords = 24; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
-                                //!< neighbors, [6] candidates tested, [8] union entries, [12..21] profile build
+constexpr int kStatsWords = 26; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
+                                //!< neighbors, [6] candidates tested, [8] union entries, [12..23] profile build
 
 //! neighbor-search arguments (sx_neighbors.hip)
 struct NsArgs
