@@ -19,6 +19,7 @@
  *   sx_iad_divv_curlv      sph::cuda::computeIadDivvCurlv       sph_gpu.hpp:45, hydro_ve/iad_divv_curlv_gpu.cu:91
  *   sx_av_switches         sph::cuda::computeAVswitches         sph_gpu.hpp:48, hydro_ve/av_switches_gpu.cu:103
  *   sx_momentum_energy     sph::cuda::computeMomentumEnergy<avClean=false> sph_gpu.hpp:51-53, momentum_energy_gpu.cu:121
+ *   sx_momentum_energy_avclean  sph::cuda::computeMomentumEnergy<avClean=true>  (same seam, second instantiation)
  *   sx_positions           sph::computePositionsGpu             sph_gpu.hpp:64-72, positions_gpu.cu:167-179
  *   sx_update_h            sph::updateSmoothingLengthGpu        sph_gpu.hpp:78, update_h_gpu.cu:49-60
  *   sx_max_divv            cstone::MinMaxGpu (rhoTimestep)      sph/ts_global.hpp:72-94
@@ -77,6 +78,7 @@ typedef struct sx_params
     float    alphamin, alphamax, decay_constant; /* 0.05, 1.0, 0.2 */
     float    Atmin, Atmax, ramp;                 /* 0.1, 0.2, 10 */
     double   maxDtIncrease;                      /* 1.1 */
+    int32_t  avClean; /* sx_sim only: HydroVeProp<avClean=true> (ve_hydro.hpp:50, factory.hpp:56), 0 = off */
 } sx_params;
 
 /*! Device pointers in sphexa::ParticlesData field order (particles_data.hpp:247-251); NULL where unused.
@@ -214,12 +216,18 @@ int sx_xmass_only(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_
 int sx_ve_def_gradh(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
 int sx_eos(sx_ctx* ctx, uint32_t first, uint32_t last, float mui, double gamma, const double* temp, const float* m,
            const float* kx, const float* xm, const float* gradh, float* prho, float* c, float* rho, float* p);
+/*! also writes the velocity gradient dV11..dV33 when f->dV11 != NULL (doGradV: dV11.size() == x.size(),
+ *  iad_divv_curlv_gpu.cu:96-97, divv_curlv_kern.hpp:113-121) */
 int sx_iad_divv_curlv(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
 int sx_av_switches(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
                    double minDt);
 /*! writes ax,ay,az,du; *minDtCourant receives the min Courant time-step (float, like minDt_ve_device) */
 int sx_momentum_energy(sx_ctx* ctx, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
                        const sx_box* box, float* minDtCourant);
+/*! computeMomentumEnergy<avClean=true> (sph_gpu.hpp:51-53, momentum_energy_gpu.cu:147-152): adds the
+ *  avRvCorrection of the AV-cleaning propagator (momentum_energy_kern.hpp:43-63); needs f->dV11..dV33 */
+int sx_momentum_energy_avclean(sx_ctx* ctx, const sx_groups* g, float* groupDt, const sx_fields* f,
+                               const sx_params* p, const sx_box* box, float* minDtCourant);
 /*! 2nd-order Press position update + AB2 energy update on temp (positions.hpp:54-139, F2-correct); dt, dt_m1 double
  *  as in the CPU path (the reference GPU path passes them as float). */
 int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,

@@ -31,7 +31,7 @@ class OxParams(C.Structure):
     _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
-                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double)]
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32)]
 
 
 STATE_FIELDS = [
@@ -45,6 +45,8 @@ STATE_FIELDS = [
     ("xm", np.float32), ("kx", np.float32), ("gradh", np.float32), ("divv", np.float32), ("curlv", np.float32),
     ("c11", np.float32), ("c12", np.float32), ("c13", np.float32), ("c22", np.float32), ("c23", np.float32),
     ("c33", np.float32), ("nc", np.uint32), ("keys", np.uint64),
+    ("dV11", np.float32), ("dV12", np.float32), ("dV13", np.float32), ("dV22", np.float32), ("dV23", np.float32),
+    ("dV33", np.float32),
 ]
 CONSERVED = ["x", "y", "z", "x_m1", "y_m1", "z_m1", "vx", "vy", "vz", "temp", "h", "m", "alpha", "du_m1", "id"]
 
@@ -57,11 +59,12 @@ class OxState(C.Structure):
         ("minDtRho", C.c_double)]
 
 
-def default_params(K):
-    """ParticlesData defaults (particles_data.hpp:86-138)."""
+def default_params(K, av_clean=False):
+    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true>."""
     return OxParams(K=K, ng0=100, ngmax=150, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0,
                     alphamin=0.05, alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
-                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1)
+                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
+                    avClean=1 if av_clean else 0)
 
 
 def make_box(lo=-0.5, hi=0.5, periodic=True):
@@ -237,8 +240,8 @@ class Lib:
                                C.byref(K))
         self.wh, self.whd, self.K = wh, whd, K.value
 
-    def params(self):
-        return default_params(self.K)
+    def params(self, av_clean=False):
+        return default_params(self.K, av_clean)
 
     def sfc_keys(self, st, box):
         self.lib.sfc_keys(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.n, C.byref(box),

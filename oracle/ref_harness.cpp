@@ -221,6 +221,16 @@ void bindState(MockData<T>& d, ox_state* s, const ox_params* p)
     d.c23    = {s->c23, n};
     d.c33    = {s->c33, n};
     d.nc     = {s->nc, n};
+    if (p && p->avClean)
+    {
+        // GradVFields acquired (ve_hydro.hpp:80-85): dV11.size() == x.size() turns on doGradV
+        d.dV11 = {s->dV11, n};
+        d.dV12 = {s->dV12, n};
+        d.dV13 = {s->dV13, n};
+        d.dV22 = {s->dV22, n};
+        d.dV23 = {s->dV23, n};
+        d.dV33 = {s->dV33, n};
+    }
     d.minDt    = s->minDt;
     d.minDt_m1 = s->minDt_m1;
     if (p)
@@ -403,7 +413,8 @@ extern "C"
                                unsigned first, unsigned last)
     {
         auto d = kernelData(s, p, neighbors);
-        sph::computeMomentumEnergyImpl<false>(first, last, d, makeBox(b));
+        if (p->avClean) sph::computeMomentumEnergyImpl<true>(first, last, d, makeBox(b));
+        else sph::computeMomentumEnergyImpl<false>(first, last, d, makeBox(b));
         s->minDtCourant = d.minDtCourant;
         return d.minDtCourant;
     }
@@ -475,7 +486,8 @@ extern "C"
             d.minDtRho = d.Krho / std::abs(maxDivv);
         }
         sph::computeAVswitchesImpl(0, n, d, box);
-        sph::computeMomentumEnergyImpl<false>(0, n, d, box);
+        if (p->avClean) sph::computeMomentumEnergyImpl<true>(0, n, d, box);
+        else sph::computeMomentumEnergyImpl<false>(0, n, d, box);
 
         // --- integrate: computeTimestep (ts_global.hpp:97-112 without MPI_Allreduce)
         double minDtLoc = std::min({double(INFINITY), d.minDtCourant, d.minDtRho, 1.1 * d.minDt});

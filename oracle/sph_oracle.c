@@ -835,8 +835,10 @@ static void IADJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, 
     s->c33[i]    = (tau11 * tau22 - tau12 * tau12) * factor;
 }
 
-/* divV_curlVJLoop (divv_curlv_kern.hpp:43-123), doGradV = false, curlv stored */
-static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s)
+/* divV_curlVJLoop (divv_curlv_kern.hpp:43-123), curlv stored; doGradV (dV11.size() == x.size(),
+ * iad_divv_curlv.hpp) writes the velocity-gradient fields of the avClean propagator (:113-121) */
+static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
+                           int doGradV)
 {
     double xi = s->x[i], yi = s->y[i], zi = s->z[i];
     float  vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
@@ -880,6 +882,15 @@ static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t
         float cv0 = dVz[1] - dVy[2], cv1 = dVx[2] - dVz[0], cv2 = dVy[0] - dVx[1];
         s->curlv[i] = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
     }
+    if (doGradV)
+    {
+        s->dV11[i] = norm_kxi * dVx[0];
+        s->dV12[i] = norm_kxi * (dVx[1] + dVy[0]);
+        s->dV13[i] = norm_kxi * (dVx[2] + dVz[0]);
+        s->dV22[i] = norm_kxi * dVy[1];
+        s->dV23[i] = norm_kxi * (dVy[2] + dVz[1]);
+        s->dV33[i] = norm_kxi * dVz[2];
+    }
 }
 
 void ox_iad_divv_curlv(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
@@ -892,7 +903,7 @@ void ox_iad_divv_curlv(ox_state* s, const ox_params* p, const ox_box* b, const u
         size_t   ni  = i - first;
         unsigned cnt = nc_capped(s->nc, i, p->ngmax);
         IADJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s);
-        divVcurlVJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s);
+        divVcurlVJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s, p->avClean);
     }
 }
 
@@ -974,8 +985,34 @@ void ox_av_switches(ox_state* s, const ox_params* p, const ox_box* b, const uint
  * The Atwood ramp calls unqualified `pow(float, float)` inside namespace sph (momentum_energy_kern.hpp:192-193);
  * with libstdc++ that resolves to ::pow(double, double) from <math.h>, so each product is formed in double and
  * rounded once to float -- verified bit-for-bit against oracle/_ref on the Noh IC, where powf() differs. */
+/* avRvCorrection<float, float> (momentum_energy_kern.hpp:43-63): symv is the upper-triangle product
+ * (kernels.hpp:88-95) and dot the right fold a0*b0 + (a1*b1 + a2*b2) (util/array.hpp:253-256) */
+static inline float dot3(float a0, float a1, float a2, float b0, float b1, float b2)
+{
+    return a0 * b0 + (a1 * b1 + a2 * b2);
+}
+static float avRvCorrection(float rx, float ry, float rz, float eta_ab, float eta_crit, const float* gi,
+                            const float* gj)
+{
+    float dmy1 = dot3(rx, ry, rz, gi[0] * rx + gi[1] * ry + gi[2] * rz, gi[3] * ry + gi[4] * rz, gi[5] * rz);
+    float dmy2 = dot3(rx, ry, rz, gj[0] * rx + gj[1] * ry + gj[2] * rz, gj[3] * ry + gj[4] * rz, gj[5] * rz);
+    float dmy3 = 1.0f;
+    if (eta_ab < eta_crit)
+    {
+        float etaDiff = 5.0f * (eta_ab - eta_crit);
+        dmy3          = expf(-etaDiff * etaDiff);
+    }
+    float A_ab   = (dmy2 != 0.0f) ? dmy1 / dmy2 : 0.0f;
+    float A_abp1 = 1.0f + A_ab;
+    float q      = 4.0f * A_ab / (A_abp1 * A_abp1);
+    q            = q < 1.0f ? q : 1.0f;  /* stl::min(T(1), x) */
+    q            = 0.0f < q ? q : 0.0f;  /* stl::max(T(0), x) */
+    float phi_ab = 0.5f * dmy3 * q;
+    return -phi_ab * (dmy1 + dmy2);
+}
+
 static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
-                          float Atmin, float Atmax, float ramp, float* maxvsignal)
+                          float Atmin, float Atmax, float ramp, int avClean, float* maxvsignal)
 {
     double xi = s->x[i], yi = s->y[i], zi = s->z[i];
     float  vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
@@ -990,6 +1027,14 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
     float  mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
     float  c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i],
           c33i = s->c33[i];
+    float gradV_i[6] = {0, 0, 0, 0, 0, 0};
+    if (avClean)
+    {
+        gradV_i[0] = s->dV11[i], gradV_i[1] = s->dV12[i], gradV_i[2] = s->dV13[i];
+        gradV_i[3] = s->dV22[i], gradV_i[4] = s->dV23[i], gradV_i[5] = s->dV33[i];
+    }
+    /* T(32) * M_PI / T(3) / T(neighborsCount + 1) is formed in double, cbrt in double, stored as float */
+    float eta_crit = (float)cbrt((double)32.0f * M_PI / (double)3.0f / (double)(float)(cnt + 1));
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
         uint32_t j   = nb[pj];
@@ -1024,6 +1069,11 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
         float xmassj = s->xm[j];
         float rhoj   = kxj * mj / xmassj;
         float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+        if (avClean)
+        {
+            float gradV_j[6] = {s->dV11[j], s->dV12[j], s->dV13[j], s->dV22[j], s->dV23[j], s->dV33[j]};
+            rv += avRvCorrection(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gradV_j); /* stl::min */
+        }
         float wij    = rv / dist;
         /* artificial_viscosity<float> (kernels.hpp:70-84): (alpha_i + alpha_j) / 4.0 is a double */
         float viscosity_ij = 0.0f;
@@ -1093,7 +1143,7 @@ double ox_momentum_energy(ox_state* s, const ox_params* p, const ox_box* b, cons
         size_t ni         = i - first;
         float  maxvsignal = 0;
         momentumJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s, p->Atmin,
-                      p->Atmax, p->ramp, &maxvsignal);
+                      p->Atmax, p->ramp, p->avClean, &maxvsignal);
         float dt_i = tsKCourant(maxvsignal, s->h[i], s->c[i], (float)p->Kcour);
         minDt      = minDt < dt_i ? minDt : dt_i;
     }

@@ -39,6 +39,7 @@ typedef struct ox_params
     float    alphamin, alphamax, decay_constant; /* 0.05, 1.0, 0.2 */
     float    Atmin, Atmax, ramp;                 /* 0.1, 0.2, 1/(Atmax-Atmin) */
     double   maxDtIncrease;                      /* 1.1 */
+    int32_t  avClean; /* HydroVeProp<avClean> (ve_hydro.hpp:50): IAD writes dV11..dV33, momentum adds avRvCorrection */
 } ox_params;
 
 /* Host particle state of the VE propagator (ve_hydro.hpp:70-85 conserved + dependent fields). */
@@ -59,6 +60,7 @@ typedef struct ox_state
     float    *c11, *c12, *c13, *c22, *c23, *c33;
     uint32_t* nc;
     uint64_t* keys;
+    float    *dV11, *dV12, *dV13, *dV22, *dV23, *dV33; /* velocity gradient (GradVFields), avClean only */
     /* scalars (ParticlesData members) */
     double minDt, minDt_m1, ttot, minDtCourant, minDtRho;
 } ox_state;

@@ -507,7 +507,39 @@ PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_pa
     a.Atmax          = p->Atmax;
     a.ramp           = p->ramp;
     a.Kcour          = (float)p->Kcour;
+    a.dV11           = f->dV11;
+    a.dV12           = f->dV12;
+    a.dV13           = f->dV13;
+    a.dV22           = f->dV22;
+    a.dV23           = f->dV23;
+    a.dV33           = f->dV33;
+    a.avClean        = 0;
     return a;
+}
+
+int momentumEnergy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
+                   const sx_box* box, float* minDtCourant, bool avClean)
+{
+    if (int e = checkList(c, g, p)) return e;
+    if (f->tdpdTrho) return fail(c, SX_ERR_ARG, "tdpdTrho != NULL is not supported by the VE momentum kernel");
+    if (avClean && !(f->dV11 && f->dV12 && f->dV13 && f->dV22 && f->dV23 && f->dV33))
+        return fail(c, SX_ERR_ARG, "avClean momentum needs the velocity gradient dV11..dV33");
+    Records r = records(c, f->n);
+    packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+    packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
+    packT(f->n, f->xm, f->kx, f->prho, f->alpha, r.rt, c->stream);
+    packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, nullptr, r.rc, c->stream);
+    float huge = 1e10f; // momentum_energy_gpu.cu:127
+    SX_HIP(c, hipMemcpyAsync(c->minDt, &huge, 4, hipMemcpyHostToDevice, c->stream));
+    PairArgs a = pairArgs(c, g, f, p, box, r);
+    a.groupDt  = groupDt;
+    a.avClean  = avClean ? 1 : 0;
+    c->hydro().momentumEnergy(a, c->stream);
+    SX_HIP(c, hipGetLastError());
+    SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->minDt, 4, hipMemcpyDeviceToHost, c->stream));
+    SX_HIP(c, hipStreamSynchronize(c->stream));
+    if (minDtCourant) *minDtCourant = c->hostScalar[0];
+    return SX_OK;
 }
 
 } // namespace
@@ -588,23 +620,13 @@ extern "C"
     int sx_momentum_energy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
                            const sx_box* box, float* minDtCourant)
     {
-        if (int e = checkList(c, g, p)) return e;
-        if (f->tdpdTrho) return fail(c, SX_ERR_ARG, "tdpdTrho != NULL is not supported by the VE momentum kernel");
-        Records r = records(c, f->n);
-        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
-        packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
-        packT(f->n, f->xm, f->kx, f->prho, f->alpha, r.rt, c->stream);
-        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, nullptr, r.rc, c->stream);
-        float huge = 1e10f; // momentum_energy_gpu.cu:127
-        SX_HIP(c, hipMemcpyAsync(c->minDt, &huge, 4, hipMemcpyHostToDevice, c->stream));
-        PairArgs a = pairArgs(c, g, f, p, box, r);
-        a.groupDt  = groupDt;
-        c->hydro().momentumEnergy(a, c->stream);
-        SX_HIP(c, hipGetLastError());
-        SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->minDt, 4, hipMemcpyDeviceToHost, c->stream));
-        SX_HIP(c, hipStreamSynchronize(c->stream));
-        if (minDtCourant) *minDtCourant = c->hostScalar[0];
-        return SX_OK;
+        return momentumEnergy(c, g, groupDt, f, p, box, minDtCourant, false);
+    }
+
+    int sx_momentum_energy_avclean(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f,
+                                   const sx_params* p, const sx_box* box, float* minDtCourant)
+    {
+        return momentumEnergy(c, g, groupDt, f, p, box, minDtCourant, true);
     }
 
     int sx_positions(sx_ctx* c, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,

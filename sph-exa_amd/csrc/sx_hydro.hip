@@ -212,6 +212,15 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(PairArgs a)
         float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
         a.curlv[i] = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
     }
+    if (a.dV11) // doGradV (divv_curlv_kern.hpp:113-121)
+    {
+        a.dV11[i] = norm_kxi * dVx0;
+        a.dV12[i] = norm_kxi * (dVx1 + dVy0);
+        a.dV13[i] = norm_kxi * (dVx2 + dVz0);
+        a.dV22[i] = norm_kxi * dVy1;
+        a.dV23[i] = norm_kxi * (dVy2 + dVz1);
+        a.dV33[i] = norm_kxi * dVz2;
+    }
 }
 
 //! AVswitchesJLoop (hydro_ve/av_switches_kern.hpp:43-137); alpha is read-modify-write
@@ -280,8 +289,9 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(PairArgs a)
     a.alpha[i] = alpha_i;
 }
 
-//! momentumAndEnergyJLoop<avClean=false> (hydro_ve/momentum_energy_kern.hpp:65-222) + Courant time-step
+//! momentumAndEnergyJLoop<avClean> (hydro_ve/momentum_energy_kern.hpp:65-222) + Courant time-step
 //! reduction (momentum_energy_gpu.cu:94-118).  tdpdTrho == nullptr => eCoeff = prho_i.
+template<bool AVC>
 __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
 {
     SX_PAIR_PROLOGUE
@@ -301,6 +311,14 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
         float      hiInv3  = hiInv * hiInv * hiInv;
         float      maxvsignali = 0.0f;
         float      mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
+        float      gradV_i[6] = {0, 0, 0, 0, 0, 0};
+        float      eta_crit   = 0.0f;
+        if constexpr (AVC)
+        {
+            gradV_i[0] = a.dV11[i], gradV_i[1] = a.dV12[i], gradV_i[2] = a.dV13[i];
+            gradV_i[3] = a.dV22[i], gradV_i[4] = a.dV23[i], gradV_i[5] = a.dV33[i];
+            eta_crit   = avEtaCrit(cnt);
+        }
         for (unsigned k = 0; k < cnt; ++k)
         {
             uint32_t   j  = nbj(k);
@@ -335,6 +353,11 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
             float xmassj = tj.xm;
             float rhoj   = tj.kx * mj / xmassj;
             float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            if constexpr (AVC)
+            {
+                const float gradV_j[6] = {a.dV11[j], a.dV12[j], a.dV13[j], a.dV22[j], a.dV23[j], a.dV33[j]};
+                rv += avRvCorrection<!kFastClusters>(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gradV_j);
+            }
             float wij    = rv / dist;
             // artificial_viscosity<float> (kernels.hpp:70-84): (alpha_i + alpha_j) / 4.0 is evaluated in double
             float viscosity_ij = 0.0f;
@@ -510,7 +533,9 @@ static void launchAv(const PairArgs& a, hipStream_t s)
 static void launchMomentum(const PairArgs& a, hipStream_t s)
 {
     if (kFastClusters && a.localLists) return cluster::momentumEnergy(a, s);
-    if (a.numGroups) momentumEnergyKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
+    if (!a.numGroups) return;
+    if (a.avClean) momentumEnergyKernel<true><<<pairGrid(a), kBlock, 0, s>>>(a);
+    else momentumEnergyKernel<false><<<pairGrid(a), kBlock, 0, s>>>(a);
 }
 static void launchEos(const EosArgs& a, hipStream_t s)
 {

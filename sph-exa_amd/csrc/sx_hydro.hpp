@@ -45,7 +45,43 @@ struct PairArgs
     double        dt;    // AV switches time-step (d.minDt)
     const double* dtPtr; // if non-null, *dtPtr replaces dt (device-resident time-step)
     float  Atmin, Atmax, ramp, Kcour;
+    // avClean (HydroVeProp<true>, ve_hydro.hpp:50-85): the IAD kernel writes the velocity gradient (GradVFields)
+    // when dV11 != nullptr (doGradV, iad_divv_curlv_gpu.cu:96-97); momentum reads it when avClean != 0
+    float *dV11, *dV12, *dV13, *dV22, *dV23, *dV33;
+    int    avClean;
 };
+
+//! eta_crit of momentumAndEnergyJLoop<avClean> (momentum_energy_kern.hpp:112): formed in double, stored as float
+__device__ __forceinline__ float avEtaCrit(unsigned cnt)
+{
+    return (float)cbrt((double)32.0f * 3.14159265358979323846 / 3.0 / (double)(float)(cnt + 1));
+}
+
+/*! avRvCorrection<float, float> (momentum_energy_kern.hpp:43-63): symv is the upper-triangle product
+ *  (kernels.hpp:88-95), dot the right fold a0*b0 + (a1*b1 + a2*b2) (util/array.hpp:253-256), stl::min/max
+ *  (primitives/stl.hpp:53-65).  EXACT evaluates exp in double and rounds once (glibc's expf wherever that is
+ *  correctly rounded); the fast variant uses expf. */
+template<bool EXACT>
+__device__ __forceinline__ float avRvCorrection(float rx, float ry, float rz, float eta_ab, float eta_crit,
+                                                const float (&gi)[6], const float (&gj)[6])
+{
+    const float dmy1 = rx * (gi[0] * rx + gi[1] * ry + gi[2] * rz) + (ry * (gi[3] * ry + gi[4] * rz) + rz * (gi[5] * rz));
+    const float dmy2 = rx * (gj[0] * rx + gj[1] * ry + gj[2] * rz) + (ry * (gj[3] * ry + gj[4] * rz) + rz * (gj[5] * rz));
+    float       dmy3 = 1.0f;
+    if (eta_ab < eta_crit)
+    {
+        const float etaDiff = 5.0f * (eta_ab - eta_crit);
+        const float arg     = -etaDiff * etaDiff;
+        dmy3                = EXACT ? (float)exp((double)arg) : expf(arg);
+    }
+    const float A_ab   = (dmy2 != 0.0f) ? dmy1 / dmy2 : 0.0f;
+    const float A_abp1 = 1.0f + A_ab;
+    float       q      = 4.0f * A_ab / (A_abp1 * A_abp1);
+    q                  = q < 1.0f ? q : 1.0f;
+    q                  = 0.0f < q ? q : 0.0f;
+    const float phi_ab = 0.5f * dmy3 * q;
+    return -phi_ab * (dmy1 + dmy2);
+}
 
 struct EosArgs
 {

@@ -62,11 +62,6 @@ struct Rec9
     float4 a, b;
     float  s;
 };
-struct Rec20
-{
-    float4 p, v, t, a, b;
-};
-
 __device__ __forceinline__ float relc(double x, double o, const DevBox& b, int k) { return (float)foldPbc(x - o, b, k); }
 
 //! sets up the cluster and decides (workgroup-uniformly) whether folded coordinates are minimum-image for every
@@ -436,6 +431,15 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
             a.curlv[i]      = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
         }
+        if (a.dV11) // doGradV (divv_curlv_kern.hpp:113-121)
+        {
+            a.dV11[i] = norm_kxi * dVx0;
+            a.dV12[i] = norm_kxi * (dVx1 + dVy0);
+            a.dV13[i] = norm_kxi * (dVx2 + dVz0);
+            a.dV22[i] = norm_kxi * dVy1;
+            a.dV23[i] = norm_kxi * (dVy2 + dVz1);
+            a.dV33[i] = norm_kxi * dVz2;
+        }
     }
 }
 
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
     a.alpha[cu.i] = alpha_i;
 }
 
-// ---- momentum + energy: momentumAndEnergyJLoop<avClean=false> (momentum_energy_kern.hpp:65-222) -------------------
+// ---- momentum + energy: momentumAndEnergyJLoop<avClean> (momentum_energy_kern.hpp:65-222) -------------------
 //! Atwood-ramped momentum weights (momentum_energy_kern.hpp:178-195): xm_i^(2-s) xm_j^s and xm_j^(2-s) xm_i^s with
 //! s = 0 below Atmin, 1 above Atmax (both exact products) and the ramp in between (exp2/log2 form)
 __device__ __forceinline__ void atwoodWeights(float Atwood, float Atmin, float Atmax, float ramp, float xmi, float lxi,
@@ -535,7 +539,15 @@ __device__ __forceinline__ void atwoodWeights(float Atwood, float Atmin, float A
     }
 }
 
-template<int CH, int SPLIT>
+//! LDS record of the momentum kernel: 80 B, + 24 B of velocity gradient with avClean
+template<bool AVC>
+struct RecM
+{
+    float4 p, v, t, a, b, g;
+    float2 g2;
+};
+
+template<int CH, int SPLIT, bool AVC>
 __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, 1/h
@@ -543,6 +555,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     __shared__ float4 sT[CH]; // m, xm, rho, m*prho
     __shared__ float4 sA[CH]; // alpha, c11, c12, c13
     __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
+    __shared__ float4 sG[AVC ? CH : 1];  // dV11, dV12, dV13, dV22 (avClean)
+    __shared__ float2 sG2[AVC ? CH : 1]; // dV23, dV33
     __shared__ float  s_red[kClusterWaves * SPLIT];
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
@@ -562,6 +576,15 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     float maxvsignali = 0.0f;
     float mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
     bool  res = false;
+    float gradV_i[6] = {0, 0, 0, 0, 0, 0};
+    float eta_crit   = 0.0f;
+    if constexpr (AVC)
+    {
+        const uint32_t q = cu.iSafe;
+        gradV_i[0] = a.dV11[q], gradV_i[1] = a.dV12[q], gradV_i[2] = a.dV13[q];
+        gradV_i[3] = a.dV22[q], gradV_i[4] = a.dV23[q], gradV_i[5] = a.dV33[q];
+        eta_crit   = avEtaCrit(cu.cnt);
+    }
     neighborLoop<CH, SPLIT>(
         cu,
         [&](uint32_t j, uint32_t slot) {
@@ -576,9 +599,19 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             sT[slot]        = make_float4(r.m, t.xm, rho, r.m * t.prho);
             sA[slot]        = make_float4(t.alpha, c6.c11, c6.c12, c6.c13);
             sB[slot]        = make_float4(c6.c22, c6.c23, c6.c33, r.m / rho);
+            if constexpr (AVC)
+            {
+                sG[slot]  = make_float4(a.dV11[j], a.dV12[j], a.dV13[j], a.dV22[j]);
+                sG2[slot] = make_float2(a.dV23[j], a.dV33[j]);
+            }
         },
-        [&](uint32_t p) { return Rec20{sP[p], sV[p], sT[p], sA[p], sB[p]}; },
-        [&](const Rec20& r) {
+        [&](uint32_t p) {
+            RecM<AVC> r;
+            r.p = sP[p], r.v = sV[p], r.t = sT[p], r.a = sA[p], r.b = sB[p];
+            if constexpr (AVC) r.g = sG[p], r.g2 = sG2[p];
+            return r;
+        },
+        [&](const RecM<AVC>& r) {
             const float4 &P = r.p, &V = r.v, &T = r.t, &A = r.a, &B = r.b;
             float         rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
@@ -588,8 +621,9 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
             const float hjInv  = P.w;
             const float hjInv3 = hjInv * hjInv * hjInv;
-            const float Wi     = hiInv3 * kernelW(dist * hiInv);
-            const float Wj     = hjInv3 * kernelW(dist * hjInv);
+            const float v1     = dist * hiInv, v2 = dist * hjInv;
+            const float Wi     = hiInv3 * kernelW(v1);
+            const float Wj     = hjInv3 * kernelW(v2);
             const float tA1i   = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
             const float tA2i   = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
             const float tA3i   = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
@@ -597,7 +631,12 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float tA2j   = -(A.z * rx + B.x * ry + B.y * rz) * Wj;
             const float tA3j   = -(A.w * rx + B.y * ry + B.z * rz) * Wj;
             const float mj = T.x, rhoj = T.z, cj = V.w;
-            const float rv  = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            float       rv = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            if constexpr (AVC)
+            {
+                const float gj[6] = {r.g.x, r.g.y, r.g.z, r.g.w, r.g2.x, r.g2.y};
+                rv += avRvCorrection<false>(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gj);
+            }
             const float wij = rv * rinv;
             // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
             const float vij_signal = (alpha_i + A.x) * 0.25f * (ci + cj) - 2.0f * wij;
@@ -682,7 +721,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
 #ifndef SX_SPLIT_ME
 #define SX_SPLIT_ME 2
 #endif
-constexpr int kChXm = 2048, kChVd = 2048, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME;
+constexpr int kChXm = 2048, kChVd = 2048, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME, kChMeAvc = 1536;
 
 static inline unsigned clusters(const PairArgs& a) { return (a.numGroups + kClusterWaves - 1) / kClusterWaves; }
 
@@ -704,7 +743,9 @@ void avSwitches(const PairArgs& a, hipStream_t s)
 }
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) momentumEnergyKernel<kChMe, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    if (!a.numGroups) return;
+    if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME, true><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
 
 } // namespace cluster

@@ -354,6 +354,7 @@ struct sx_sim
     uint32_t *order, *nc;
     float *   xm, *kx, *gradh, *prho, *c, *divv, *curlv, *c11, *c12, *c13, *c22, *c23, *c33, *ax, *ay, *az;
     double*   du;
+    float*    dV[6]{}; // dV11, dV12, dV13, dV22, dV23, dV33 (avClean only)
     RecX*     rx;
     RecV*     rv;
     RecT*     rt;
@@ -432,6 +433,16 @@ void allocFields(sx_sim* s, size_t cap)
     s->ay    = a.get<float>("ay", cap);
     s->az    = a.get<float>("az", cap);
     s->du    = a.get<double>("du", cap);
+    if (s->p.avClean)
+    {
+        // GradVFields, allocated only with avClean (ve_hydro.hpp:80-85)
+        s->dV[0] = a.get<float>("dV11", cap);
+        s->dV[1] = a.get<float>("dV12", cap);
+        s->dV[2] = a.get<float>("dV13", cap);
+        s->dV[3] = a.get<float>("dV22", cap);
+        s->dV[4] = a.get<float>("dV23", cap);
+        s->dV[5] = a.get<float>("dV33", cap);
+    }
     s->rx    = a.get<RecX>("rx", cap);
     s->rv    = a.get<RecV>("rv", cap);
     s->rt    = a.get<RecT>("rt", cap);
@@ -510,6 +521,8 @@ PairArgs simPairArgs(sx_sim* s)
     a.Atmax          = s->p.Atmax;
     a.ramp           = s->p.ramp;
     a.Kcour          = (float)s->p.Kcour;
+    a.dV11 = s->dV[0], a.dV12 = s->dV[1], a.dV13 = s->dV[2], a.dV22 = s->dV[3], a.dV23 = s->dV[4], a.dV33 = s->dV[5];
+    a.avClean = s->p.avClean ? 1 : 0;
     return a;
 }
 
@@ -1040,7 +1053,16 @@ extern "C"
         SIM_HIP(hipEventRecord(s->kev[8], st));
         H.avSwitches(pa, st);
         SIM_HIP(hipEventRecord(s->kev[9], st));
-        if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
+        if (s->p.avClean)
+        {
+            // the reference exchanges dV11,dV12,dV22,dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo
+            // dV13 undefined; all six are exchanged here so the result does not depend on the decomposition
+            if (int e = haloExchange(s, {{s->dV[0], 4}, {s->dV[1], 4}, {s->dV[2], 4}, {s->dV[3], 4}, {s->dV[4], 4},
+                                         {s->dV[5], 4}, {s->alpha, 4}},
+                                     st))
+                return e;
+        }
+        else if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- momentum + energy
         packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);

@@ -144,6 +144,15 @@ sx_fields toFields(Dataset& d)
     f.gradh    = rawPtr(dv.gradh);
     f.keys     = rawPtr(dv.keys);
     f.nc       = rawPtr(dv.nc);
+    if constexpr (requires { dv.dV11; })
+    {
+        // GradVFields: non-empty only with avClean (ve_hydro.hpp:80-85); doGradV = dV11.size() == x.size()
+        if (dv.dV11.size() == dv.x.size())
+        {
+            f.dV11 = rawPtr(dv.dV11), f.dV12 = rawPtr(dv.dV12), f.dV13 = rawPtr(dv.dV13);
+            f.dV22 = rawPtr(dv.dV22), f.dV23 = rawPtr(dv.dV23), f.dV33 = rawPtr(dv.dV33);
+        }
+    }
     return f;
 }
 
@@ -242,13 +251,15 @@ template<bool avClean, class GroupView, class Dataset, class Box>
 void computeMomentumEnergy(const GroupView& grp, float* groupDt, Dataset& d, const Box& box)
 {
     namespace sa = sphexa_amd;
-    static_assert(!avClean, "the AV-cleaning momentum variant is not provided by libsphexa_hip (DESIGN.md 9)");
     auto  g = sa::toGroups(grp);
     auto  f = sa::toFields(d);
     auto  p = sa::toParams(d);
     auto  b = sa::toBox(box);
     float minDt;
-    sa::check(sx_momentum_energy(sa::context(), &g, groupDt, &f, &p, &b, &minDt), "computeMomentumEnergy");
+    // both instantiations of the reference seam (momentum_energy_gpu.cu:147-152)
+    if constexpr (avClean)
+        sa::check(sx_momentum_energy_avclean(sa::context(), &g, groupDt, &f, &p, &b, &minDt), "computeMomentumEnergy");
+    else sa::check(sx_momentum_energy(sa::context(), &g, groupDt, &f, &p, &b, &minDt), "computeMomentumEnergy");
     d.minDtCourant = minDt;
 }
 

@@ -29,7 +29,7 @@ class SxParams(C.Structure):
     _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
-                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double)]
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -136,6 +136,8 @@ def lib():
                                      C.POINTER(SxBox), C.c_double]),
         "sx_momentum_energy": (C.c_int, [vp, C.POINTER(SxGroups), vp, C.POINTER(SxFields), C.POINTER(SxParams),
                                          C.POINTER(SxBox), C.POINTER(C.c_float)]),
+        "sx_momentum_energy_avclean": (C.c_int, [vp, C.POINTER(SxGroups), vp, C.POINTER(SxFields),
+                                                 C.POINTER(SxParams), C.POINTER(SxBox), C.POINTER(C.c_float)]),
         "sx_positions": (C.c_int, [vp, u32, u32, C.c_double, C.c_double, C.POINTER(SxFields), C.c_double,
                                    C.c_float, C.POINTER(SxBox)]),
         "sx_update_h": (C.c_int, [vp, u32, u32, u32, vp, vp]),
@@ -192,13 +194,14 @@ def halo_layout(recv_counts, rank, num_local):
     return off, tuple(int(v) for v in out)
 
 
-def default_params(K=None, ngmax=150, ng0=100):
-    """ParticlesData defaults (particles_data.hpp:86-138)."""
+def default_params(K=None, ngmax=150, ng0=100, av_clean=False):
+    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> in sx_sim."""
     if K is None:
         K = lib().sx_kernel_constant()
     return SxParams(K=K, ng0=ng0, ngmax=ngmax, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0, alphamin=0.05,
                     alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
-                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1)
+                    ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
+                    avClean=1 if av_clean else 0)
 
 
 def make_box(lim, bnd):
@@ -279,16 +282,18 @@ class DeviceArray:
 class DeviceState:
     """A full ParticlesData-like device field set built from a host dict of numpy arrays."""
 
-    def __init__(self, ctx, host):
+    def __init__(self, ctx, host, grad_v=False):
+        """grad_v: also allocate the velocity gradient dV11..dV33 (GradVFields of the avClean propagator)"""
         self.ctx = ctx
         n = len(host["x"])
         self.n = n
         self.dev = {}
         self.fields = SxFields()
         self.fields.n = n
+        grad = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
         for name, _ in FIELD_ORDER:
-            if name in ("rho", "p", "tdpdTrho", "u", "mue", "mui", "cv", "dV11", "dV12", "dV13", "dV22", "dV23",
-                        "dV33", "markRamp", "rung"):
+            if name in ("rho", "p", "tdpdTrho", "u", "mue", "mui", "cv", "markRamp", "rung") or \
+                    (name in grad and not grad_v):
                 continue
             dt = DTYPES[name]
             if name in host:

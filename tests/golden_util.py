@@ -25,7 +25,8 @@ def state_from(d, prefix):
     n = d[prefix + "x"].size
     st = po.HostState(n)
     for name, _ in po.STATE_FIELDS:
-        st.arrays[name][:] = d[prefix + name]
+        if prefix + name in d:  # fixtures made before the avClean fields existed hold no dV*
+            st.arrays[name][:] = d[prefix + name]
     sc = d[prefix + "scalars"]
     st.minDt, st.minDt_m1, st.ttot, st.minDtCourant, st.minDtRho = [float(v) for v in sc]
     return st

@@ -164,7 +164,7 @@ def test_neighbors_edge_cases(ctx, ora):
 
 # ---- per-kernel parity on the reference's own neighbor list ---------------------------------------------------
 
-def kernel_chain(ctx, d, exact):
+def kernel_chain(ctx, d, exact, av_clean=False):
     """run the VE kernels on fixture kernels.npz inputs with the reference neighbor list imported"""
     ctx.set_exact(exact)
     box = gutil.box_to_sx(gu.box_from(d["box"]))
@@ -173,7 +173,7 @@ def kernel_chain(ctx, d, exact):
     host = gutil.host_dict(st)
     host["h"] = d["h_after_iter"]
     host["nc"] = d["nc"]
-    ds = sx.DeviceState(ctx, host)
+    ds = sx.DeviceState(ctx, host, grad_v=av_clean)
     p = sx.default_params()
     nb = ctx.upload(d["nbr"])
     ctx.check(ctx.L.sx_import_neighbors(ctx.h, 0, n, 150, nb.ptr), "import")
@@ -188,13 +188,14 @@ def kernel_chain(ctx, d, exact):
     ctx.check(L.sx_eos(h, 0, n, 10.0, 5.0 / 3.0, f.temp, f.m, f.kx, f.xm, f.gradh, f.prho, f.c, None, None), "eos")
     out["prho"], out["c"] = ds.get("prho"), ds.get("c")
     ctx.check(L.sx_iad_divv_curlv(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box)), "iad")
-    for k in ["c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv"]:
+    for k in ["c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv"] + \
+            (["dV11", "dV12", "dV13", "dV22", "dV23", "dV33"] if av_clean else []):
         out[k] = ds.get(k)
     ctx.check(L.sx_av_switches(h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box), float(st.minDt)), "av")
     out["alpha"] = ds.get("alpha")
     mdt = C.c_float()
-    ctx.check(L.sx_momentum_energy(h, C.byref(g), None, C.byref(ds.fields), C.byref(p), C.byref(box),
-                                   C.byref(mdt)), "momentum")
+    me = L.sx_momentum_energy_avclean if av_clean else L.sx_momentum_energy
+    ctx.check(me(h, C.byref(g), None, C.byref(ds.fields), C.byref(p), C.byref(box), C.byref(mdt)), "momentum")
     out["minDtCourant"] = np.array([mdt.value])
     for k in ["du", "ax", "ay", "az"]:
         out[k] = ds.get(k)

@@ -69,3 +69,26 @@ def test_full_steps(ora, ic, side, steps):
         for k in a.arrays:
             assert np.array_equal(a.arrays[k], b.arrays[k]), k
         assert a.minDt == b.minDt
+
+
+@pytest.mark.parametrize("ic,side,steps", [("sedov", 12, 4), ("noh", 14, 4)])
+def test_full_steps_av_clean(ora, ic, side, steps):
+    """HydroVeProp<avClean=true>: IAD writes the velocity gradient (divv_curlv_kern.hpp:113-121), momentum adds
+    avRvCorrection (momentum_energy_kern.hpp:43-63, 157-161); bit-exact against the reference's template"""
+    st, box = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
+    a, b = st.copy(), st.copy()
+    pr, po_ = ref.params(av_clean=True), ora.params(av_clean=True)
+    for _ in range(steps):
+        ref.step(a, box, params=pr)
+        ora.step(b, box, params=po_)
+        for k in a.arrays:
+            assert np.array_equal(a.arrays[k], b.arrays[k]), k
+        assert a.minDt == b.minDt
+    assert np.any(b.dV11 != 0) and not np.array_equal(b.ax, _plain_steps(ora, ic, side, steps).ax)
+
+
+def _plain_steps(lib, ic, side, steps):
+    st, box = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
+    for _ in range(steps):
+        lib.step(st, box)
+    return st
