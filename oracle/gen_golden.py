@@ -12,6 +12,10 @@ Fixtures
                  per-kernel output computed by the reference *Impl loops on it
   tree_rand.npz  2000 seeded random points: Hilbert keys, cornerstone leaves (bucket 16), linked octree
                  arrays, node centers/sizes, neighbor lists + counts with and without h iteration
+  evrard14.npz   Evrard substitute n=14 (1472 particles, key-sorted): gravity alone (expansion centers + MAC
+                 radii, quadrupoles, accelerations, egrav; G = 1, theta = 0.5) and 2 full VE steps with gravity
+
+    python oracle/gen_golden.py [--only gravity]
 """
 import os
 import sys
@@ -44,11 +48,35 @@ def run_steps(ref, st, box, nsteps, name):
     np.savez_compressed(os.path.join(OUT, name), **out)
 
 
+def gravity_fixture(ref):
+    st, box = po.evrard_state(14)
+    keys = ref.sfc_keys(st, box).copy()
+    order = np.argsort(keys, kind="stable")
+    for k in po.CONSERVED:
+        st.arrays[k][:] = st.arrays[k][order]
+    st.keys[:] = keys[order]
+    p = ref.params(g=1.0, theta=0.5)
+    out = {"box": box_arr(box)}
+    out.update(snapshot(st, "s0_"))
+    g = st.copy()
+    egrav, cen, mp = ref.gravity(g, box, p)
+    out.update({"grav_centers": cen, "grav_multipoles": mp, "grav_ax": g.ax.copy(), "grav_ay": g.ay.copy(),
+                "grav_az": g.az.copy(), "grav_egrav": np.array([egrav])})
+    for s in range(1, 3):
+        ref.step(st, box, params=p)
+        out.update(snapshot(st, f"s{s}_"))
+        out[f"s{s}_egrav"] = np.array([st.egrav])
+    np.savez_compressed(os.path.join(OUT, "evrard14.npz"), **out)
+
+
 def main():
     ref = po.load_ref()
     if ref is None:
         raise SystemExit("oracle/_ref/libsphexa_ref.so missing: run `make -C oracle` where /root/reference exists")
     os.makedirs(OUT, exist_ok=True)
+    gravity_fixture(ref)
+    if "--only" in sys.argv:
+        return
 
     st, box = po.sedov_state(10)
     run_steps(ref, st, box, 3, "sedov10.npz")

@@ -31,7 +31,8 @@ class OxParams(C.Structure):
     _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
-                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32)]
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32),
+                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double)]
 
 
 STATE_FIELDS = [
@@ -56,15 +57,16 @@ _CT = {np.float64: C.c_double, np.float32: C.c_float, np.uint64: C.c_uint64, np.
 class OxState(C.Structure):
     _fields_ = [("n", C.c_size_t)] + [(name, C.POINTER(_CT[t])) for name, t in STATE_FIELDS] + [
         ("minDt", C.c_double), ("minDt_m1", C.c_double), ("ttot", C.c_double), ("minDtCourant", C.c_double),
-        ("minDtRho", C.c_double)]
+        ("minDtRho", C.c_double), ("egrav", C.c_double)]
 
 
-def default_params(K, av_clean=False):
-    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true>."""
+def default_params(K, av_clean=False, g=0.0, theta=0.5):
+    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true>; g != 0 turns on
+    self-gravity with opening parameter theta (sphexa.cpp:127)."""
     return OxParams(K=K, ng0=100, ngmax=150, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0,
                     alphamin=0.05, alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
                     ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
-                    avClean=1 if av_clean else 0)
+                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2)
 
 
 def make_box(lo=-0.5, hi=0.5, periodic=True):
@@ -87,6 +89,7 @@ class HostState:
         self.ttot = 0.0
         self.minDtCourant = math.inf
         self.minDtRho = math.inf
+        self.egrav = 0.0
 
     def __getattr__(self, item):
         arrays = self.__dict__.get("arrays")
@@ -103,12 +106,14 @@ class HostState:
             setattr(s, name, a.ctypes.data_as(C.POINTER(_CT[t])))
         s.minDt, s.minDt_m1, s.ttot = self.minDt, self.minDt_m1, self.ttot
         s.minDtCourant, s.minDtRho = self.minDtCourant, self.minDtRho
+        s.egrav = self.egrav
         self._s = s
         return s
 
     def pull(self, s):
         self.minDt, self.minDt_m1, self.ttot = s.minDt, s.minDt_m1, s.ttot
         self.minDtCourant, self.minDtRho = s.minDtCourant, s.minDtRho
+        self.egrav = s.egrav
 
     def copy(self):
         o = HostState(self.n)
@@ -192,6 +197,40 @@ def noh_state(side):
     return st, make_box(lo, hi, False)
 
 
+def evrard_state(side):
+    """Evrard collapse substitute (the glass block is unavailable): side^3 lattice in [-1,1]^3 cut to
+    r <= 1, contracted by sqrt(r) to a 1/r density profile (evrard_init.hpp:90-108 contractRhoProfile), field values of
+    initEvrardFields (:50-88): m = 1/N, u0 = 0.05, v = 0, h from the 1/r concentration; G = 1, dt0 = 1e-4.
+    Open box [-1.25,1.25]^3: the reference re-fits open boxes to the particles every sync (makeGlobalBox), this
+    fixed box leaves room for the outer shell to expand."""
+    r = 1.0
+    step = (2.0 * r) / side
+    coord = -r + 0.5 * step + np.arange(side, dtype=np.float64) * step
+    zz, yy, xx = np.meshgrid(coord, coord, coord, indexing="ij")
+    x, y, z = xx.ravel(), yy.ravel(), zz.ravel()
+    rad0 = np.sqrt(x * x + y * y + z * z)
+    keep = (rad0 <= r) & (rad0 > 1e-9 * r)  # odd sides: no particle at the singular center (h -> 0)
+    x, y, z, rad0 = x[keep], y[keep], z[keep], rad0[keep]
+    con = np.sqrt(rad0)
+    x, y, z = x * con, y * con, z * con
+    n = x.size
+    st = HostState(n)
+    st.x[:], st.y[:], st.z[:] = x, y, z
+    st.m[:] = np.float32(1.0 / n)
+    st.alpha[:] = np.float32(0.05)
+    cv = ideal_gas_cv()
+    st.temp[:] = 0.05 / np.float64(cv)
+    total_volume = 4.0 * math.pi / 3.0 * r ** 3
+    c0 = 2.0 / 3.0 * n / total_volume
+    radius = np.sqrt(x * x + y * y + z * z)
+    conc = c0 / np.maximum(radius, 1e-12)
+    st.h[:] = (np.cbrt(3.0 / (4.0 * math.pi) * 100 / conc) * 0.5).astype(np.float32)
+    st.id[:] = np.arange(n, dtype=np.uint64)
+    st.minDt = 1e-4
+    st.minDt_m1 = 1e-4
+    return st, make_box(-1.25 * r, 1.25 * r, False)
+
+
 def _bind(lib):
     P = C.c_void_p
     u32p = C.POINTER(C.c_uint32)
@@ -217,6 +256,8 @@ def _bind(lib):
         ("update_h_range", None, [C.POINTER(OxState), C.c_uint, C.c_uint, C.c_uint]),
         ("step", C.c_int, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint]),
         ("update_h", C.c_float, [C.c_uint, C.c_uint, C.c_float]),
+        ("gravity", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint, C.c_uint,
+                                 C.c_uint, P, P, C.c_int]),
     ]:
         for prefix in ("ref_", "ox_"):
             if hasattr(lib, prefix + name):
@@ -240,8 +281,8 @@ class Lib:
                                C.byref(K))
         self.wh, self.whd, self.K = wh, whd, K.value
 
-    def params(self, av_clean=False):
-        return default_params(self.K, av_clean)
+    def params(self, av_clean=False, g=0.0, theta=0.5):
+        return default_params(self.K, av_clean, g, theta)
 
     def sfc_keys(self, st, box):
         self.lib.sfc_keys(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.n, C.byref(box),
@@ -315,6 +356,19 @@ class Lib:
         p = params or self.params()
         s = st.struct()
         self.lib.positions(C.byref(s), C.byref(p), C.byref(box), first, st.n if last is None else last)
+
+    def gravity(self, st, box, params, first=0, last=None, bucket=64):
+        """self-gravity of a key-sorted state: adds G*acc to ax, ay, az of [first, last); returns
+        (egrav, centers (numNodes x 4: mass center, mac^2), multipoles (numNodes x 8 float))"""
+        last = st.n if last is None else last
+        s = st.struct()
+        nn = int(self.lib.gravity(C.byref(s), C.byref(params), C.byref(box), bucket, first, last, None, None, -1))
+        cen = np.zeros((nn, 4), np.float64)
+        mp = np.zeros((nn, 8), np.float32)
+        s = st.struct()
+        eg = self.lib.gravity(C.byref(s), C.byref(params), C.byref(box), bucket, first, last, cen.ctypes.data,
+                              mp.ctypes.data, nn)
+        return eg, cen, mp
 
     def step(self, st, box, bucket=64, params=None):
         p = params or self.params()

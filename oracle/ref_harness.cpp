@@ -54,6 +54,9 @@
 #include "sph/sph_kernel_tables.hpp"
 #include "sph/update_h.hpp"
 
+#include "ryoanji/nbody/traversal_cpu.hpp"
+#include "ryoanji/nbody/upsweep_cpu.hpp"
+
 #include "sx_host_types.h"
 
 using KeyType = uint64_t;
@@ -426,6 +429,53 @@ extern "C"
         sph::updateTempHost(first, last, d);
     }
 
+    /*! @brief self-gravity with the reference's own functions on the tree of the key-sorted state (single rank):
+     *  expansion centers as FocusedOctree::updateCenters + setMacRadius(1/theta) (octree_focus_mpi.hpp:325-459),
+     *  ryoanji::computeLeafMultipoles + upsweepMultipoles (global_multipole.hpp:44-71 without the MPI exchanges),
+     *  ryoanji::computeGravity (traversal_cpu.hpp:166-230, numShells 0).  cap < 0: return the node count. */
+    static double gravityOnTree(ox_state* s, const ox_params* p, const cstone::Box<double>& box, TreeArrays& t,
+                                unsigned first, unsigned last, double* centersOut, float* multipolesOut, int cap)
+    {
+        using namespace cstone;
+        TreeNodeIndex nLeaf = nNodes(t.leaves), nTot = TreeNodeIndex(t.prefixes.size()), nInt = nTot - nLeaf;
+        std::vector<SourceCenterType<double>> centers(nTot);
+        computeLeafMassCenter<double, float, double>(gsl::span<const double>(s->x, s->n),
+                                                     gsl::span<const double>(s->y, s->n),
+                                                     gsl::span<const double>(s->z, s->n),
+                                                     gsl::span<const float>(s->m, s->n),
+                                                     {t.leafToInternal.data() + nInt, size_t(nLeaf)}, t.layout.data(),
+                                                     centers.data());
+        upsweep({t.levelRange.data(), t.levelRange.size()}, {t.childOffsets.data(), t.childOffsets.size()},
+                centers.data(), CombineSourceCenter<double>{});
+        setMac<double, KeyType>({t.prefixes.data(), t.prefixes.size()}, {centers.data(), centers.size()},
+                                1.0f / p->theta, box);
+        std::vector<ryoanji::CartesianQuadrupole<float>> mp(nTot);
+        ryoanji::computeLeafMultipoles(s->x, s->y, s->z, s->m, {t.leafToInternal.data() + nInt, size_t(nLeaf)},
+                                       t.layout.data(), centers.data(), mp.data());
+        ryoanji::upsweepMultipoles({t.levelRange.data(), t.levelRange.size()}, t.childOffsets.data(), centers.data(),
+                                   mp.data());
+        // computeGravity works on leaf-index ranges: targets [layout[l0], layout[l1])
+        TreeNodeIndex l0 = TreeNodeIndex(std::upper_bound(t.layout.begin(), t.layout.end(), first) - t.layout.begin()) - 1;
+        TreeNodeIndex l1 = TreeNodeIndex(std::lower_bound(t.layout.begin(), t.layout.end(), last) - t.layout.begin());
+        double egrav = 0;
+        ryoanji::computeGravity(t.childOffsets.data(), t.internalToLeaf.data(), centers.data(), mp.data(),
+                                t.layout.data(), l0, l1, s->x, s->y, s->z, s->h, s->m, box, float(p->g),
+                                (double*)nullptr, s->ax, s->ay, s->az, &egrav, 0);
+        if (centersOut && cap >= nTot) std::memcpy(centersOut, centers.data(), sizeof(double) * 4 * nTot);
+        if (multipolesOut && cap >= nTot) std::memcpy(multipolesOut, mp.data(), sizeof(float) * 8 * nTot);
+        return egrav;
+    }
+
+    double ref_gravity(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket, unsigned first,
+                       unsigned last, double* centersOut, float* multipolesOut, int cap)
+    {
+        auto       box = makeBox(b);
+        TreeArrays t;
+        t.build(s->keys, s->n, bucket, box);
+        if (cap < 0) return double(t.prefixes.size());
+        return gravityOnTree(s, p, box, t, first, last, centersOut, multipolesOut, cap);
+    }
+
     void ref_update_h_range(ox_state* s, unsigned ng0, unsigned first, unsigned last)
     {
         sph::updateSmoothingLengthCpu(first, last, ng0, s->nc, s->h);
@@ -488,9 +538,22 @@ extern "C"
         sph::computeAVswitchesImpl(0, n, d, box);
         if (p->avClean) sph::computeMomentumEnergyImpl<true>(0, n, d, box);
         else sph::computeMomentumEnergyImpl<false>(0, n, d, box);
+        double minDtAcc = INFINITY;
+        if (p->g != 0.0)
+        {
+            // mHolder_.upsweep + traverse (ve_hydro.hpp:193-202), accelerationTimestep (ts_global.hpp:47-67)
+            s->egrav = gravityOnTree(s, p, box, t, 0, unsigned(n), nullptr, nullptr, 0);
+            double maxAccSq = 0.0;
+            for (size_t i = 0; i < n; ++i)
+            {
+                cstone::Vec3<double> X{s->ax[i], s->ay[i], s->az[i]};
+                maxAccSq = std::max(norm2(X), maxAccSq);
+            }
+            minDtAcc = p->etaAcc * std::sqrt(p->eps / std::sqrt(maxAccSq));
+        }
 
         // --- integrate: computeTimestep (ts_global.hpp:97-112 without MPI_Allreduce)
-        double minDtLoc = std::min({double(INFINITY), d.minDtCourant, d.minDtRho, 1.1 * d.minDt});
+        double minDtLoc = std::min({minDtAcc, d.minDtCourant, d.minDtRho, 1.1 * d.minDt});
         s->ttot += minDtLoc;
         d.minDt_m1 = d.minDt;
         d.minDt    = minDtLoc;

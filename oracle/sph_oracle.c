@@ -1225,6 +1225,326 @@ void ox_update_h_range(ox_state* s, unsigned ng0, unsigned first, unsigned last)
         s->h[i] = ox_update_h(ng0, s->nc[i], s->h[i]);
 }
 
+
+/* ------------------------------------------------------------------------------------------------
+ * self-gravity (ryoanji CPU path, single rank, open box): expansion centers and MAC radii of the focus tree
+ * (octree_focus_mpi.hpp:325-392 updateCenters, :432-459 setMacRadius), Cartesian quadrupoles
+ * (upsweep_cpu.hpp:53-86, cartesian_qpole.hpp:88-257), Barnes-Hut traversal (traversal_cpu.hpp:80-230)
+ * ------------------------------------------------------------------------------------------------ */
+
+/* cstone::massCenter<double> + normalizeMass (source_center.hpp:45-81) */
+static void grav_mass_center(const double* x, const double* y, const double* z, const float* m, uint32_t first,
+                             uint32_t last, double* c)
+{
+    c[0] = c[1] = c[2] = c[3] = 0.0;
+    for (uint32_t i = first; i < last; ++i)
+    {
+        double w = (double)m[i];
+        c[0] += w * x[i];
+        c[1] += w * y[i];
+        c[2] += w * z[i];
+        c[3] += w;
+    }
+    double invM = (c[3] != 0.0) ? 1.0 / c[3] : 0.0;
+    c[0] *= invM;
+    c[1] *= invM;
+    c[2] *= invM;
+}
+
+/* P2M<double, float, float> (cartesian_qpole.hpp:88-126): float accumulators, each update formed in double */
+static void grav_p2m(const double* x, const double* y, const double* z, const float* m, uint32_t begin, uint32_t end,
+                     const double* center, float* gv)
+{
+    for (int k = 0; k < 8; ++k)
+        gv[k] = 0.0f;
+    if (begin == end) return;
+    for (uint32_t i = begin; i < end; ++i)
+    {
+        double m_i = (double)m[i];
+        double rx = x[i] - center[0], ry = y[i] - center[1], rz = z[i] - center[2];
+        gv[0] = (float)((double)gv[0] + m_i);
+        gv[1] = (float)((double)gv[1] + rx * rx * m_i);
+        gv[2] = (float)((double)gv[2] + rx * ry * m_i);
+        gv[3] = (float)((double)gv[3] + rx * rz * m_i);
+        gv[4] = (float)((double)gv[4] + ry * ry * m_i);
+        gv[5] = (float)((double)gv[5] + ry * rz * m_i);
+        gv[6] = (float)((double)gv[6] + rz * rz * m_i);
+    }
+    float traceQ = gv[1] + gv[4] + gv[6];
+    gv[7]        = traceQ;
+    gv[1]        = 3 * gv[1] - traceQ;
+    gv[4]        = 3 * gv[4] - traceQ;
+    gv[6]        = 3 * gv[6] - traceQ;
+    gv[2] *= 3;
+    gv[3] *= 3;
+    gv[5] *= 3;
+}
+
+/* addQuadrupole<float, double> (cartesian_qpole.hpp:210-232), parallel axis theorem */
+static void grav_add_quadrupole(float* comp, double rx, double ry, double rz, const float* add)
+{
+    double rx_2 = rx * rx, ry_2 = ry * ry, rz_2 = rz * rz;
+    double r_2  = (rx_2 + ry_2 + rz_2) * (1.0 / 3.0);
+    double ml   = (double)(add[0] * 3);
+    comp[7]     = (float)((double)(comp[7] + add[7]) + ml * r_2);
+    comp[0] += add[0];
+    comp[1] = (float)((double)comp[1] + ((double)add[1] + ml * (rx_2 - r_2)));
+    comp[2] = (float)((double)comp[2] + ((double)add[2] + ml * rx * ry));
+    comp[3] = (float)((double)comp[3] + ((double)add[3] + ml * rx * rz));
+    comp[4] = (float)((double)comp[4] + ((double)add[4] + ml * (ry_2 - r_2)));
+    comp[5] = (float)((double)comp[5] + ((double)add[5] + ml * ry * rz));
+    comp[6] = (float)((double)comp[6] + ((double)add[6] + ml * (rz_2 - r_2)));
+}
+
+/* expansion centers (mass centers, upsweep with CombineSourceCenter) and setMac (computeVecMacR2,
+ * traversal/macs.hpp:82-97), then leaf P2M + upsweepMultipoles (M2M); centers4[4*node] = {x,y,z,mac^2} */
+static void grav_upsweep(const ox_state* s, const ox_tree* t, float invTheta, double* centers4, float* mp)
+{
+    int nInt = t->nTot - t->nLeaf;
+#pragma omp parallel for schedule(static)
+    for (int L = 0; L < t->nLeaf; ++L)
+    {
+        int node = t->leafToInternal[nInt + L];
+        grav_mass_center(s->x, s->y, s->z, s->m, t->layout[L], t->layout[L + 1], centers4 + 4 * (size_t)node);
+    }
+    for (int level = MAXLEVEL; level >= 0; --level)
+    {
+#pragma omp parallel for schedule(static)
+        for (int i = t->levelRange[level]; i < t->levelRange[level + 1]; ++i)
+        {
+            int c = t->childOffsets[i];
+            if (!c) continue;
+            double acc[4] = {0, 0, 0, 0};
+            for (int k = c; k < c + 8; ++k)
+            {
+                double w = centers4[4 * (size_t)k + 3];
+                acc[0] += w * centers4[4 * (size_t)k + 0];
+                acc[1] += w * centers4[4 * (size_t)k + 1];
+                acc[2] += w * centers4[4 * (size_t)k + 2];
+                acc[3] += w;
+            }
+            double invM = (acc[3] != 0.0) ? 1.0 / acc[3] : 0.0;
+            centers4[4 * (size_t)i + 0] = acc[0] * invM;
+            centers4[4 * (size_t)i + 1] = acc[1] * invM;
+            centers4[4 * (size_t)i + 2] = acc[2] * invM;
+            centers4[4 * (size_t)i + 3] = acc[3];
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < t->nTot; ++i)
+    {
+        double* c  = centers4 + 4 * (size_t)i;
+        double  dx = c[0] - t->centers[3 * (size_t)i], dy = c[1] - t->centers[3 * (size_t)i + 1],
+               dz = c[2] - t->centers[3 * (size_t)i + 2];
+        double sx = t->sizes[3 * (size_t)i], sy = t->sizes[3 * (size_t)i + 1], sz = t->sizes[3 * (size_t)i + 2];
+        double smax = sx > sy ? sx : sy;
+        smax        = smax > sz ? smax : sz;
+        double sd   = sqrt(dx * dx + (dy * dy + dz * dz)); /* norm2 = right fold */
+        double l    = 2.0 * smax;
+        double mac  = l * (double)invTheta + sd;
+        c[3]        = (c[3] != 0.0) ? mac * mac : 0.0;
+    }
+#pragma omp parallel for schedule(static)
+    for (int L = 0; L < t->nLeaf; ++L)
+    {
+        int node = t->leafToInternal[nInt + L];
+        grav_p2m(s->x, s->y, s->z, s->m, t->layout[L], t->layout[L + 1], centers4 + 4 * (size_t)node,
+                 mp + 8 * (size_t)node);
+    }
+    for (int level = MAXLEVEL; level >= 0; --level)
+    {
+#pragma omp parallel for schedule(static)
+        for (int i = t->levelRange[level]; i < t->levelRange[level + 1]; ++i)
+        {
+            int c = t->childOffsets[i];
+            if (!c) continue;
+            float* out = mp + 8 * (size_t)i;
+            for (int k = 0; k < 8; ++k)
+                out[k] = 0.0f;
+            for (int k = c; k < c + 8; ++k)
+            {
+                const double* Xo = centers4 + 4 * (size_t)i;
+                const double* Xi = centers4 + 4 * (size_t)k;
+                grav_add_quadrupole(out, Xo[0] - Xi[0], Xo[1] - Xi[1], Xo[2] - Xi[2], mp + 8 * (size_t)k);
+            }
+        }
+    }
+}
+
+/* M2P<double, double, float> (cartesian_qpole.hpp:175-201); inverseSquareRoot on the host = 1/sqrt */
+static inline void grav_m2p(double* acc, double tx, double ty, double tz, const double* com, const float* M)
+{
+    double r0 = tx - com[0], r1 = ty - com[1], r2 = tz - com[2];
+    double rr       = r0 * r0 + (r1 * r1 + r2 * r2);
+    double r_minus1 = 1.0 / sqrt(rr);
+    double r_minus2 = r_minus1 * r_minus1;
+    double r_minus5 = r_minus2 * r_minus2 * r_minus1;
+    double Qrx      = r0 * (double)M[1] + r1 * (double)M[2] + r2 * (double)M[3];
+    double Qry      = r0 * (double)M[2] + r1 * (double)M[4] + r2 * (double)M[5];
+    double Qrz      = r0 * (double)M[3] + r1 * (double)M[5] + r2 * (double)M[6];
+    double rQr      = r0 * Qrx + r1 * Qry + r2 * Qrz;
+    double rQrAndMonopole = (-2.5 * rQr * r_minus5 - (double)M[0] * r_minus1) * r_minus2;
+    acc[0] += -((double)M[0] * r_minus1 + 0.5 * r_minus5 * rQr);
+    acc[1] += r_minus5 * Qrx + rQrAndMonopole * r0;
+    acc[2] += r_minus5 * Qry + rQrAndMonopole * r1;
+    acc[3] += r_minus5 * Qrz + rQrAndMonopole * r2;
+}
+
+/* P2P<double, double, float, float> (kernel.hpp:514-535), softened by h_i + h_j */
+static inline void grav_p2p(double* acc, double xi, double yi, double zi, double xj, double yj, double zj, float mj,
+                            float hi, float hj)
+{
+    double dx = xj - xi, dy = yj - yi, dz = zj - zi;
+    double R2     = dx * dx + (dy * dy + dz * dz);
+    float  h_ij   = hi + hj;
+    float  h_ij2  = h_ij * h_ij;
+    double R2eff  = (R2 < (double)h_ij2) ? (double)h_ij2 : R2;
+    double invR   = 1.0 / sqrt(R2eff);
+    double invR2  = invR * invR;
+    double invR3m = (double)mj * invR * invR2;
+    acc[0] -= invR3m * R2;
+    acc[1] += dx * invR3m;
+    acc[2] += dy * invR3m;
+    acc[3] += dz * invR3m;
+}
+
+#define GRAV_GROUP 16
+
+/* computeGravity (traversal_cpu.hpp:166-230) over targets [first, last) in groups of 16 consecutive particles,
+ * computeGravityGroup (:80-151) with singleTraversal (traversal.hpp:69-110).  The reference sizes the target box of
+ * a partial last group over all 16 array slots (uninitialised past the valid ones); the valid targets are used
+ * here.  Adds G*acc to ax, ay, az; returns 0.5 * sum G m_i phi_i. */
+static double grav_traverse(ox_state* s, const ox_tree* t, const double* centers4, const float* mp, float G,
+                            uint32_t first, uint32_t last)
+{
+    double egrav = 0.0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : egrav)
+    for (uint32_t i0 = first; i0 < last; i0 += GRAV_GROUP)
+    {
+        uint32_t nt = last - i0 < GRAV_GROUP ? last - i0 : GRAV_GROUP;
+        double   acc[GRAV_GROUP][4];
+        double   lo[3], hi[3];
+        for (uint32_t k = 0; k < nt; ++k)
+        {
+            acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0;
+            double p[3] = {s->x[i0 + k], s->y[i0 + k], s->z[i0 + k]};
+            for (int d = 0; d < 3; ++d)
+            {
+                if (k == 0 || p[d] < lo[d]) lo[d] = p[d];
+                if (k == 0 || p[d] > hi[d]) hi[d] = p[d];
+            }
+        }
+        double tc[3], ts[3];
+        for (int d = 0; d < 3; ++d)
+        {
+            tc[d] = (hi[d] + lo[d]) * 0.5;
+            ts[d] = (hi[d] - lo[d]) * 0.5;
+        }
+#define GRAV_DESCEND(node, out)                                                                                        \
+    do {                                                                                                               \
+        const double* com_ = centers4 + 4 * (size_t)(node);                                                            \
+        double        d0 = fabs(tc[0] - com_[0]) - ts[0], d1 = fabs(tc[1] - com_[1]) - ts[1],                          \
+               d2 = fabs(tc[2] - com_[2]) - ts[2];                                                                     \
+        d0 += fabs(d0);                                                                                                \
+        d1 += fabs(d1);                                                                                                \
+        d2 += fabs(d2);                                                                                                \
+        d0 *= 0.5;                                                                                                     \
+        d1 *= 0.5;                                                                                                     \
+        d2 *= 0.5;                                                                                                     \
+        double R2_ = d0 * d0 + (d1 * d1 + d2 * d2);                                                                    \
+        (out)      = R2_ < fabs(com_[3]);                                                                              \
+        if (!(out))                                                                                                    \
+            for (uint32_t k = 0; k < nt; ++k)                                                                          \
+                grav_m2p(acc[k], s->x[i0 + k], s->y[i0 + k], s->z[i0 + k], com_, mp + 8 * (size_t)(node));            \
+    } while (0)
+#define GRAV_LEAF(node)                                                                                                \
+    do {                                                                                                               \
+        int      lidx_ = t->internalToLeaf[node];                                                                      \
+        uint32_t s0_ = t->layout[lidx_], s1_ = t->layout[lidx_ + 1];                                                   \
+        for (uint32_t k = 0; k < nt; ++k)                                                                              \
+            for (uint32_t j = s0_; j < s1_; ++j)                                                                       \
+                grav_p2p(acc[k], s->x[i0 + k], s->y[i0 + k], s->z[i0 + k], s->x[j], s->y[j], s->z[j], s->m[j],         \
+                         s->h[i0 + k], s->h[j]);                                                                       \
+    } while (0)
+        int descend;
+        GRAV_DESCEND(0, descend);
+        if (descend)
+        {
+            if (t->childOffsets[0] == 0) { GRAV_LEAF(0); }
+            else
+            {
+                int stack[128];
+                stack[0]     = 0;
+                int stackPos = 1, node = 0;
+                do
+                {
+                    for (int octant = 0; octant < 8; ++octant)
+                    {
+                        int child = t->childOffsets[node] + octant;
+                        int d;
+                        GRAV_DESCEND(child, d);
+                        if (d)
+                        {
+                            if (t->childOffsets[child] == 0) { GRAV_LEAF(child); }
+                            else { stack[stackPos++] = child; }
+                        }
+                    }
+                    node = stack[--stackPos];
+                } while (node != 0);
+            }
+        }
+#undef GRAV_DESCEND
+#undef GRAV_LEAF
+        for (uint32_t k = 0; k < nt; ++k)
+        {
+            double u = (double)(G * s->m[i0 + k]) * acc[k][0];
+            egrav += u;
+            s->ax[i0 + k] = (float)((double)s->ax[i0 + k] + (double)G * acc[k][1]);
+            s->ay[i0 + k] = (float)((double)s->ay[i0 + k] + (double)G * acc[k][2]);
+            s->az[i0 + k] = (float)((double)s->az[i0 + k] + (double)G * acc[k][3]);
+        }
+    }
+    return 0.5 * egrav;
+}
+
+/* upsweep + traversal on the tree of the (key-sorted) state: adds gravity to ax, ay, az of [first, last), returns
+ * egrav; centers4/multipoles (numNodes x 4 doubles / x 8 floats) are written when non-null */
+double ox_gravity(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket, unsigned first, unsigned last,
+                  double* centersOut, float* multipolesOut, int cap)
+{
+    ox_tree t;
+    tree_build(&t, s->keys, s->n, bucket, b);
+    if (cap < 0)
+    {
+        int nTot = t.nTot; /* size query */
+        tree_free(&t);
+        return (double)nTot;
+    }
+    double* c4 = (double*)calloc(4 * (size_t)t.nTot, sizeof(double));
+    float*  mp = (float*)calloc(8 * (size_t)t.nTot, sizeof(float));
+    grav_upsweep(s, &t, 1.0f / p->theta, c4, mp);
+    double egrav = grav_traverse(s, &t, c4, mp, (float)p->g, first, last);
+    if (centersOut && cap >= t.nTot) memcpy(centersOut, c4, sizeof(double) * 4 * (size_t)t.nTot);
+    if (multipolesOut && cap >= t.nTot) memcpy(multipolesOut, mp, sizeof(float) * 8 * (size_t)t.nTot);
+    free(c4);
+    free(mp);
+    tree_free(&t);
+    return egrav;
+}
+
+/* accelerationTimestep (ts_global.hpp:47-67) over [first, last) */
+double ox_acc_timestep(const ox_state* s, const ox_params* p, unsigned first, unsigned last)
+{
+    double maxAccSq = 0.0;
+    for (size_t i = first; i < last; ++i)
+    {
+        double ax = s->ax[i], ay = s->ay[i], az = s->az[i];
+        double a2 = ax * ax + (ay * ay + az * az);
+        maxAccSq  = a2 > maxAccSq ? a2 : maxAccSq;
+    }
+    return p->etaAcc * sqrt(p->eps / sqrt(maxAccSq));
+}
+
 typedef struct
 {
     uint64_t key;
@@ -1298,10 +1618,22 @@ int ox_step(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket)
     s->minDtRho = p->Krho / fabs((double)maxDivv);
     ox_av_switches(s, p, b, nbr, 0, (unsigned)n);
     ox_momentum_energy(s, p, b, nbr, 0, (unsigned)n);
+    double minDtAcc = INFINITY;
+    if (p->g != 0.0)
+    {
+        /* mHolder_.upsweep + traverse (ve_hydro.hpp:193-202) on the same tree, then accelerationTimestep */
+        double* c4 = (double*)calloc(4 * (size_t)t.nTot, sizeof(double));
+        float*  mp = (float*)calloc(8 * (size_t)t.nTot, sizeof(float));
+        grav_upsweep(s, &t, 1.0f / p->theta, c4, mp);
+        s->egrav = grav_traverse(s, &t, c4, mp, (float)p->g, 0, (unsigned)n);
+        free(c4);
+        free(mp);
+        minDtAcc = ox_acc_timestep(s, p, 0, (unsigned)n);
+    }
 
     double minDtLoc = INFINITY;
-    double cand[3]  = {s->minDtCourant, s->minDtRho, p->maxDtIncrease * s->minDt};
-    for (int k = 0; k < 3; ++k)
+    double cand[4]  = {minDtAcc, s->minDtCourant, s->minDtRho, p->maxDtIncrease * s->minDt};
+    for (int k = 0; k < 4; ++k)
         minDtLoc = cand[k] < minDtLoc ? cand[k] : minDtLoc;
     s->ttot += minDtLoc;
     s->minDt_m1 = s->minDt;

@@ -40,6 +40,10 @@ typedef struct ox_params
     float    Atmin, Atmax, ramp;                 /* 0.1, 0.2, 1/(Atmax-Atmin) */
     double   maxDtIncrease;                      /* 1.1 */
     int32_t  avClean; /* HydroVeProp<avClean> (ve_hydro.hpp:50): IAD writes dV11..dV33, momentum adds avRvCorrection */
+    float    theta;   /* gravity opening parameter (--theta, sphexa.cpp:127: 0.5 with gravity) */
+    double   g;       /* gravitational constant (ParticlesData::g, 0 = no self-gravity) */
+    double   eps;     /* 0.005 (accelerationTimestep, ts_global.hpp:47-67) */
+    double   etaAcc;  /* 0.2 */
 } ox_params;
 
 /* Host particle state of the VE propagator (ve_hydro.hpp:70-85 conserved + dependent fields). */
@@ -63,6 +67,7 @@ typedef struct ox_state
     float    *dV11, *dV12, *dV13, *dV22, *dV23, *dV33; /* velocity gradient (GradVFields), avClean only */
     /* scalars (ParticlesData members) */
     double minDt, minDt_m1, ttot, minDtCourant, minDtRho;
+    double egrav; /* gravitational potential energy of the last step (ParticlesData::egrav) */
 } ox_state;
 
 #ifdef __cplusplus

@@ -1,0 +1,102 @@
+"""Self-gravity of the CPU oracle (oracle/sph_oracle.c, ryoanji CPU path restated) against the reference.
+
+* golden fixture tests/golden/evrard14.npz (made by oracle/gen_golden.py from oracle/_ref, the reference's own
+  computeLeafMassCenter / upsweep / setMac / computeLeafMultipoles / upsweepMultipoles / computeGravity):
+  expansion centers + MAC radii, quadrupoles and accelerations bit-exact; 2 full VE steps with gravity bit-exact;
+* where /root/reference was built (oracle/_ref): the same on other sizes (`ref` marker);
+* physics: the quadrupole tree code against an O(N^2) direct sum (theta = 0.5: |a - a_direct| < 1 % of |a|
+  rms), and theta -> 0 reproduces the direct sum.
+The reference sizes the target box of a partial last group of 16 over uninitialised slots
+(traversal_cpu.hpp:184-190); comparisons use N divisible by 16 or skip that group.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+import pyoracle as po
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return po.load_oracle()
+
+
+def sorted_evrard(lib, side):
+    st, box = po.evrard_state(side)
+    keys = lib.sfc_keys(st, box).copy()
+    o = np.argsort(keys, kind="stable")
+    for k in po.CONSERVED:
+        st.arrays[k][:] = st.arrays[k][o]
+    st.keys[:] = keys[o]
+    return st, box
+
+
+def test_gravity_golden(ora):
+    d = gu.load("evrard14.npz")
+    box = gu.box_from(d["box"])
+    st = gu.state_from(d, "s0_")
+    eg, cen, mp = ora.gravity(st, box, ora.params(g=1.0, theta=0.5))
+    assert np.array_equal(cen, d["grav_centers"])
+    assert np.array_equal(mp, d["grav_multipoles"])
+    for k in ("ax", "ay", "az"):
+        assert np.array_equal(st.arrays[k], d["grav_" + k]), k
+    assert eg == pytest.approx(float(d["grav_egrav"][0]), rel=1e-12)
+
+
+def test_gravity_steps_golden(ora):
+    d = gu.load("evrard14.npz")
+    box = gu.box_from(d["box"])
+    st = gu.state_from(d, "s0_")
+    p = ora.params(g=1.0, theta=0.5)
+    for s in (1, 2):
+        ora.step(st, box, params=p)
+        ref = gu.state_from(d, f"s{s}_")
+        for k in st.arrays:
+            assert np.array_equal(st.arrays[k], ref.arrays[k]), (s, k)
+        assert st.minDt == ref.minDt and st.egrav == pytest.approx(float(d[f"s{s}_egrav"][0]), rel=1e-12)
+
+
+@pytest.mark.ref
+@pytest.mark.skipif(po.load_ref() is None, reason="oracle/_ref not built (no /root/reference here)")
+@pytest.mark.parametrize("side,theta", [(16, 0.5), (20, 0.3), (20, 0.8)])
+def test_gravity_vs_reference(ora, side, theta):
+    ref = po.load_ref()
+    a, box = sorted_evrard(ref, side)
+    b = a.copy()
+    p = ora.params(g=1.0, theta=theta)
+    ea, ca, ma = ref.gravity(a, box, p)
+    eb, cb, mb = ora.gravity(b, box, p)
+    assert np.array_equal(ca, cb) and np.array_equal(ma, mb)
+    n = a.n - a.n % 16
+    for k in ("ax", "ay", "az"):
+        assert np.array_equal(a.arrays[k][:n], b.arrays[k][:n]), k
+    assert ea == pytest.approx(eb, rel=1e-6)
+
+
+def direct_sum(st, G=1.0):
+    x = np.stack([st.x, st.y, st.z], 1)
+    h = st.h.astype(np.float64)
+    m = st.m.astype(np.float64)
+    acc = np.zeros((st.n, 3))
+    for i in range(st.n):
+        dx = x - x[i]
+        r2 = np.sum(dx * dx, 1)
+        hij = (h[i] + h) ** 2
+        r2e = np.where(r2 < hij, hij, r2)
+        inv = 1.0 / np.sqrt(r2e)
+        acc[i] = G * np.sum((m * inv ** 3)[:, None] * dx, 0)
+    return acc
+
+
+def test_gravity_matches_direct_sum(ora):
+    st, box = sorted_evrard(ora, 12)
+    ref = direct_sum(st)
+    rms = np.sqrt(np.mean(np.sum(ref * ref, 1)))
+    for theta, tol in ((0.5, 1e-2), (0.05, 1e-4)):
+        s = st.copy()
+        ora.gravity(s, box, ora.params(g=1.0, theta=theta))
+        got = np.stack([s.ax, s.ay, s.az], 1).astype(np.float64)
+        err = np.sqrt(np.mean(np.sum((got - ref) ** 2, 1)))
+        assert err < tol * rms, (theta, err / rms)
