@@ -79,6 +79,9 @@ typedef struct sx_params
     float    Atmin, Atmax, ramp;                 /* 0.1, 0.2, 10 */
     double   maxDtIncrease;                      /* 1.1 */
     int32_t  avClean; /* sx_sim only: HydroVeProp<avClean=true> (ve_hydro.hpp:50, factory.hpp:56), 0 = off */
+    float    theta;   /* gravity opening parameter (sphexa.cpp:127: 0.5 with gravity) */
+    double   g;       /* gravitational constant (ParticlesData::g); sx_sim adds self-gravity when != 0 */
+    double   eps, etaAcc; /* accelerationTimestep (ts_global.hpp:47-67): 0.005, 0.2 */
 } sx_params;
 
 /*! Device pointers in sphexa::ParticlesData field order (particles_data.hpp:247-251); NULL where unused.
@@ -234,6 +237,19 @@ int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double d
                  double gamma, float muiConst, const sx_box* box);
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
 int sx_max_divv(sx_ctx* ctx, uint32_t first, uint32_t last, const float* divv, float* maxDivv);
+
+/* ---- self-gravity: ryoanji MultipoleHolder seam (multipole_holder.cuh:40-66, gravity_wrapper.hpp:104-174) ----- */
+/*! expansion centers (mass centers, {x,y,z,mac^2}, numNodes x 4 doubles; mac = 2 max(node size)/theta + |com-geo|,
+ *  setMac, source_center.hpp:130-143) and Cartesian quadrupoles (numNodes x 8 floats, Cqi order,
+ *  cartesian_qpole.hpp:59-126) of every node of the linked octree over f's particles (single rank: the focus tree
+ *  of syncGrav is the local tree).  Bit-identical to the reference CPU upsweep. */
+int sx_gravity_upsweep(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, float theta, double* centers,
+                       float* multipoles);
+/*! Barnes-Hut traversal for targets [g->firstBody, g->lastBody) (computeGravity, traversal_cpu.hpp:166-230: groups
+ *  of 16, vector MAC, quadrupole M2P, P2P softened by h_i + h_j): adds G * acc to f->ax, ay, az and returns the
+ *  potential energy 0.5 sum G m phi in *egrav.  Open boxes only (no Ewald replicas). */
+int sx_gravity_traverse(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                        const double* centers, const float* multipoles, float G, double* egrav);
 
 /* ---- multi-GPU transport (replaces the reference's MPI calls, see sph-exa_amd/csrc/sx_comm.hpp) ---------- */
 typedef struct sx_comm sx_comm;

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/sphexa_hip.h"
+#include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
 #include "sx_kernel_poly.hpp"
 #include "sx_tree.hpp"
@@ -683,3 +684,76 @@ extern "C"
     }
 
 } // extern "C"
+
+// ---- self-gravity (MultipoleHolder seam, ryoanji/interface/multipole_holder.cuh:40-66) -------------------------
+
+namespace
+{
+
+GravArgs gravArgs(sx_ctx* c, const sx_fields* f, const sx_tree* t)
+{
+    GravArgs a{};
+    a.numLeaves      = t->numLeafNodes;
+    a.numNodes       = t->numNodes;
+    a.childOffsets   = t->childOffsets;
+    a.internalToLeaf = t->internalToLeaf;
+    a.layout         = t->layout;
+    a.geoCenters     = t->centers;
+    a.geoSizes       = t->sizes;
+    a.x = f->x, a.y = f->y, a.z = f->z, a.m = f->m, a.h = f->h;
+    a.ax = f->ax, a.ay = f->ay, a.az = f->az;
+    return a;
+}
+
+} // namespace
+
+extern "C"
+{
+    int sx_gravity_upsweep(sx_ctx* c, const sx_fields* f, const sx_tree* tree, float theta, double* centers,
+                           float* multipoles)
+    {
+        if (!f || !tree || !centers || !multipoles || !(theta > 0.0f) || tree->numNodes < 1)
+            return fail(c, SX_ERR_ARG, "sx_gravity_upsweep: bad arguments");
+        GravArgs a   = gravArgs(c, f, tree);
+        a.leafToNode = c->arena.get<int32_t>("grav.leafToNode", (size_t)tree->numLeafNodes);
+        a.centers4   = centers;
+        a.multipoles = multipoles;
+        a.invTheta   = 1.0f / theta;
+        int32_t lr[kMaxLevel + 2];
+        SX_HIP(c, hipMemcpyAsync(lr, tree->levelRange, sizeof(lr), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        SX_HIP(c, gravityUpsweep(a, lr, c->stream));
+        return SX_OK;
+    }
+
+    int sx_gravity_traverse(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                            const double* centers, const float* multipoles, float G, double* egrav)
+    {
+        if (!g || !f || !tree || !box || !centers || !multipoles || g->lastBody > f->n)
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: bad arguments");
+        if (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic gravity (Ewald replicas) is not provided");
+        GravArgs a   = gravArgs(c, f, tree);
+        a.first      = g->firstBody;
+        a.last       = g->lastBody;
+        a.centers4   = const_cast<double*>(centers);
+        a.multipoles = const_cast<float*>(multipoles);
+        a.G          = G;
+        double* acc  = c->arena.get<double>("grav.egrav", 1);
+        uint32_t* er = c->arena.get<uint32_t>("grav.err", 1);
+        a.egrav      = acc;
+        a.err        = er;
+        SX_HIP(c, hipMemsetAsync(acc, 0, sizeof(double), c->stream));
+        SX_HIP(c, hipMemsetAsync(er, 0, sizeof(uint32_t), c->stream));
+        SX_HIP(c, gravityTraverse(a, c->stream));
+        double   eh = 0;
+        uint32_t eb = 0;
+        SX_HIP(c, hipMemcpyAsync(&eh, acc, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipMemcpyAsync(&eb, er, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        if (eb) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in Barnes-Hut");
+        if (egrav) *egrav = eh;
+        return SX_OK;
+    }
+} // extern "C"
+

@@ -1,0 +1,412 @@
+/*! @file sx_gravity.hip
+ * @brief Self-gravity for gfx950: expansion centers + MAC radii, Cartesian quadrupole upsweep and the Barnes-Hut
+ *        traversal with softened P2P (the ryoanji path of the reference, single rank, open box).
+ *
+ * Replaces MultipoleHolder::upsweep / compute (ryoanji/interface/multipole_holder.cuh:40-66, called from
+ * ve_hydro.hpp:193-202) and the focus tree's expansion centers (octree_focus_mpi.hpp:325-459).  The arithmetic
+ * follows the reference CPU functions (file compiled with -ffp-contract=off):
+ *   upsweep   mass centers (source_center.hpp:69-97), setMac / computeVecMacR2 (macs.hpp:82-97, :130-143 of
+ *             source_center.hpp), P2M (cartesian_qpole.hpp:88-126), M2M / addQuadrupole (:210-257): one thread
+ *             per node in the reference's sequential order, so centers and multipoles are bit-identical;
+ *   traverse  one wavefront per 64 consecutive targets = the reference's four target groups of 16
+ *             (traversal_cpu.hpp:171): every 16-lane quarter keeps its own target box and MAC decisions
+ *             (evaluateMac, macs.hpp:109-116), so each target sees exactly the reference's set of M2P nodes and P2P
+ *             leaves.  The wave walks the union of the four opening sets 8 nodes x 8 octants at a time with a
+ *             per-entry 4-bit quarter mask, collecting M2P nodes and P2P leaves into LDS lists that are evaluated
+ *             in batches (node data by scalar loads, leaf sources staged through LDS).  M2P (cartesian_qpole.hpp:
+ *             175-201) and P2P (kernel.hpp:514-535) in double with 1/sqrt like the reference's host path; only the
+ *             summation order differs from the reference's depth-first walk.
+ */
+#include "sx_gravity.hpp"
+
+namespace sx
+{
+
+namespace
+{
+
+constexpr int kGStack = 512; //!< per-wave traversal stack (entries: node << 4 | quarter mask)
+constexpr int kGList  = 256; //!< per-wave M2P / P2P interaction lists
+
+//! leaf index -> node index (the reference's leafToInternal + numInternalNodes)
+__global__ void leafToNodeKernel(const int32_t* childOffsets, const int32_t* internalToLeaf, int numNodes,
+                                 int32_t* leafToNode)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < numNodes && childOffsets[i] == 0) leafToNode[internalToLeaf[i]] = i;
+}
+
+//! cstone::massCenter<double> (source_center.hpp:69-81) per leaf, sequential like the reference
+__global__ void leafCentersKernel(GravArgs a)
+{
+    int L = blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= a.numLeaves) return;
+    double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (uint32_t i = a.layout[L]; i < a.layout[L + 1]; ++i)
+    {
+        double w = (double)a.m[i];
+        c0 += w * a.x[i];
+        c1 += w * a.y[i];
+        c2 += w * a.z[i];
+        c3 += w;
+    }
+    double invM = (c3 != 0.0) ? 1.0 / c3 : 0.0;
+    double* c   = a.centers4 + 4 * (size_t)a.leafToNode[L];
+    c[0] = c0 * invM, c[1] = c1 * invM, c[2] = c2 * invM, c[3] = c3;
+}
+
+//! CombineSourceCenter over the nodes of one level (cstone::upsweep, octree.hpp:584-602)
+__global__ void upsweepCentersKernel(GravArgs a, int start, int end)
+{
+    int i = start + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+    int c = a.childOffsets[i];
+    if (!c) return;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int k = c; k < c + 8; ++k)
+    {
+        const double* q = a.centers4 + 4 * (size_t)k;
+        double        w = q[3];
+        s0 += w * q[0];
+        s1 += w * q[1];
+        s2 += w * q[2];
+        s3 += w;
+    }
+    double  invM = (s3 != 0.0) ? 1.0 / s3 : 0.0;
+    double* o    = a.centers4 + 4 * (size_t)i;
+    o[0] = s0 * invM, o[1] = s1 * invM, o[2] = s2 * invM, o[3] = s3;
+}
+
+//! setMac: mac = 2 max(geo size) / theta + |com - geo center|, stored squared (0 for massless nodes)
+__global__ void setMacKernel(GravArgs a)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.numNodes) return;
+    double*       c  = a.centers4 + 4 * (size_t)i;
+    const double* gc = a.geoCenters + 3 * (size_t)i;
+    const double* gs = a.geoSizes + 3 * (size_t)i;
+    double dx = c[0] - gc[0], dy = c[1] - gc[1], dz = c[2] - gc[2];
+    double smax = gs[0] > gs[1] ? gs[0] : gs[1];
+    smax        = smax > gs[2] ? smax : gs[2];
+    double s    = sqrt(dx * dx + (dy * dy + dz * dz));
+    double mac  = 2.0 * smax * (double)a.invTheta + s;
+    c[3]        = (c[3] != 0.0) ? mac * mac : 0.0;
+}
+
+//! P2M<double, float, float> per leaf (float accumulators, each update formed in double)
+__global__ void leafP2MKernel(GravArgs a)
+{
+    int L = blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= a.numLeaves) return;
+    const int     node = a.leafToNode[L];
+    const double* cen  = a.centers4 + 4 * (size_t)node;
+    float         gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t b = a.layout[L], e = a.layout[L + 1];
+    if (b != e)
+    {
+        for (uint32_t i = b; i < e; ++i)
+        {
+            double m_i = (double)a.m[i];
+            double rx = a.x[i] - cen[0], ry = a.y[i] - cen[1], rz = a.z[i] - cen[2];
+            gv[0] = (float)((double)gv[0] + m_i);
+            gv[1] = (float)((double)gv[1] + rx * rx * m_i);
+            gv[2] = (float)((double)gv[2] + rx * ry * m_i);
+            gv[3] = (float)((double)gv[3] + rx * rz * m_i);
+            gv[4] = (float)((double)gv[4] + ry * ry * m_i);
+            gv[5] = (float)((double)gv[5] + ry * rz * m_i);
+            gv[6] = (float)((double)gv[6] + rz * rz * m_i);
+        }
+        float traceQ = gv[1] + gv[4] + gv[6];
+        gv[7]        = traceQ;
+        gv[1]        = 3 * gv[1] - traceQ;
+        gv[4]        = 3 * gv[4] - traceQ;
+        gv[6]        = 3 * gv[6] - traceQ;
+        gv[2] *= 3;
+        gv[3] *= 3;
+        gv[5] *= 3;
+    }
+    float* o = a.multipoles + 8 * (size_t)node;
+    for (int k = 0; k < 8; ++k)
+        o[k] = gv[k];
+}
+
+//! M2M with addQuadrupole<float, double> over the nodes of one level (upsweepMultipoles, upsweep_cpu.hpp:71-86)
+__global__ void upsweepMultipolesKernel(GravArgs a, int start, int end)
+{
+    int i = start + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+    int c = a.childOffsets[i];
+    if (!c) return;
+    float         comp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const double* Xo      = a.centers4 + 4 * (size_t)i;
+    for (int k = c; k < c + 8; ++k)
+    {
+        const double* Xi  = a.centers4 + 4 * (size_t)k;
+        const float*  add = a.multipoles + 8 * (size_t)k;
+        double rx = Xo[0] - Xi[0], ry = Xo[1] - Xi[1], rz = Xo[2] - Xi[2];
+        double rx_2 = rx * rx, ry_2 = ry * ry, rz_2 = rz * rz;
+        double r_2  = (rx_2 + ry_2 + rz_2) * (1.0 / 3.0);
+        double ml   = (double)(add[0] * 3);
+        comp[7]     = (float)((double)(comp[7] + add[7]) + ml * r_2);
+        comp[0] += add[0];
+        comp[1] = (float)((double)comp[1] + ((double)add[1] + ml * (rx_2 - r_2)));
+        comp[2] = (float)((double)comp[2] + ((double)add[2] + ml * rx * ry));
+        comp[3] = (float)((double)comp[3] + ((double)add[3] + ml * rx * rz));
+        comp[4] = (float)((double)comp[4] + ((double)add[4] + ml * (ry_2 - r_2)));
+        comp[5] = (float)((double)comp[5] + ((double)add[5] + ml * ry * rz));
+        comp[6] = (float)((double)comp[6] + ((double)add[6] + ml * (rz_2 - r_2)));
+    }
+    float* o = a.multipoles + 8 * (size_t)i;
+    for (int k = 0; k < 8; ++k)
+        o[k] = comp[k];
+}
+
+//! M2P<double, double, float> (cartesian_qpole.hpp:175-201)
+__device__ __forceinline__ void m2p(double (&acc)[4], double tx, double ty, double tz, const double* com, const float* M)
+{
+    double r0 = tx - com[0], r1 = ty - com[1], r2 = tz - com[2];
+    double rr       = r0 * r0 + (r1 * r1 + r2 * r2);
+    double r_minus1 = 1.0 / sqrt(rr);
+    double r_minus2 = r_minus1 * r_minus1;
+    double r_minus5 = r_minus2 * r_minus2 * r_minus1;
+    double Qrx      = r0 * (double)M[1] + r1 * (double)M[2] + r2 * (double)M[3];
+    double Qry      = r0 * (double)M[2] + r1 * (double)M[4] + r2 * (double)M[5];
+    double Qrz      = r0 * (double)M[3] + r1 * (double)M[5] + r2 * (double)M[6];
+    double rQr      = r0 * Qrx + r1 * Qry + r2 * Qrz;
+    double rQrAndMonopole = (-2.5 * rQr * r_minus5 - (double)M[0] * r_minus1) * r_minus2;
+    acc[0] += -((double)M[0] * r_minus1 + 0.5 * r_minus5 * rQr);
+    acc[1] += r_minus5 * Qrx + rQrAndMonopole * r0;
+    acc[2] += r_minus5 * Qry + rQrAndMonopole * r1;
+    acc[3] += r_minus5 * Qrz + rQrAndMonopole * r2;
+}
+
+//! P2P<double, double, float, float> (kernel.hpp:514-535), softened with h_i + h_j
+__device__ __forceinline__ void p2p(double (&acc)[4], double xi, double yi, double zi, double xj, double yj, double zj,
+                                    float mj, float hi, float hj)
+{
+    double dx = xj - xi, dy = yj - yi, dz = zj - zi;
+    double R2     = dx * dx + (dy * dy + dz * dz);
+    float  h_ij   = hi + hj;
+    float  h_ij2  = h_ij * h_ij;
+    double R2eff  = (R2 < (double)h_ij2) ? (double)h_ij2 : R2;
+    double invR   = 1.0 / sqrt(R2eff);
+    double invR2  = invR * invR;
+    double invR3m = (double)mj * invR * invR2;
+    acc[0] -= invR3m * R2;
+    acc[1] += dx * invR3m;
+    acc[2] += dy * invR3m;
+    acc[3] += dz * invR3m;
+}
+
+struct __attribute__((aligned(16))) GSrc
+{
+    double x, y, z;
+    float  m, h;
+};
+
+__global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
+{
+    __shared__ int  s_stack[4][kGStack];
+    __shared__ int  s_m2p[4][kGList];
+    __shared__ int  s_p2p[4][kGList];
+    __shared__ GSrc s_src[4][kWave];
+
+    const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4;
+    const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * 4 + wave;
+    const uint32_t i0   = a.first + g * kWave;
+    if (i0 >= a.last) return; // whole wave
+    const uint32_t i     = i0 + lane;
+    const bool     valid = i < a.last;
+    const uint32_t iS    = valid ? i : i0;
+    const double   xi = a.x[iS], yi = a.y[iS], zi = a.z[iS];
+    const float    hi = a.h[iS];
+    const uint64_t ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    // target box of each 16-lane quarter (computeCenterAndSize, traversal_cpu.hpp:43-59), over its valid targets
+    double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
+    double hiB[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1)
+        for (int d = 0; d < 3; ++d)
+        {
+            lo[d]  = fmin(lo[d], __shfl_xor(lo[d], o, 16));
+            hiB[d] = fmax(hiB[d], __shfl_xor(hiB[d], o, 16));
+        }
+    double tc[4][3], ts[4][3];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+        for (int d = 0; d < 3; ++d)
+        {
+            const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
+            tc[qq][d]      = (h + l) * 0.5;
+            ts[qq][d]      = (h - l) * 0.5;
+        }
+    const uint64_t bv     = __ballot(valid); // quarters with at least one valid target (lanes fill in order)
+    const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
+                            (((bv >> 32) & 0xffffull) ? 4u : 0u) | (((bv >> 48) & 0xffffull) ? 8u : 0u);
+
+    // evaluateMac: true = the target box is inside the node's acceptance radius (descend / P2P)
+    auto violates = [&](int node, unsigned mask) -> unsigned {
+        const double* com = a.centers4 + 4 * (size_t)node;
+        const double  c0 = com[0], c1 = com[1], c2 = com[2], mac2 = fabs(com[3]);
+        unsigned      v   = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+        {
+            if (!((mask >> qq) & 1u)) continue;
+            double d0 = fabs(tc[qq][0] - c0) - ts[qq][0], d1 = fabs(tc[qq][1] - c1) - ts[qq][1],
+                   d2 = fabs(tc[qq][2] - c2) - ts[qq][2];
+            d0 += fabs(d0);
+            d1 += fabs(d1);
+            d2 += fabs(d2);
+            d0 *= 0.5;
+            d1 *= 0.5;
+            d2 *= 0.5;
+            if (d0 * d0 + (d1 * d1 + d2 * d2) < mac2) v |= 1u << qq;
+        }
+        return v;
+    };
+
+    double acc[4] = {0, 0, 0, 0};
+    int    nM = 0, nP = 0, sp = 0;
+    bool   overflow = false;
+
+    auto flushM2P = [&]() {
+        for (int k = 0; k < nM; ++k)
+        {
+            const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
+            const int node = e >> 4;
+            if (valid && (((e & 15) >> q) & 1))
+                m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+        }
+        nM = 0;
+    };
+    auto flushP2P = [&]() {
+        for (int k = 0; k < nP; ++k)
+        {
+            const int      e    = __builtin_amdgcn_readfirstlane(s_p2p[wave][k]);
+            const int      node = e >> 4;
+            const bool     mine = valid && (((e & 15) >> q) & 1);
+            const int      lidx = a.internalToLeaf[node];
+            const uint32_t s0 = a.layout[lidx], s1 = a.layout[lidx + 1];
+            for (uint32_t c0 = s0; c0 < s1; c0 += kWave)
+            {
+                const uint32_t cnt = min((uint32_t)kWave, s1 - c0);
+                __builtin_amdgcn_wave_barrier();
+                if ((uint32_t)lane < cnt)
+                {
+                    const uint32_t j = c0 + lane;
+                    s_src[wave][lane] = GSrc{a.x[j], a.y[j], a.z[j], a.m[j], a.h[j]};
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+                if (mine)
+                    for (uint32_t s = 0; s < cnt; ++s)
+                    {
+                        const GSrc src = s_src[wave][s];
+                        p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
+                    }
+            }
+        }
+        nP = 0;
+    };
+    // append the entries of the lanes with `want` to a list (ballot compaction)
+    auto append = [&](int* list, int& n, bool want, int entry) {
+        const uint64_t b = __ballot(want);
+        if (want) list[n + __popcll(b & ltMask)] = entry;
+        n += __popcll(b);
+    };
+
+    // root (singleTraversal, traversal.hpp:69-80)
+    {
+        const unsigned v = violates(0, qValid);
+        if (qValid & ~v) { s_m2p[wave][0] = (0 << 4) | (int)(qValid & ~v), nM = 1; }
+        if (v)
+        {
+            if (a.childOffsets[0] == 0) { s_p2p[wave][0] = (int)v, nP = 1; }
+            else { s_stack[wave][0] = (int)v, sp = 1; }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    while (sp > 0)
+    {
+        const int take = min(8, sp);
+        sp -= take;
+        const int  slot = lane >> 3, oct = lane & 7;
+        const bool ok   = slot < take;
+        const int  e    = ok ? s_stack[wave][sp + slot] : 0;
+        __builtin_amdgcn_wave_barrier();
+        const int      parent = e >> 4;
+        const unsigned pmask  = ok ? (unsigned)(e & 15) : 0u;
+        const int      child  = ok ? a.childOffsets[parent] + oct : 0;
+        const unsigned v      = ok ? violates(child, pmask) : 0u;
+        const unsigned accept = pmask & ~v;
+        const bool     leaf   = ok && a.childOffsets[child] == 0;
+        append(s_m2p[wave], nM, accept != 0, (child << 4) | (int)accept);
+        append(s_p2p[wave], nP, v != 0 && leaf, (child << 4) | (int)v);
+        {
+            const bool     push = v != 0 && !leaf;
+            const uint64_t b    = __ballot(push);
+            if (sp + __popcll(b) > kGStack) overflow = true;
+            else
+            {
+                if (push) s_stack[wave][sp + __popcll(b & ltMask)] = (child << 4) | (int)v;
+                sp += __popcll(b);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (overflow) break;
+        if (nM > kGList - kWave) flushM2P();
+        if (nP > kGList - kWave) flushP2P();
+    }
+    flushM2P();
+    flushP2P();
+    if (overflow && lane == 0) atomicOr(a.err, 1u);
+
+    // output: ax += G * acc (computeGravity, traversal_cpu.hpp:218-228), egrav = 0.5 sum G m_i phi_i
+    double u = 0.0;
+    if (valid)
+    {
+        const double G = (double)a.G;
+        u              = (double)(a.G * a.m[i]) * acc[0];
+        a.ax[i]        = (float)((double)a.ax[i] + G * acc[1]);
+        a.ay[i]        = (float)((double)a.ay[i] + G * acc[2]);
+        a.az[i]        = (float)((double)a.az[i] + G * acc[3]);
+    }
+    u = waveSum(u);
+    if (lane == 0 && a.egrav) atomicAdd(a.egrav, 0.5 * u);
+}
+
+inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+} // namespace
+
+hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipStream_t s)
+{
+    if (a.numNodes <= 0) return hipSuccess;
+    leafToNodeKernel<<<grid(a.numNodes), 256, 0, s>>>(a.childOffsets, a.internalToLeaf, a.numNodes, a.leafToNode);
+    leafCentersKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
+        if (e > b) upsweepCentersKernel<<<grid(e - b), 256, 0, s>>>(a, b, e);
+    }
+    setMacKernel<<<grid(a.numNodes), 256, 0, s>>>(a);
+    leafP2MKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
+        if (e > b) upsweepMultipolesKernel<<<grid(e - b), 256, 0, s>>>(a, b, e);
+    }
+    return hipGetLastError();
+}
+
+hipError_t gravityTraverse(const GravArgs& a, hipStream_t s)
+{
+    if (a.last <= a.first) return hipSuccess;
+    const uint32_t waves = (a.last - a.first + kWave - 1) / kWave;
+    gravityTraverseKernel<<<(waves + 3) / 4, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+} // namespace sx

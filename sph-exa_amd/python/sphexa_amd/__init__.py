@@ -29,7 +29,8 @@ class SxParams(C.Structure):
     _fields_ = [("K", C.c_double), ("ng0", C.c_uint32), ("ngmax", C.c_uint32), ("Kcour", C.c_double),
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
-                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32)]
+                ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32),
+                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double)]
 
 
 _P = C.c_void_p
@@ -161,6 +162,9 @@ def lib():
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
         "sx_comm_destroy": (None, [vp]),
         "sx_domain_splitters": (C.c_int, [vp, u32, C.c_int, vp]),
+        "sx_gravity_upsweep": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.c_float, vp, vp]),
+        "sx_gravity_traverse": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxTree),
+                                          C.POINTER(SxBox), vp, vp, C.c_float, C.POINTER(C.c_double)]),
         "sx_domain_halo_layout": (C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -194,14 +198,14 @@ def halo_layout(recv_counts, rank, num_local):
     return off, tuple(int(v) for v in out)
 
 
-def default_params(K=None, ngmax=150, ng0=100, av_clean=False):
+def default_params(K=None, ngmax=150, ng0=100, av_clean=False, g=0.0, theta=0.5):
     """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> in sx_sim."""
     if K is None:
         K = lib().sx_kernel_constant()
     return SxParams(K=K, ng0=ng0, ngmax=ngmax, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0, alphamin=0.05,
                     alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
                     ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
-                    avClean=1 if av_clean else 0)
+                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2)
 
 
 def make_box(lim, bnd):

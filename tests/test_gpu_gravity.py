@@ -1,0 +1,98 @@
+"""Self-gravity on the GPU (sx_gravity_upsweep / sx_gravity_traverse) against the CPU oracle, whose gravity is pinned
+bit-exact to the reference's ryoanji CPU functions (tests/test_oracle_gravity.py).
+
+* expansion centers + MAC radii and quadrupoles: bit-identical (same sequential order per node);
+* accelerations: each target sees the reference's M2P/P2P set (16-target groups, per-quarter MAC), only the double
+  summation order differs: |a - a_ref| <= 1e-6 |a_ref| + 1e-7 max|a|; egrav to 1e-10;
+* golden fixture evrard14 (the reference's own outputs) the same way.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+import gpu_util as gutil
+import pyoracle as po
+import sphexa_amd as sx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sx.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return po.load_oracle()
+
+
+def gpu_gravity(ctx, st, obox, theta=0.5, G=1.0, first=0, last=None):
+    last = st.n if last is None else last
+    box = gutil.box_to_sx(obox)
+    ds = sx.DeviceState(ctx, gutil.host_dict(st))
+    tree, host = gutil.device_tree(ctx, ds.dev["keys"], st.n, 64, box)
+    nn = tree.numNodes
+    cen = ctx.alloc(4 * nn, np.float64)
+    mp = ctx.alloc(8 * nn, np.float32)
+    ctx.check(ctx.L.sx_gravity_upsweep(ctx.h, C.byref(ds.fields), C.byref(tree), theta, cen.ptr, mp.ptr), "upsweep")
+    g = sx.SxGroups(firstBody=first, lastBody=last, numGroups=(last - first + 63) // 64)
+    eg = C.c_double()
+    ctx.check(ctx.L.sx_gravity_traverse(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(tree), C.byref(box), cen.ptr,
+                                        mp.ptr, G, C.byref(eg)), "traverse")
+    out = {k: ds.get(k) for k in ("ax", "ay", "az")}
+    out["centers"] = cen.get().reshape(-1, 4)
+    out["multipoles"] = mp.get().reshape(-1, 8)
+    out["egrav"] = eg.value
+    return out
+
+
+def check_acc(out, ref_arrays):
+    amax = max(np.max(np.abs(ref_arrays[k])) for k in ("ax", "ay", "az"))
+    for k in ("ax", "ay", "az"):
+        a, b = out[k].astype(np.float64), ref_arrays[k].astype(np.float64)
+        assert np.all(np.abs(a - b) <= 1e-6 * np.abs(b) + 1e-7 * amax), (k, np.max(np.abs(a - b)))
+
+
+@pytest.mark.parametrize("side,theta", [(14, 0.5), (21, 0.5), (24, 0.3), (24, 0.9)])
+def test_gravity_vs_oracle(ctx, ora, side, theta):
+    st, box = po.evrard_state(side)
+    gutil.sorted_state(st, box, ora)
+    out = gpu_gravity(ctx, st, box, theta=theta)
+    ref = st.copy()
+    eg, cen, mp = ora.gravity(ref, box, ora.params(g=1.0, theta=theta))
+    assert np.array_equal(out["centers"], cen)
+    assert np.array_equal(out["multipoles"], mp)
+    check_acc(out, ref.arrays)
+    assert out["egrav"] == pytest.approx(eg, rel=1e-10)
+    ctx.free_all()
+
+
+def test_gravity_sub_range(ctx, ora):
+    """targets [first, last) only (a rank's locals among halos): the others keep their acceleration"""
+    st, box = po.evrard_state(18)
+    gutil.sorted_state(st, box, ora)
+    st.ax[:] = 0.25
+    f, l = 100, st.n - 77
+    out = gpu_gravity(ctx, st, box, first=f, last=l)
+    ref = st.copy()
+    ora.gravity(ref, box, ora.params(g=1.0), first=f, last=l)
+    check_acc(out, ref.arrays)
+    assert np.all(out["ax"][:f] == 0.25) and np.all(out["ax"][l:] == 0.25)
+    ctx.free_all()
+
+
+def test_gravity_golden(ctx):
+    d = gu.load("evrard14.npz")
+    box = gu.box_from(d["box"])
+    st = gu.state_from(d, "s0_")
+    out = gpu_gravity(ctx, st, box)
+    assert np.array_equal(out["centers"], d["grav_centers"])
+    assert np.array_equal(out["multipoles"], d["grav_multipoles"])
+    check_acc(out, {k: d["grav_" + k] for k in ("ax", "ay", "az")})
+    assert out["egrav"] == pytest.approx(float(d["grav_egrav"][0]), rel=1e-10)
+    ctx.free_all()
