@@ -302,7 +302,7 @@ size_t sx_sim_size(sx_sim* sim);
 /*! one VE step; the time-step scalars stay on the device (no host sync unless stats are requested) */
 int    sx_sim_step(sx_sim* sim);
 /*! minDt, minDt_m1, ttot, minDtCourant, minDtRho (synchronises) */
-int    sx_sim_scalars(sx_sim* sim, double out[5]);
+int    sx_sim_scalars(sx_sim* sim, double out[6]);
 /*! per-stage device time of the last step (ms) measured with HIP events, names in stage order */
 int    sx_sim_stage_times(sx_sim* sim, float* ms, int cap, const char** names);
 int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);

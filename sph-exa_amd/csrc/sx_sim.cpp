@@ -34,6 +34,7 @@
 
 #include "../../include/sphexa_hip.h"
 #include "sx_comm.hpp"
+#include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
@@ -76,7 +77,25 @@ struct Scalars
     double   dtCand;   // rank-local candidate, globally min-reduced
     float    courant;  // atomic-min target of the momentum kernel
     unsigned maxDivvU; // order-preserving image of max divv
+    double   egrav;    // gravitational potential energy (ParticlesData::egrav)
+    unsigned long long maxAccSqBits; // max |a|^2 of the locals (bit image of a non-negative double)
+    unsigned gravErr;
 };
+
+//! max |a|^2 over [first, last) for accelerationTimestep (ts_global.hpp:47-67)
+__global__ void maxAccSqKernel(const float* ax, const float* ay, const float* az, size_t first, size_t last,
+                               unsigned long long* out)
+{
+    size_t i = first + blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    double v = 0.0;
+    if (i < last)
+    {
+        double x = ax[i], y = ay[i], z = az[i];
+        v        = x * x + (y * y + z * z);
+    }
+    v = waveMax(v);
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(v));
+}
 
 //! particle record of the SFC exchange (conserved fields of the VE propagator, ve_hydro.hpp:74)
 struct __attribute__((aligned(16))) PRec
@@ -98,16 +117,18 @@ struct __attribute__((aligned(16))) ReqBox
 // ---- time step --------------------------------------------------------------------------------------------
 
 //! rhoTimestep (ts_global.hpp:72-94) and the rank-local part of computeTimestep (:97-112)
-__global__ void dtCandidateKernel(Scalars* s, double Krho, double maxDtIncrease)
+__global__ void dtCandidateKernel(Scalars* s, double Krho, double maxDtIncrease, double g, double eps, double etaAcc)
 {
     unsigned u = s->maxDivvU;
     u          = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
     float maxDivv   = __uint_as_float(u);
     s->minDtRho     = Krho / (double)fabsf(maxDivv);
     s->minDtCourant = (double)s->courant;
-    double m        = INFINITY;
-    double cand[3]  = {s->minDtCourant, s->minDtRho, maxDtIncrease * s->minDt};
-    for (int k = 0; k < 3; ++k)
+    double minDtAcc = INFINITY;
+    if (g != 0.0) minDtAcc = etaAcc * sqrt(eps / sqrt(__longlong_as_double((long long)s->maxAccSqBits)));
+    double m       = INFINITY;
+    double cand[4] = {minDtAcc, s->minDtCourant, s->minDtRho, maxDtIncrease * s->minDt};
+    for (int k = 0; k < 4; ++k)
         m = cand[k] < m ? cand[k] : m;
     s->dtCand = m;
 }
@@ -123,8 +144,11 @@ __global__ void dtApplyKernel(Scalars* s)
 
 __global__ void resetScalarsKernel(Scalars* s)
 {
-    s->courant  = 1e10f;
-    s->maxDivvU = 0;
+    s->courant      = 1e10f;
+    s->maxDivvU     = 0;
+    s->egrav        = 0.0;
+    s->maxAccSqBits = 0;
+    s->gravErr      = 0;
 }
 
 // ---- initial conditions -----------------------------------------------------------------------------------
@@ -781,20 +805,21 @@ extern "C"
             delete s;
             return SX_ERR_NOMEM;
         }
-        const char* names[] = {"sync",       "FindNeighbors", "XMass",      "VeDefGradh",     "EOS",
-                               "IadDivvCurlv", "AVswitches",  "MomentumEnergy", "UpdateQuantities"};
+        const char* names[] = {"sync",         "FindNeighbors", "XMass",          "VeDefGradh", "EOS",
+                               "IadDivvCurlv", "AVswitches",    "MomentumEnergy", "Gravity",    "UpdateQuantities"};
         s->stageNames.assign(std::begin(names), std::end(names));
         s->ev.resize(s->stageNames.size() + 1);
         for (auto& e : s->ev)
             (void)hipEventCreate(&e);
         s->stageMs.assign(s->stageNames.size(), 0.f);
-        const char* knames[] = {"findNeighbors", "xmass", "veDefGradh", "iadDivvCurlv", "avSwitches", "momentumEnergy"};
+        const char* knames[] = {"findNeighbors", "xmass",          "veDefGradh", "iadDivvCurlv",
+                                "avSwitches",    "momentumEnergy", "gravity"};
         s->kernelNames.assign(std::begin(knames), std::end(knames));
         s->kev.resize(2 * s->kernelNames.size());
         for (auto& e : s->kev)
             (void)hipEventCreate(&e);
         s->kernelMs.assign(s->kernelNames.size(), 0.f);
-        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
+        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
         return SX_OK;
@@ -847,7 +872,7 @@ extern "C"
             sedovInitKernel<<<grid(n), 256, 0, st>>>(side, f, n, s->x, s->y, s->z, s->h, s->m, s->temp, s->vx, s->vy,
                                                      s->vz, s->xm1, s->ym1, s->zm1, s->dum1, s->alpha, s->id,
                                                      (float)hInit, (float)(1.0 / N), ener0, width * width, 1e-8, cv);
-        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
+        Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         SIM_HIP(hipMemcpyAsync(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice, st));
         SIM_HIP(hipStreamSynchronize(st));
         return SX_OK;
@@ -1070,8 +1095,39 @@ extern "C"
         H.momentumEnergy(pa, st);
         SIM_HIP(hipEventRecord(s->kev[11], st));
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
+        // ---- self-gravity (ve_hydro.hpp:193-202): upsweep + traversal on the step's tree, added to ax, ay, az
+        SIM_HIP(hipEventRecord(s->kev[12], st));
+        if (s->p.g != 0.0)
+        {
+            if (dist) return SX_ERR_ARG; // multi-rank gravity needs the global multipole exchange
+            GravArgs ga{};
+            ga.first          = (uint32_t)s->first;
+            ga.last           = (uint32_t)s->last;
+            ga.numLeaves      = s->tree.numLeaves;
+            ga.numNodes       = s->tree.numNodes;
+            ga.childOffsets   = s->tree.childOffsets;
+            ga.internalToLeaf = s->tree.internalToLeaf;
+            ga.layout         = s->tree.layout;
+            ga.geoCenters     = s->tree.centers;
+            ga.geoSizes       = s->tree.sizes;
+            ga.leafToNode     = s->work.get<int32_t>("grav.leafToNode", (size_t)s->tree.numLeaves);
+            ga.x = s->x, ga.y = s->y, ga.z = s->z, ga.m = s->m, ga.h = s->h;
+            ga.centers4   = s->work.get<double>("grav.centers", 4 * (size_t)s->tree.numNodes);
+            ga.multipoles = s->work.get<float>("grav.multipoles", 8 * (size_t)s->tree.numNodes);
+            ga.G          = (float)s->p.g;
+            ga.invTheta   = 1.0f / s->p.theta;
+            ga.ax = s->ax, ga.ay = s->ay, ga.az = s->az;
+            ga.egrav = &s->sc->egrav;
+            ga.err   = &s->sc->gravErr;
+            SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
+            SIM_HIP(gravityTraverse(ga, st));
+            const size_t nl = s->last - s->first;
+            if (nl) maxAccSqKernel<<<grid(nl), 256, 0, st>>>(s->ax, s->ay, s->az, s->first, s->last, &s->sc->maxAccSqBits);
+        }
+        SIM_HIP(hipEventRecord(s->kev[13], st));
+        SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- integrate: global time-step, positions, h
-        dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease);
+        dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease, s->p.g, s->p.eps, s->p.etaAcc);
         if (dist) SIM_COMM(s->comm->allreduceMinF64(&s->sc->dtCand, 1, st));
         dtApplyKernel<<<1, 1, 0, st>>>(s->sc);
         PosArgs qa{};
@@ -1123,10 +1179,15 @@ extern "C"
         }
 #endif
         if (s->statsHost[0] & 1u) return SX_ERR_TRAVERSAL;
+        if (s->p.g != 0.0)
+        {
+            SIM_HIP(hipMemcpy(s->scHost, s->sc, sizeof(Scalars), hipMemcpyDeviceToHost));
+            if (s->scHost->gravErr) return SX_ERR_TRAVERSAL; // Barnes-Hut stack exhausted
+        }
         return SX_OK;
     }
 
-    int sx_sim_scalars(sx_sim* s, double out[5])
+    int sx_sim_scalars(sx_sim* s, double out[6])
     {
         hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
         SIM_HIP(hipMemcpyAsync(s->scHost, s->sc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -1136,6 +1197,7 @@ extern "C"
         out[2] = s->scHost->ttot;
         out[3] = s->scHost->minDtCourant;
         out[4] = s->scHost->minDtRho;
+        out[5] = s->scHost->egrav;
         return SX_OK;
     }
 

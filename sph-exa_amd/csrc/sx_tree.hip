@@ -464,7 +464,8 @@ hipError_t buildTree(Arena& arena, const uint64_t* keys, size_t n, uint32_t buck
     t.reserve(arena);
 
     // levelRange (getLevelRangeCpu): first node of each level, then numNodes
-    std::vector<int32_t> lr(kMaxLevel + 2, numNodes);
+    std::vector<int32_t>& lr = t.levelRangeHost;
+    lr.assign(kMaxLevel + 2, numNodes);
     for (size_t l = 0; l < levelStart.size() && l <= (size_t)kMaxLevel; ++l)
         lr[l] = levelStart[l];
     lr[kMaxLevel + 1] = numNodes;

@@ -96,6 +96,7 @@ struct DevTree
     int32_t*  leafToInternal{nullptr};
     double*   centers{nullptr};
     double*   sizes{nullptr};
+    std::vector<int32_t> levelRangeHost; // host copy of levelRange (per-level upsweep launches)
 
     int  parentsSize() const { return std::max(1, (numNodes - 1) / 8); }
     void reserve(Arena& a)

@@ -425,9 +425,9 @@ class Sim:
         return self.L.sx_sim_size(self.h)
 
     def scalars(self):
-        out = (C.c_double * 5)()
+        out = (C.c_double * 6)()
         self.ctx.check(self.L.sx_sim_scalars(self.h, out), "scalars")
-        return dict(zip(["minDt", "minDt_m1", "ttot", "minDtCourant", "minDtRho"], list(out)))
+        return dict(zip(["minDt", "minDt_m1", "ttot", "minDtCourant", "minDtRho", "egrav"], list(out)))
 
     def fields(self):
         f = SxFields()
