@@ -3,7 +3,8 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--side S] [--no-cpu-baseline]
 
 A step is one full HydroVeProp step (ve_hydro.hpp:132-218): sync (keys, sort, reorder, tree), neighbor search with
-h iteration, XMass, VeDefGradh, EOS, IAD+divv/curlv, AV switches, momentum/energy, time-step, positions, h update.
+h iteration, XMass, VeDefGradh, EOS, IAD+divv/curlv, AV switches, momentum/energy, [self-gravity], time-step,
+positions, h update.  --init noh|evrard run BASELINE configs 3 and 5 (lattice substitutes for the glass block).
 Inputs are generated and kept in HBM; nothing leaves the device inside the timed region except the per-step
 4-byte tree-level counts and stats.  Weak scaling: side = round(200 * N^(1/3)) particles^(1/3) in total
 (N=1: Sedov -n 200 = BASELINE config 2; N=8: Sedov -n 400 = config 4).
@@ -61,6 +62,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="rccl", help="rccl (one GPU per rank) or host (staged, tests)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--init", default="sedov", choices=["sedov", "noh", "evrard"],
+                    help="sedov (BASELINE metric, device IC), noh (config 3), evrard (config 5: VE + self-gravity)")
+    ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
     return ap.parse_args()
 
 
@@ -107,18 +111,32 @@ def main():
 
     import sphexa_amd as sx
 
-    side = args.side or int(round(200 * n_gpus ** (1.0 / 3.0)))
+    default_side = {"sedov": 200, "noh": 300, "evrard": 300}[args.init]
+    side = args.side or int(round(default_side * n_gpus ** (1.0 / 3.0)))
     n_total = side ** 3
+    ic_arrays = None
+    if args.init != "sedov":
+        from sphexa_amd import ic
+
+        ic_arrays, lim, bnd, dt0 = getattr(ic, args.init)(side)
+        n_total = ic_arrays["x"].size
+        if args.init == "evrard" and world > 1:
+            raise SystemExit("evrard (self-gravity) runs on one GPU: multi-rank gravity needs the global multipole "
+                             "exchange (DESIGN.md 9)")
     device = 0
     if args.backend != "host":
         import torch  # device_count() does not initialise the GPU runtime
 
         device = local % max(1, torch.cuda.device_count())
     ctx = sx.Context(device, exact=args.exact)
-    box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
+    if ic_arrays is None:
+        box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
+    else:
+        box = sx.make_box(lim, bnd)
     # capacity: the rank's share plus halos (surface layer of the SFC domain) with headroom
     cap = n_total if world == 1 else int(1.6 * n_total / world) + 65536
-    sim = sx.Sim(ctx, cap, box, bucket=args.bucket)
+    params = sx.default_params(av_clean=args.av_clean, g=1.0 if args.init == "evrard" else 0.0)
+    sim = sx.Sim(ctx, cap, box, params=params, bucket=args.bucket)
     comm = None
     transport = args.backend
     if world > 1:
@@ -138,7 +156,11 @@ def main():
             comm = sx.Comm("host")
             transport = f"host (fallback: {args.backend} communicator creation failed)"
         sim.set_comm(comm)
-    sim.init_sedov(side, rank, world)
+    if ic_arrays is None:
+        sim.init_sedov(side, rank, world)
+    else:
+        f, l = n_total * rank // world, n_total * (rank + 1) // world  # index slab; the first sync redistributes
+        sim.set_state({k: v[f:l] for k, v in ic_arrays.items()}, dt0, dt0)
     for _ in range(args.warmup):
         sim.step()
 
@@ -188,8 +210,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 hydro / f64 coordinates (sph::SphTypes)",
-        "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint",
-        "config": {"workload": f"Sedov -n {side} ({side ** 3} particles), VE propagator, {args.steps} steps",
+        "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint" if ic_arrays is None
+                else f"synthetic {args.init} lattice substitute for the glass block (SURVEY F6), sphexa_amd/ic.py",
+        "config": {"workload": f"{args.init.capitalize()} -n {side} ({n_total} particles), VE propagator"
+                               f"{' + self-gravity' if args.init == 'evrard' else ''}"
+                               f"{' + AV cleaning' if args.av_clean else ''}, {args.steps} steps",
                    "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
                    "parallelism": "1 GPU" if world == 1 else
                    f"{world} GPUs: SFC domain decomposition, halo + particle exchange over {transport}",

@@ -7,7 +7,7 @@
  *
  * Per cluster (workgroup):
  *   1. wave + LDS reductions give the cluster's bounding box and max h;
- *   2. wave 0 collects every leaf whose geometric box comes within 2*hmax of the cluster box (waveCollectLeaves,
+ *   2. wave 0 collects every leaf whose geometric box comes within 2*hmax_w of some wave's box (waveCollectLeaves,
  *      sx_traverse.hpp; minimum image on periodic axes, inflated by the key-quantisation margin) and numbers the
  *      particles of those leaves consecutively: the cluster's CANDIDATE SPACE (leaf cc's particles start at
  *      s_cOff[cc]);
@@ -39,6 +39,8 @@ namespace sx
 constexpr int kNsGroup = SX_NS_GROUP;
 
 constexpr int kCandSpace = 1 << 16; //!< candidate particles per cluster (u16 list entries)
+constexpr int kSubGroups  = kCluster / 16; //!< 16-particle sub-groups per cluster
+constexpr int kMaxRegions = 128;           //!< search regions per cluster (boxes or particle spheres)
 constexpr int kCandWords = kCandSpace / 32;
 
 __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t* pre, uint32_t idx)
@@ -106,14 +108,16 @@ findNeighborsKernel(NsArgs a)
     __shared__ uint8_t  s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
     __shared__ uint32_t s_bits[kCandWords];
     __shared__ uint32_t s_pre[kCandWords];
-    __shared__ double   s_box[kClusterWaves][6];
-    __shared__ float    s_hmax[kClusterWaves];
+    __shared__ int      s_nreg;
     __shared__ int      s_again[kClusterWaves];
     __shared__ uint32_t s_wsum[kClusterWaves];
     __shared__ float4   s_chunk[kClusterWaves][2][kWave]; // per wave: double-buffered leaf-frame pair records
     __shared__ int      s_numCand;
     // leaf frames of the first kDCap candidate leaves; s_pre is only used after the last stream
     float4* const s_d = reinterpret_cast<float4*>(s_pre);
+    // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}; s_chunk is only used inside the stream
+    double4* const s_reg = reinterpret_cast<double4*>(&s_chunk[0][0][0]);
+    static_assert(sizeof(s_chunk) >= 2 * kMaxRegions * sizeof(double4), "search regions alias s_chunk");
 
     const int      wave  = threadIdx.x >> 6;
     const int      lane  = threadIdx.x & 63;
@@ -139,29 +143,10 @@ findNeighborsKernel(NsArgs a)
     unsigned           stored     = 0;
     unsigned long long candTested = 0;
 
-    // cluster bounding box (positions do not change between iterations)
-    {
-        const double wx0 = waveMin(xi), wx1 = waveMax(xi);
-        const double wy0 = waveMin(yi), wy1 = waveMax(yi);
-        const double wz0 = waveMin(zi), wz1 = waveMax(zi);
-        if (lane == 0)
-        {
-            s_box[wave][0] = wx0, s_box[wave][1] = wx1, s_box[wave][2] = wy0;
-            s_box[wave][3] = wy1, s_box[wave][4] = wz0, s_box[wave][5] = wz1;
-        }
-    }
-    __syncthreads();
-    double bx0 = s_box[0][0], bx1 = s_box[0][1], by0 = s_box[0][2], by1 = s_box[0][3], bz0 = s_box[0][4],
-           bz1 = s_box[0][5];
-    for (int w = 1; w < kClusterWaves; ++w)
-    {
-        bx0 = fmin(bx0, s_box[w][0]), bx1 = fmax(bx1, s_box[w][1]);
-        by0 = fmin(by0, s_box[w][2]), by1 = fmax(by1, s_box[w][3]);
-        bz0 = fmin(bz0, s_box[w][4]), bz1 = fmax(bz1, s_box[w][5]);
-    }
-    const double gcx = 0.5 * (bx0 + bx1), gcy = 0.5 * (by0 + by1), gcz = 0.5 * (bz0 + bz1);
-    const double gsx = 0.5 * (bx1 - bx0), gsy = 0.5 * (by1 - by0), gsz = 0.5 * (bz1 - bz0);
-
+    // search regions.  An SFC range can jump across empty space (the curve leaves and re-enters a sphere's
+    // surface), so a cluster or wave box may span a gap; regions are therefore the boxes of the 16 sub-groups of
+    // 16 consecutive particles, and a sub-group whose box is wider than 8 of its search radii (it straddles such a
+    // jump) is replaced by the spheres of its particles.  Positions do not change over the h iteration.
     int numCand = 0;
 #ifdef SX_NS_PROFILE
     uint64_t prof[6] = {0, 0, 0, 0, 0, 0}; // cycles: candidates+scan, stream, tests, post-test, union; chunks
@@ -171,25 +156,86 @@ findNeighborsKernel(NsArgs a)
 #ifdef SX_NS_PROFILE
         const uint64_t tB = __builtin_readcyclecounter();
 #endif
-        // ---- 2. candidate leaves for radius 2*hmax of the cluster, numbered into the candidate space -----
-        const float hmaxW = waveMax(valid ? hi : 0.0f);
-        if (lane == 0) s_hmax[wave] = hmaxW;
+        // ---- 2. candidate leaves within reach of some search region, numbered into the candidate space ----
+        if (threadIdx.x == 0) s_nreg = 0;
         __syncthreads();
-        float hmax = s_hmax[0];
-        for (int w = 1; w < kClusterWaves; ++w)
-            hmax = fmaxf(hmax, s_hmax[w]);
+        {
+            // regions: the wave box when it is coherent (no wider than 8 search radii), else its coherent 16-particle
+            // sub-group boxes and, for incoherent sub-groups, the spheres of their particles (all in registers:
+            // 16-lane then 64-lane shuffles over the valid lanes)
+            double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
+            double hb[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
+            float  hq    = valid ? hi : 0.0f;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1)
+            {
+                for (int d = 0; d < 3; ++d)
+                {
+                    lo[d] = fmin(lo[d], __shfl_xor(lo[d], o, 16));
+                    hb[d] = fmax(hb[d], __shfl_xor(hb[d], o, 16));
+                }
+                hq = fmaxf(hq, __shfl_xor(hq, o, 16));
+            }
+            double wl[3] = {lo[0], lo[1], lo[2]}, wh[3] = {hb[0], hb[1], hb[2]};
+            float  hw    = hq;
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1)
+            {
+                for (int d = 0; d < 3; ++d)
+                {
+                    wl[d] = fmin(wl[d], __shfl_xor(wl[d], o, 64));
+                    wh[d] = fmax(wh[d], __shfl_xor(wh[d], o, 64));
+                }
+                hw = fmaxf(hw, __shfl_xor(hw, o, 64));
+            }
+            auto addRegion = [&](double x0, double x1, double y0, double y1, double z0, double z1, float h) {
+                const int k = atomicAdd(&s_nreg, 1);
+                if (k < kMaxRegions)
+                {
+                    s_reg[2 * k]     = make_double4(0.5 * (x0 + x1), 0.5 * (y0 + y1), 0.5 * (z0 + z1),
+                                                2.0 * (double)h * (1.0 + 1e-6) + a.margin);
+                    s_reg[2 * k + 1] = make_double4(0.5 * (x1 - x0), 0.5 * (y1 - y0), 0.5 * (z1 - z0), (double)wave);
+                }
+            };
+            const double extW = fmax(wh[0] - wl[0], fmax(wh[1] - wl[1], wh[2] - wl[2]));
+            if (extW <= 16.0 * (double)hw)
+            {
+                if (lane == 0 && hw > 0.0f) addRegion(wl[0], wh[0], wl[1], wh[1], wl[2], wh[2], hw);
+            }
+            else
+            {
+                const double ext = fmax(hb[0] - lo[0], fmax(hb[1] - lo[1], hb[2] - lo[2]));
+                if (ext <= 16.0 * (double)hq)
+                {
+                    if ((lane & 15) == 0 && hq > 0.0f) addRegion(lo[0], hb[0], lo[1], hb[1], lo[2], hb[2], hq);
+                }
+                else if (valid) addRegion(xi, xi, yi, yi, zi, zi, hi);
+            }
+        }
+        __syncthreads();
+        const int nreg = min(s_nreg, kMaxRegions);
+        // waves whose regions reach node (bit w)
+        auto reachMask = [&](int node, bool any) -> unsigned {
+            const double* nc_  = a.centers + 3 * (size_t)node;
+            const double* ns_  = a.sizes + 3 * (size_t)node;
+            unsigned      bits = 0;
+            for (int k = 0; k < nreg; ++k)
+            {
+                const double4 rc = s_reg[2 * k], rh = s_reg[2 * k + 1];
+                if (boxDist2(nc_, ns_, rc.x, rc.y, rc.z, rh.x, rh.y, rh.z, a.box) < rc.w * rc.w)
+                {
+                    bits |= 1u << (int)rh.w;
+                    if (any) break;
+                }
+            }
+            return bits;
+        };
         if (wave == 0)
         {
-            const double R  = 2.0 * (double)hmax * (1.0 + 1e-6) + a.margin;
-            const double R2 = R * R;
-            bool         overflow;
-            const int    nCand = waveCollectLeaves(
-                a.childOffsets,
-                [&](int node) {
-                    return boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node, gcx, gcy, gcz, gsx, gsy,
-                                    gsz, a.box) < R2;
-                },
-                s_queue, s_cand, lane, overflow);
+            bool      overflow;
+            const int nCand = waveCollectLeaves(
+                a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, lane, overflow);
+            if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short
             // exclusive scan of the candidate leaf sizes
             uint32_t run = 0;
             for (int b = 0; b < nCand; b += kWave)
@@ -215,9 +261,14 @@ findNeighborsKernel(NsArgs a)
             if (lane == 0)
             {
                 s_cOff[nCand] = run;
-                if (local && run > (uint32_t)kCandSpace) overflow = true;
-                if (overflow) atomicOr(&a.stats[0], 1u);
-                s_numCand = overflow ? 0 : nCand;
+                // error bits: 2 = traversal queue / candidate-leaf list full, 4 = candidate space beyond u16
+                const unsigned f = (overflow ? 2u : 0u) | ((local && run > (uint32_t)kCandSpace) ? 4u : 0u);
+                if (f) atomicOr(&a.stats[0], 1u | f);
+#ifdef SX_NS_DEBUG
+                if (f && atomicAdd(&a.stats[3], 1u) < 8)
+                    printf("ns overflow: cluster %u flags %u nCand %d run %u regions %d\n", c, f, nCand, run, s_nreg);
+#endif
+                s_numCand = f ? 0 : nCand;
             }
         }
         __syncthreads();
@@ -227,19 +278,7 @@ findNeighborsKernel(NsArgs a)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
         {
             const int node = s_cand[cc];
-            uint32_t  bits = 0;
-            for (int w = 0; w < kClusterWaves; ++w)
-            {
-                const float hw = s_hmax[w];
-                if (hw <= 0.0f) continue; // no valid lane
-                const double R  = 2.0 * (double)hw * (1.0 + 1e-6) + a.margin;
-                const double d2 = boxDist2(a.centers + 3 * (size_t)node, a.sizes + 3 * (size_t)node,
-                                           0.5 * (s_box[w][0] + s_box[w][1]), 0.5 * (s_box[w][2] + s_box[w][3]),
-                                           0.5 * (s_box[w][4] + s_box[w][5]), 0.5 * (s_box[w][1] - s_box[w][0]),
-                                           0.5 * (s_box[w][3] - s_box[w][2]), 0.5 * (s_box[w][5] - s_box[w][4]), a.box);
-                if (d2 < R * R) bits |= 1u << w;
-            }
-            s_reach[cc] = (uint8_t)bits;
+            s_reach[cc]    = (uint8_t)reachMask(node, false);
             if (cc < kDCap && a.qrel) s_d[cc] = leafFrame(a, node, s_p0[cc], ox, oy, oz);
         }
         if (local)
@@ -597,7 +636,7 @@ findNeighborsKernel(NsArgs a)
                 while (s_cOff[cc + 1] <= idx)
                     ++cc;
                 if (run < a.ucap) uni[run] = s_p0[cc] + (idx - s_cOff[cc]);
-                else atomicOr(&a.stats[0], 1u); // union larger than its capacity: reported as a traversal error
+                else atomicOr(&a.stats[0], 1u | 8u); // union larger than its capacity (bit 8)
                 ++run;
             }
         }

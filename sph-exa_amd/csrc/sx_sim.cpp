@@ -1178,11 +1178,20 @@ extern "C"
                     100.0 * (pr[5] >> 32) / std::max(1.0, (double)(pr[5] & 0xffffffffu)));
         }
 #endif
-        if (s->statsHost[0] & 1u) return SX_ERR_TRAVERSAL;
+        if (s->statsHost[0] & 1u)
+        {
+            fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 queue/candidate leaves, "
+                            "4 candidate space, 8 union)\n", s->statsHost[0]);
+            return SX_ERR_TRAVERSAL;
+        }
         if (s->p.g != 0.0)
         {
             SIM_HIP(hipMemcpy(s->scHost, s->sc, sizeof(Scalars), hipMemcpyDeviceToHost));
-            if (s->scHost->gravErr) return SX_ERR_TRAVERSAL; // Barnes-Hut stack exhausted
+            if (s->scHost->gravErr)
+            {
+                fprintf(stderr, "sx_sim_step: GPU traversal stack exhausted in Barnes-Hut\n");
+                return SX_ERR_TRAVERSAL;
+            }
         }
         return SX_OK;
     }
