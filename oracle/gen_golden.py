@@ -15,7 +15,11 @@ Fixtures
   evrard14.npz   Evrard substitute n=14 (1472 particles, key-sorted): gravity alone (expansion centers + MAC
                  radii, quadrupoles, accelerations, egrav; G = 1, theta = 0.5) and 2 full VE steps with gravity
 
-    python oracle/gen_golden.py [--only gravity]
+  std_sedov10.npz, std_noh12.npz  std propagator (HydroProp, std_hydro.hpp:124-184): IC and states after 3 steps
+  std_kernels.npz  Sedov n=12 after 2 std steps + neighbor list and the outputs of density, EOS_HydroStd, IAD,
+                   momentumEnergySTD (the reference's std *Impl loops)
+
+    python oracle/gen_golden.py [--only gravity|std]
 """
 import os
 import sys
@@ -69,13 +73,54 @@ def gravity_fixture(ref):
     np.savez_compressed(os.path.join(OUT, "evrard14.npz"), **out)
 
 
+def std_fixture(ref):
+    """std propagator (HydroProp): 3 steps of Sedov n=10 and Noh n=12, and each std kernel on a Sedov n=12 state"""
+    p = ref.params(std=True)
+    for ic, side, name in [(po.sedov_state, 10, "sedov"), (po.noh_state, 12, "noh")]:
+        st, box = ic(side)
+        out = {"box": box_arr(box)}
+        out.update(snapshot(st, "s0_"))
+        for s in range(1, 4):
+            ref.step(st, box, params=p)
+            out.update(snapshot(st, f"s{s}_"))
+        out_name = f"std_{name}{side}.npz"
+        np.savez_compressed(os.path.join(OUT, out_name), **out)
+    st, box = po.sedov_state(12)
+    ref.step(st, box, params=p)
+    ref.step(st, box, params=p)
+    ref.sfc_keys(st, box)
+    order = np.argsort(st.keys, kind="stable")
+    for k in po.CONSERVED + ["keys"]:
+        st.arrays[k][:] = st.arrays[k][order]
+    pre = st.copy()
+    nbr, nc = ref.find_neighbors(st, box, iterate_h=True)
+    st.nc[:] = nc
+    out = {"box": box_arr(box), "nbr": nbr, "nc": nc}
+    out.update(snapshot(pre, "in_"))
+    ref.density(st, box, nbr, params=p)
+    out["rho"] = st.rho.copy()
+    ref.eos_std(st, params=p)
+    out["p"], out["c"] = st.p.copy(), st.c.copy()
+    ref.iad_std(st, box, nbr, params=p)
+    for k in ["c11", "c12", "c13", "c22", "c23", "c33"]:
+        out[k] = st.arrays[k].copy()
+    out["minDtCourant"] = np.array([ref.momentum_energy_std(st, box, nbr, params=p)])
+    for k in ["du", "ax", "ay", "az"]:
+        out[k] = st.arrays[k].copy()
+    np.savez_compressed(os.path.join(OUT, "std_kernels.npz"), **out)
+
+
 def main():
     ref = po.load_ref()
     if ref is None:
         raise SystemExit("oracle/_ref/libsphexa_ref.so missing: run `make -C oracle` where /root/reference exists")
     os.makedirs(OUT, exist_ok=True)
-    gravity_fixture(ref)
-    if "--only" in sys.argv:
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only in (None, "std"):
+        std_fixture(ref)
+    if only in (None, "gravity"):
+        gravity_fixture(ref)
+    if only is not None:
         return
 
     st, box = po.sedov_state(10)

@@ -32,7 +32,7 @@ class OxParams(C.Structure):
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
                 ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32),
-                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double)]
+                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double), ("prop", C.c_int32)]
 
 
 STATE_FIELDS = [
@@ -47,7 +47,7 @@ STATE_FIELDS = [
     ("c11", np.float32), ("c12", np.float32), ("c13", np.float32), ("c22", np.float32), ("c23", np.float32),
     ("c33", np.float32), ("nc", np.uint32), ("keys", np.uint64),
     ("dV11", np.float32), ("dV12", np.float32), ("dV13", np.float32), ("dV22", np.float32), ("dV23", np.float32),
-    ("dV33", np.float32),
+    ("dV33", np.float32), ("rho", np.float32), ("p", np.float32),
 ]
 CONSERVED = ["x", "y", "z", "x_m1", "y_m1", "z_m1", "vx", "vy", "vz", "temp", "h", "m", "alpha", "du_m1", "id"]
 
@@ -60,13 +60,14 @@ class OxState(C.Structure):
         ("minDtRho", C.c_double), ("egrav", C.c_double)]
 
 
-def default_params(K, av_clean=False, g=0.0, theta=0.5):
+def default_params(K, av_clean=False, g=0.0, theta=0.5, std=False):
     """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true>; g != 0 turns on
-    self-gravity with opening parameter theta (sphexa.cpp:127)."""
+    self-gravity with opening parameter theta (sphexa.cpp:127); std selects the std propagator (HydroProp)."""
     return OxParams(K=K, ng0=100, ngmax=150, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0,
                     alphamin=0.05, alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
                     ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
-                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2)
+                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2,
+                    prop=1 if std else 0)
 
 
 def make_box(lo=-0.5, hi=0.5, periodic=True):
@@ -252,6 +253,11 @@ def _bind(lib):
                                C.c_uint]),
         ("momentum_energy", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p,
                                           C.c_uint, C.c_uint]),
+        ("density", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint, C.c_uint]),
+        ("eos_std", None, [C.POINTER(OxState), C.POINTER(OxParams), C.c_uint, C.c_uint]),
+        ("iad_std", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p, C.c_uint, C.c_uint]),
+        ("momentum_energy_std", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), u32p,
+                                              C.c_uint, C.c_uint]),
         ("positions", None, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint, C.c_uint]),
         ("update_h_range", None, [C.POINTER(OxState), C.c_uint, C.c_uint, C.c_uint]),
         ("step", C.c_int, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint]),
@@ -281,8 +287,8 @@ class Lib:
                                C.byref(K))
         self.wh, self.whd, self.K = wh, whd, K.value
 
-    def params(self, av_clean=False, g=0.0, theta=0.5):
-        return default_params(self.K, av_clean, g, theta)
+    def params(self, av_clean=False, g=0.0, theta=0.5, std=False):
+        return default_params(self.K, av_clean, g, theta, std)
 
     def sfc_keys(self, st, box):
         self.lib.sfc_keys(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.n, C.byref(box),
@@ -346,6 +352,20 @@ class Lib:
 
     def momentum_energy(self, st, box, nbr, first=0, last=None, params=None):
         return self._kern("momentum_energy", st, box, nbr, first, st.n if last is None else last, params)
+
+    def density(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("density", st, box, nbr, first, st.n if last is None else last, params)
+
+    def iad_std(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("iad_std", st, box, nbr, first, st.n if last is None else last, params)
+
+    def momentum_energy_std(self, st, box, nbr, first=0, last=None, params=None):
+        return self._kern("momentum_energy_std", st, box, nbr, first, st.n if last is None else last, params)
+
+    def eos_std(self, st, first=0, last=None, params=None):
+        p = params or self.params()
+        s = st.struct()
+        self.lib.eos_std(C.byref(s), C.byref(p), first, st.n if last is None else last)
 
     def eos(self, st, first=0, last=None, params=None):
         p = params or self.params()

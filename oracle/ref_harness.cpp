@@ -50,6 +50,10 @@
 #include "sph/hydro_ve/momentum_energy.hpp"
 #include "sph/hydro_ve/ve_def_gradh.hpp"
 #include "sph/hydro_ve/xmass.hpp"
+#include "sph/hydro_std/density.hpp"
+#include "sph/hydro_std/eos.hpp"
+#include "sph/hydro_std/iad.hpp"
+#include "sph/hydro_std/momentum_energy.hpp"
 #include "sph/positions.hpp"
 #include "sph/sph_kernel_tables.hpp"
 #include "sph/update_h.hpp"
@@ -78,6 +82,14 @@ struct PtrVec
     T&     operator[](size_t i) const { return p[i]; }
 };
 
+//! found by ADL for computeDensityImpl's unqualified swap(d.xm, d.rho) (hydro_std/density.hpp:44-46)
+template<class T>
+void swap(PtrVec<T>& a, PtrVec<T>& b)
+{
+    std::swap(a.p, b.p);
+    std::swap(a.n, b.n);
+}
+
 //! @brief by-value element access: makes updateTempHost's `decltype(d.du[0])` a value type (F2 fix)
 template<class T>
 struct ValVec
@@ -94,9 +106,10 @@ struct ValVec
 template<class T>
 struct MockData
 {
-    using RealType  = double;
-    using HydroType = T;
-    using Tm        = T;
+    using RealType        = double;
+    using HydroType       = T;
+    using Tm              = T;
+    using AcceleratorType = cstone::CpuTag; // computeDensityImpl dispatches computeXMass on it (density.hpp:45)
 
     unsigned ng0{100}, ngmax{150};
     double   K{0};
@@ -224,6 +237,13 @@ void bindState(MockData<T>& d, ox_state* s, const ox_params* p)
     d.c23    = {s->c23, n};
     d.c33    = {s->c33, n};
     d.nc     = {s->nc, n};
+    if (p && p->prop == 1)
+    {
+        // rho, p are HydroProp DependentFields (std_hydro.hpp:78-79); HydroVeProp leaves them unallocated, which
+        // keeps computeEOS_Impl from writing them (hydro_ve/eos.hpp)
+        d.rho = {s->rho, n};
+        d.p   = {s->p, n};
+    }
     if (p && p->avClean)
     {
         // GradVFields acquired (ve_hydro.hpp:80-85): dV11.size() == x.size() turns on doGradV
@@ -422,6 +442,38 @@ extern "C"
         return d.minDtCourant;
     }
 
+    // ---- std propagator kernels (HydroProp, std_hydro.hpp:124-166) --------------------------------------
+
+    void ref_density(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                     unsigned last)
+    {
+        auto            d = kernelData(s, p, neighbors);
+        sph::GroupView  g{first, last, 0, nullptr, nullptr};
+        sph::computeDensityImpl(g, d, makeBox(b));
+    }
+
+    void ref_eos_std(ox_state* s, const ox_params* p, unsigned first, unsigned last)
+    {
+        auto d = kernelData(s, p, nullptr);
+        sph::computeEOS_HydroStdImpl(first, last, d);
+    }
+
+    void ref_iad_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                     unsigned last)
+    {
+        auto d = kernelData(s, p, neighbors);
+        sph::computeIADImpl(first, last, d, makeBox(b));
+    }
+
+    double ref_momentum_energy_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors,
+                                   unsigned first, unsigned last)
+    {
+        auto d = kernelData(s, p, neighbors);
+        sph::computeMomentumEnergyStdImpl(first, last, d, makeBox(b));
+        s->minDtCourant = d.minDtCourant;
+        return d.minDtCourant;
+    }
+
     void ref_positions(ox_state* s, const ox_params* p, const ox_box* b, unsigned first, unsigned last)
     {
         auto d = kernelData(s, p, nullptr);
@@ -524,20 +576,32 @@ extern "C"
         // --- computeForces
         sph::findNeighborsSph(s->x, s->y, s->z, s->h, 0u, unsigned(n), box, view, d.ng0, d.ngmax, nbr.data(),
                               s->nc);
-        sph::computeXMassImpl(0, n, d, box);
-        sph::computeVeDefGradhImpl(0, n, d, box);
-        sph::computeEOS_Impl(0, n, d);
-        sph::computeIadDivvCurlvImpl(0, n, d, box);
-        {   // rhoTimestep (ts_global.hpp:72-94), single rank
-            float maxDivv = -INFINITY;
-#pragma omp parallel for reduction(max : maxDivv)
-            for (size_t i = 0; i < n; ++i)
-                maxDivv = std::max(s->divv[i], maxDivv);
-            d.minDtRho = d.Krho / std::abs(maxDivv);
+        if (p->prop == 1)
+        {
+            // HydroProp::computeForces (std_hydro.hpp:124-166): minDtRho is never set there
+            sph::GroupView g{0, cstone::LocalIndex(n), 0, nullptr, nullptr};
+            sph::computeDensityImpl(g, d, box);
+            sph::computeEOS_HydroStdImpl(0, n, d);
+            sph::computeIADImpl(0, n, d, box);
+            sph::computeMomentumEnergyStdImpl(0, n, d, box);
         }
-        sph::computeAVswitchesImpl(0, n, d, box);
-        if (p->avClean) sph::computeMomentumEnergyImpl<true>(0, n, d, box);
-        else sph::computeMomentumEnergyImpl<false>(0, n, d, box);
+        else
+        {
+            sph::computeXMassImpl(0, n, d, box);
+            sph::computeVeDefGradhImpl(0, n, d, box);
+            sph::computeEOS_Impl(0, n, d);
+            sph::computeIadDivvCurlvImpl(0, n, d, box);
+            {   // rhoTimestep (ts_global.hpp:72-94), single rank
+                float maxDivv = -INFINITY;
+#pragma omp parallel for reduction(max : maxDivv)
+                for (size_t i = 0; i < n; ++i)
+                    maxDivv = std::max(s->divv[i], maxDivv);
+                d.minDtRho = d.Krho / std::abs(maxDivv);
+            }
+            sph::computeAVswitchesImpl(0, n, d, box);
+            if (p->avClean) sph::computeMomentumEnergyImpl<true>(0, n, d, box);
+            else sph::computeMomentumEnergyImpl<false>(0, n, d, box);
+        }
         double minDtAcc = INFINITY;
         if (p->g != 0.0)
         {
@@ -566,6 +630,31 @@ extern "C"
         s->minDtCourant = d.minDtCourant;
         s->minDtRho     = d.minDtRho;
         return 0;
+    }
+
+    /*! @brief std KATs in double precision (sph/test/std.cpp:98-127): particle 0 vs neighbors 1..4 in the open box
+     *  [0,6]^3.  cols: 5 x 19 doubles, column order x y z h m rho vx vy vz c p c11 c12 c13 c22 c23 c33 (xm kx unused).
+     *  out: c11 c12 c13 c22 c23 c33, grad_Px grad_Py grad_Pz du maxvsignal */
+    void ref_kat_std_f64(const double* cols, double* out)
+    {
+        constexpr int       np = 5, nc = 17;
+        std::vector<double> c[nc];
+        for (int k = 0; k < nc; ++k)
+            for (int i = 0; i < np; ++i)
+                c[k].push_back(cols[i * 19 + k]);
+        auto wh  = sph::tabulateFunction<double, sph::lt::kTableSize>(sph::getSphKernel(sph::sinc_n, 6.0), 0, 2);
+        auto whd = sph::tabulateFunction<double, sph::lt::kTableSize>(sph::getSphKernelDerivative(sph::sinc_n, 6.0),
+                                                                      0, 2);
+        double                          K = sph::sphynx_3D_k(6.0);
+        cstone::Box<double>             box(0, 6, cstone::BoundaryType::open);
+        std::vector<cstone::LocalIndex> nb{1, 2, 3, 4};
+        sph::IADJLoopSTD(0, K, box, nb.data(), 4u, c[0].data(), c[1].data(), c[2].data(), c[3].data(), c[4].data(),
+                         c[5].data(), wh.data(), whd.data(), &out[0], &out[1], &out[2], &out[3], &out[4], &out[5]);
+        sph::momentumAndEnergyJLoop(0, K, box, nb.data(), 4u, c[0].data(), c[1].data(), c[2].data(), c[6].data(),
+                                    c[7].data(), c[8].data(), c[3].data(), c[4].data(), c[5].data(), c[10].data(),
+                                    c[9].data(), c[11].data(), c[12].data(), c[13].data(), c[14].data(), c[15].data(),
+                                    c[16].data(), wh.data(), whd.data(), &out[6], &out[7], &out[8], &out[9],
+                                    &out[10]);
     }
 
     //! @brief KAT helpers in double precision (sph/test/ve.cpp:52-233), particle 0 vs neighbors 1..98

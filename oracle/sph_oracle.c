@@ -790,7 +790,10 @@ void ox_eos(ox_state* s, const ox_params* p, unsigned first, unsigned last)
 }
 
 /* IADJLoop (iad_kern.hpp:43-109) */
-static void IADJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s)
+/* volume weight of neighbor j: xm_j / kx_j (VE, iad_kern.hpp:74) or m_j / rho_j (std IADJLoopSTD,
+ * hydro_std/iad_kern.hpp:40), both evaluated as (num / den) * w */
+static void IADJLoopVol(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
+                        const float* num, const float* den)
 {
     float  tau11 = 0, tau12 = 0, tau13 = 0, tau22 = 0, tau23 = 0, tau33 = 0;
     double xi = s->x[i], yi = s->y[i], zi = s->z[i];
@@ -806,7 +809,7 @@ static void IADJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, 
         float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
         float vloc   = dist * hiInv;
         float w      = lookup(g_wh, vloc);
-        float volj_w = s->xm[j] / s->kx[j] * w;
+        float volj_w = num[j] / den[j] * w;
         tau11 += rx * rx * volj_w;
         tau12 += rx * ry * volj_w;
         tau13 += rx * rz * volj_w;
@@ -902,7 +905,7 @@ void ox_iad_divv_curlv(ox_state* s, const ox_params* p, const ox_box* b, const u
     {
         size_t   ni  = i - first;
         unsigned cnt = nc_capped(s->nc, i, p->ngmax);
-        IADJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s);
+        IADJLoopVol((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s, s->xm, s->kx);
         divVcurlVJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, cnt, s, p->avClean);
     }
 }
@@ -1144,6 +1147,144 @@ double ox_momentum_energy(ox_state* s, const ox_params* p, const ox_box* b, cons
         float  maxvsignal = 0;
         momentumJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s, p->Atmin,
                       p->Atmax, p->ramp, p->avClean, &maxvsignal);
+        float dt_i = tsKCourant(maxvsignal, s->h[i], s->c[i], (float)p->Kcour);
+        minDt      = minDt < dt_i ? minDt : dt_i;
+    }
+    s->minDtCourant = minDt;
+    return minDt;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * std propagator kernels (HydroProp, std_hydro.hpp:124-184)
+ * ------------------------------------------------------------------------------------------------ */
+
+/* computeDensityImpl (hydro_std/density.hpp:41-52): xmassJLoop written to rho, then rho = m / rho */
+void ox_density(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; i++)
+    {
+        size_t ni  = i - first;
+        float  xmi = xmassJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s);
+        s->rho[i]  = s->m[i] / xmi;
+    }
+}
+
+/* computeEOS_HydroStdImpl (hydro_std/eos.hpp:43-56): idealGasEOS(temp, rho, mui, gamma) in double */
+void ox_eos_std(ox_state* s, const ox_params* p, unsigned first, unsigned last)
+{
+#pragma omp parallel for schedule(static)
+    for (size_t i = first; i < last; ++i)
+    {
+        double tmp = (double)ideal_gas_cv_f(p->muiConst, p->gamma) * s->temp[i] * (p->gamma - 1.0);
+        s->p[i]    = (float)((double)s->rho[i] * tmp);
+        s->c[i]    = (float)sqrt(tmp);
+    }
+}
+
+/* computeIADImpl (hydro_std/iad.hpp:41-70) with IADJLoopSTD (hydro_std/iad_kern.hpp:12-77) */
+void ox_iad_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
+                unsigned last)
+{
+    ensure_tables();
+#pragma omp parallel for
+    for (size_t i = first; i < last; ++i)
+    {
+        size_t ni = i - first;
+        IADJLoopVol((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s, s->m, s->rho);
+    }
+}
+
+/* momentumAndEnergyJLoop of the std propagator (hydro_std/momentum_energy_kern.hpp:12-134): gradh = 1, constant
+ * alpha = 1 with the halved AV, r_ij and v_ij as i - j and the sign applied at the end (du only) */
+static void momentumStdJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
+                             float* maxvsignal)
+{
+    const float gradh_i = 1.0f, gradh_j = 1.0f;
+    double      xi = s->x[i], yi = s->y[i], zi = s->z[i];
+    float       vxi = s->vx[i], vyi = s->vy[i], vzi = s->vz[i];
+    float       hi = s->h[i], roi = s->rho[i], pri = s->p[i], ci = s->c[i];
+    float       mi_roi = s->m[i] / s->rho[i];
+    float       hiInv  = 1.0f / hi;
+    float       hiInv3 = hiInv * hiInv * hiInv;
+    float       maxvsignali = 0.0f;
+    float       momentum_x = 0, momentum_y = 0, momentum_z = 0, energy = 0;
+    float c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i], c33i = s->c33[i];
+    for (unsigned pj = 0; pj < cnt; ++pj)
+    {
+        uint32_t j  = nb[pj];
+        float    rx = (float)(xi - s->x[j]);
+        float    ry = (float)(yi - s->y[j]);
+        float    rz = (float)(zi - s->z[j]);
+        applyPBC(b, 2.0f * hi, &rx, &ry, &rz);
+        float r2     = rx * rx + ry * ry + rz * rz;
+        float dist   = sqrtf(r2);
+        float vx_ij  = vxi - s->vx[j];
+        float vy_ij  = vyi - s->vy[j];
+        float vz_ij  = vzi - s->vz[j];
+        float hj     = s->h[j];
+        float hjInv  = 1.0f / hj;
+        float v1     = dist * hiInv;
+        float v2     = dist * hjInv;
+        float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+        float hjInv3 = hjInv * hjInv * hjInv;
+        float Wi     = hiInv3 * lookup(g_wh, v1);
+        float Wj     = hjInv3 * lookup(g_wh, v2);
+        float tA1i   = c11i * rx + c12i * ry + c13i * rz;
+        float tA2i   = c12i * rx + c22i * ry + c23i * rz;
+        float tA3i   = c13i * rx + c23i * ry + c33i * rz;
+        float c11j = s->c11[j], c12j = s->c12[j], c13j = s->c13[j], c22j = s->c22[j], c23j = s->c23[j],
+              c33j = s->c33[j];
+        float tA1j = c11j * rx + c12j * ry + c13j * rz;
+        float tA2j = c12j * rx + c22j * ry + c23j * rz;
+        float tA3j = c13j * rx + c23j * ry + c33j * rz;
+        float roj  = s->rho[j];
+        float cj   = s->c[j];
+        float wij  = rv / dist;
+        /* 0.5 * artificial_viscosity(1, 1, ci, cj, wij) (kernels.hpp:70-84): (1 + 1) / 4.0 is a double */
+        float visc = 0.0f;
+        if (wij < 0.0f)
+        {
+            float vij_signal = (float)((double)(1.0f + 1.0f) / 4.0 * (double)(ci + cj) - (double)(2.0f * wij));
+            visc             = -vij_signal * wij;
+        }
+        float viscosity_ij = 0.5f * visc;
+        float vijsignal    = ci + cj - 3.0f * wij;
+        maxvsignali        = (vijsignal > maxvsignali) ? vijsignal : maxvsignali;
+        float mj        = s->m[j];
+        float mj_roj_Wj = mj / roj * Wj;
+        float mj_pro_i  = mj * pri / (gradh_i * roi * roi);
+        float am        = Wi * (mj_pro_i + viscosity_ij * mi_roi);
+        float bm        = mj_roj_Wj * (s->p[j] / (roj * gradh_j) + viscosity_ij);
+        momentum_x += am * tA1i + bm * tA1j;
+        momentum_y += am * tA2i + bm * tA2j;
+        momentum_z += am * tA3i + bm * tA3j;
+        float ae = Wi * (2.0f * mj_pro_i + viscosity_ij * mi_roi);
+        float be = viscosity_ij * mj_roj_Wj;
+        energy += vx_ij * (ae * tA1i + be * tA1j) + vy_ij * (ae * tA2i + be * tA2j) + vz_ij * (ae * tA3i + be * tA3j);
+    }
+    s->du[i]    = -K * 0.5 * (double)energy;
+    s->ax[i]    = (float)(K * (double)momentum_x);
+    s->ay[i]    = (float)(K * (double)momentum_y);
+    s->az[i]    = (float)(K * (double)momentum_z);
+    *maxvsignal = maxvsignali;
+}
+
+/* computeMomentumEnergyStdImpl (hydro_std/momentum_energy.hpp:40-84) */
+double ox_momentum_energy_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors,
+                              unsigned first, unsigned last)
+{
+    ensure_tables();
+    float minDt = INFINITY;
+#pragma omp parallel for schedule(static) reduction(min : minDt)
+    for (size_t i = first; i < last; ++i)
+    {
+        size_t ni         = i - first;
+        float  maxvsignal = 0;
+        momentumStdJLoop((uint32_t)i, p->K, b, neighbors + p->ngmax * ni, nc_capped(s->nc, i, p->ngmax), s,
+                         &maxvsignal);
         float dt_i = tsKCourant(maxvsignal, s->h[i], s->c[i], (float)p->Kcour);
         minDt      = minDt < dt_i ? minDt : dt_i;
     }
@@ -1607,17 +1748,29 @@ int ox_step(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket)
     uint32_t* nbr = (uint32_t*)malloc(sizeof(uint32_t) * n * p->ngmax);
 
     size_t fails = findNeighborsSph(s->x, s->y, s->z, s->h, 0, (uint32_t)n, b, &v, p->ng0, p->ngmax, nbr, s->nc);
-    ox_xmass(s, p, b, nbr, 0, (unsigned)n);
-    ox_ve_def_gradh(s, p, b, nbr, 0, (unsigned)n);
-    ox_eos(s, p, 0, (unsigned)n);
-    ox_iad_divv_curlv(s, p, b, nbr, 0, (unsigned)n);
-    float maxDivv = -INFINITY;
+    if (p->prop == 1)
+    {
+        /* HydroProp::computeForces (std_hydro.hpp:124-166); minDtRho is never set (stays INFINITY) */
+        ox_density(s, p, b, nbr, 0, (unsigned)n);
+        ox_eos_std(s, p, 0, (unsigned)n);
+        ox_iad_std(s, p, b, nbr, 0, (unsigned)n);
+        ox_momentum_energy_std(s, p, b, nbr, 0, (unsigned)n);
+        s->minDtRho = INFINITY;
+    }
+    else
+    {
+        ox_xmass(s, p, b, nbr, 0, (unsigned)n);
+        ox_ve_def_gradh(s, p, b, nbr, 0, (unsigned)n);
+        ox_eos(s, p, 0, (unsigned)n);
+        ox_iad_divv_curlv(s, p, b, nbr, 0, (unsigned)n);
+        float maxDivv = -INFINITY;
 #pragma omp parallel for reduction(max : maxDivv)
-    for (size_t i = 0; i < n; ++i)
-        maxDivv = s->divv[i] > maxDivv ? s->divv[i] : maxDivv;
-    s->minDtRho = p->Krho / fabs((double)maxDivv);
-    ox_av_switches(s, p, b, nbr, 0, (unsigned)n);
-    ox_momentum_energy(s, p, b, nbr, 0, (unsigned)n);
+        for (size_t i = 0; i < n; ++i)
+            maxDivv = s->divv[i] > maxDivv ? s->divv[i] : maxDivv;
+        s->minDtRho = p->Krho / fabs((double)maxDivv);
+        ox_av_switches(s, p, b, nbr, 0, (unsigned)n);
+        ox_momentum_energy(s, p, b, nbr, 0, (unsigned)n);
+    }
     double minDtAcc = INFINITY;
     if (p->g != 0.0)
     {

@@ -44,6 +44,7 @@ typedef struct ox_params
     double   g;       /* gravitational constant (ParticlesData::g, 0 = no self-gravity) */
     double   eps;     /* 0.005 (accelerationTimestep, ts_global.hpp:47-67) */
     double   etaAcc;  /* 0.2 */
+    int32_t  prop;    /* ox_step: 0 = VE (HydroVeProp, ve_hydro.hpp), 1 = std (HydroProp, std_hydro.hpp:124-184) */
 } ox_params;
 
 /* Host particle state of the VE propagator (ve_hydro.hpp:70-85 conserved + dependent fields). */
@@ -65,6 +66,7 @@ typedef struct ox_state
     uint32_t* nc;
     uint64_t* keys;
     float    *dV11, *dV12, *dV13, *dV22, *dV23, *dV33; /* velocity gradient (GradVFields), avClean only */
+    float    *rho, *p; /* density and pressure of the std propagator (HydroProp DependentFields) */
     /* scalars (ParticlesData members) */
     double minDt, minDt_m1, ttot, minDtCourant, minDtRho;
     double egrav; /* gravitational potential energy of the last step (ParticlesData::egrav) */
