@@ -29,6 +29,13 @@ MOM_FLOP_PER_PAIR = 150  # SURVEY.md 8(d) secondary VALU figure
 # compulsory HBM bytes of one momentum launch per target, as implemented: own packed records 96 B,
 # nc 4 B, outputs 20 B, u16 neighbor positions 2 B/neighbor, union index 4 B per union entry
 MOM_COMPULSORY_OWN = 96 + 4 + 20
+# std propagator momentum (hydro_std/momentum_energy_kern.hpp): own x,y,z,v,h,m,rho,p,c,c_ij + nc read, a,du written;
+# per edge the index + x,y,z (24) v (12) h m rho p c (20) c_ij (24)
+MOM_STD_OWN_BYTES = 24 + 12 + 20 + 24 + 4 + 12 + 8
+MOM_STD_EDGE_BYTES = 4 + 80
+# kernel-time slots of sx_sim in std mode (sx_sim.cpp: density in "xmass", IAD in "iadDivvCurlv")
+STD_KERNEL_NAMES = {"findNeighbors": "findNeighbors", "xmass": "density", "iadDivvCurlv": "iad",
+                    "momentumEnergy": "momentumEnergySTD", "gravity": "gravity"}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
@@ -65,6 +72,8 @@ def parse():
     ap.add_argument("--init", default="sedov", choices=["sedov", "noh", "evrard"],
                     help="sedov (BASELINE metric, device IC), noh (config 3), evrard (config 5: VE + self-gravity)")
     ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
+    ap.add_argument("--prop", default="ve", choices=["ve", "std"],
+                    help="ve (HydroVeProp, the BASELINE metric) or std (HydroProp, std_hydro.hpp)")
     return ap.parse_args()
 
 
@@ -135,7 +144,8 @@ def main():
         box = sx.make_box(lim, bnd)
     # capacity: the rank's share plus halos (surface layer of the SFC domain) with headroom
     cap = n_total if world == 1 else int(1.6 * n_total / world) + 65536
-    params = sx.default_params(av_clean=args.av_clean, g=1.0 if args.init == "evrard" else 0.0)
+    params = sx.default_params(av_clean=args.av_clean, g=1.0 if args.init == "evrard" else 0.0,
+                               std=args.prop == "std")
     sim = sx.Sim(ctx, cap, box, params=params, bucket=args.bucket)
     comm = None
     transport = args.backend
@@ -192,7 +202,10 @@ def main():
     ms_step = el / args.steps * 1e3
     ng = stats["sumNeighbors"] / max(1, n_local)
     mom_ms = kern_sum.get("momentumEnergy", float("nan")) / args.steps
-    mom_bytes = n_local * (MOM_OWN_BYTES + ng * MOM_EDGE_BYTES)
+    std_prop = args.prop == "std"
+    own_b, edge_b = (MOM_STD_OWN_BYTES, MOM_STD_EDGE_BYTES) if std_prop else (MOM_OWN_BYTES, MOM_EDGE_BYTES)
+    mom_kernel = "momentumStdKernel" if std_prop else "momentumEnergyKernel"
+    mom_bytes = n_local * (own_b + ng * edge_b)
     achieved = mom_bytes / (mom_ms * 1e-3) / 1e9
     union_pp = stats["sumUnion"] / max(1, n_local)
     comp_bytes = n_local * (MOM_COMPULSORY_OWN + 2 * ng + 4 * union_pp)
@@ -212,7 +225,8 @@ def main():
         "dtype": "f32 hydro / f64 coordinates (sph::SphTypes)",
         "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint" if ic_arrays is None
                 else f"synthetic {args.init} lattice substitute for the glass block (SURVEY F6), sphexa_amd/ic.py",
-        "config": {"workload": f"{args.init.capitalize()} -n {side} ({n_total} particles), VE propagator"
+        "config": {"workload": f"{args.init.capitalize()} -n {side} ({n_total} particles), "
+                               f"{'std (HydroProp)' if std_prop else 'VE'} propagator"
                                f"{' + self-gravity' if args.init == 'evrard' else ''}"
                                f"{' + AV cleaning' if args.av_clean else ''}, {args.steps} steps",
                    "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
@@ -220,17 +234,18 @@ def main():
                    f"{world} GPUs: SFC domain decomposition, halo + particle exchange over {transport}",
                    "halos_per_gpu": sim.layout()["n"] - n_local,
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
-        "roofline": {"bound": "hbm", "kernel": "momentumEnergyKernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("momentumEnergyKernel", n_local),
+        "roofline": {"bound": "hbm", "kernel": mom_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(mom_kernel, n_local),
                      "algorithmic_bytes_per_launch": mom_bytes, "avg_launch_ms": mom_ms,
-                     "model": f"edge model (SURVEY.md 8(d)): {MOM_OWN_BYTES} B own + {ng:.1f} neighbors x "
-                              f"{MOM_EDGE_BYTES} B; effective bandwidth, neighbor records come from LDS",
+                     "model": f"edge model (SURVEY.md 8(d)): {own_b} B own + {ng:.1f} neighbors x "
+                              f"{edge_b} B; effective bandwidth, neighbor records come from LDS",
                      "compulsory_bytes_per_launch": comp_bytes,
                      "compulsory_frac": comp_bytes / (mom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "valu": {"flop_per_pair": MOM_FLOP_PER_PAIR, "achieved_tflops": mom_tflops,
                               "peak_tflops": FP32_PEAK_TFLOPS, "frac": mom_tflops / FP32_PEAK_TFLOPS},
                      "traffic_source": os.path.relpath(PMC_FILE, ROOT)},
-        "kernels_ms": {k: v / args.steps for k, v in kern_sum.items()},
+        "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v / args.steps for k, v in kern_sum.items()
+                       if not std_prop or k in STD_KERNEL_NAMES},
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
         "neighbors_per_particle": ng,
         "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),

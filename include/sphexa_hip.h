@@ -20,6 +20,10 @@
  *   sx_av_switches         sph::cuda::computeAVswitches         sph_gpu.hpp:48, hydro_ve/av_switches_gpu.cu:103
  *   sx_momentum_energy     sph::cuda::computeMomentumEnergy<avClean=false> sph_gpu.hpp:51-53, momentum_energy_gpu.cu:121
  *   sx_momentum_energy_avclean  sph::cuda::computeMomentumEnergy<avClean=true>  (same seam, second instantiation)
+ *   sx_density             sph::cuda::computeDensity (std)      sph_gpu.hpp:32, hydro_ve/xmass_gpu.cu:150-164
+ *   sx_eos_std             sph::cuda::computeEOS_HydroStd       sph_gpu.hpp:46-47, hydro_std/eos_gpu.cu:54-62
+ *   sx_iad                 sph::computeIADGpu (std)             sph_gpu.hpp:19-20, hydro_std/iad_gpu.cu:111-124
+ *   sx_momentum_energy_std sph::computeMomentumEnergyStdGpu     sph_gpu.hpp:22-23, hydro_std/momentum_energy_gpu.cu:109
  *   sx_positions           sph::computePositionsGpu             sph_gpu.hpp:64-72, positions_gpu.cu:167-179
  *   sx_update_h            sph::updateSmoothingLengthGpu        sph_gpu.hpp:78, update_h_gpu.cu:49-60
  *   sx_max_divv            cstone::MinMaxGpu (rhoTimestep)      sph/ts_global.hpp:72-94
@@ -82,6 +86,7 @@ typedef struct sx_params
     float    theta;   /* gravity opening parameter (sphexa.cpp:127: 0.5 with gravity) */
     double   g;       /* gravitational constant (ParticlesData::g); sx_sim adds self-gravity when != 0 */
     double   eps, etaAcc; /* accelerationTimestep (ts_global.hpp:47-67): 0.005, 0.2 */
+    int32_t  propagator;  /* sx_sim only: 0 = ve (HydroVeProp), 1 = std (HydroProp, std_hydro.hpp; factory.hpp:50-84) */
 } sx_params;
 
 /*! Device pointers in sphexa::ParticlesData field order (particles_data.hpp:247-251); NULL where unused.
@@ -231,6 +236,23 @@ int sx_momentum_energy(sx_ctx* ctx, const sx_groups* g, float* groupDt, const sx
  *  avRvCorrection of the AV-cleaning propagator (momentum_energy_kern.hpp:43-63); needs f->dV11..dV33 */
 int sx_momentum_energy_avclean(sx_ctx* ctx, const sx_groups* g, float* groupDt, const sx_fields* f,
                                const sx_params* p, const sx_box* box, float* minDtCourant);
+/* ---- std propagator (HydroProp, main/src/propagator/std_hydro.hpp:124-184) ----------------------------- */
+/*! sph::cuda::computeDensity (sph_gpu.hpp:32, hydro_ve/xmass_gpu.cu:150-164): neighbor search with the h-nc
+ *  iteration (like sx_xmass), the XMass loop written to rho, then rho = m / rho.  Needs f->rho. */
+int sx_density(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+               const sx_tree* tree);
+/*! density on the cached (or imported) neighbor list, without a new search */
+int sx_density_only(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
+/*! sph::cuda::computeEOS_HydroStd (sph_gpu.hpp:46-47, hydro_std/eos_gpu.cu:54-62): p, c from temp and rho */
+int sx_eos_std(sx_ctx* ctx, uint32_t first, uint32_t last, float mui, double gamma, const double* temp,
+               const float* m, float* rho, float* p, float* c);
+/*! sph::computeIADGpu (sph_gpu.hpp:19-20, hydro_std/iad_gpu.cu:111-124): c11..c33 with volumes m/rho */
+int sx_iad(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box);
+/*! sph::computeMomentumEnergyStdGpu (sph_gpu.hpp:22-23, hydro_std/momentum_energy_gpu.cu:109-129): ax,ay,az,du
+ *  (alpha = 1, gradh = 1); *minDtCourant receives the min Courant time-step */
+int sx_momentum_energy_std(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p,
+                           const sx_box* box, float* minDtCourant);
+
 /*! 2nd-order Press position update + AB2 energy update on temp (positions.hpp:54-139, F2-correct); dt, dt_m1 double
  *  as in the CPU path (the reference GPU path passes them as float). */
 int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,

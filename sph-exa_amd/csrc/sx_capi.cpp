@@ -630,6 +630,79 @@ extern "C"
         return momentumEnergy(c, g, groupDt, f, p, box, minDtCourant, true);
     }
 
+    // ---- std propagator (HydroProp, std_hydro.hpp:124-184) --------------------------------------------------
+
+    int sx_density(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                   const sx_tree* tree)
+    {
+        if (!f->rho) return fail(c, SX_ERR_ARG, "sx_density needs f->rho");
+        int rc = sx_find_neighbors(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
+        if (rc != SX_OK) return rc;
+        return sx_density_only(c, g, f, p, box);
+    }
+
+    int sx_density_only(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        if (!f->rho) return fail(c, SX_ERR_ARG, "sx_density needs f->rho");
+        Records r = records(c, f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        PairArgs a = pairArgs(c, g, f, p, box, r);
+        a.xm       = f->rho; // computeDensity: swap(xm, rho), computeXMass, swap back (xmass_gpu.cu:151-153)
+        c->hydro().xmass(a, c->stream);
+        c->hydro().xmassToRho(g->firstBody, g->lastBody, f->m, f->rho, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_eos_std(sx_ctx* c, uint32_t first, uint32_t last, float mui, double gamma, const double* temp,
+                   const float* m, float* rho, float* pr, float* cs)
+    {
+        if (first < last && !(temp && rho && pr && cs)) return fail(c, SX_ERR_ARG, "sx_eos_std: null field");
+        EosArgs a{first, last, mui, gamma, temp, m, nullptr, nullptr, nullptr, nullptr, cs, rho, pr};
+        c->hydro().eosStd(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_iad(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        if (!f->rho) return fail(c, SX_ERR_ARG, "sx_iad needs f->rho");
+        Records r = records(c, f->n);
+        RecS*   rs = c->arena.get<RecS>("rec.s", f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packS(f->n, f->rho, nullptr, rs, c->stream);
+        PairArgs a = pairArgs(c, g, f, p, box, r);
+        a.rs       = rs;
+        c->hydro().iadStd(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_momentum_energy_std(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p,
+                               const sx_box* box, float* minDtCourant)
+    {
+        if (int e = checkList(c, g, p)) return e;
+        if (!(f->rho && f->p)) return fail(c, SX_ERR_ARG, "sx_momentum_energy_std needs f->rho and f->p");
+        Records r = records(c, f->n);
+        RecS*   rs = c->arena.get<RecS>("rec.s", f->n);
+        packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+        packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
+        packS(f->n, f->rho, f->p, rs, c->stream);
+        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, nullptr, r.rc, c->stream);
+        float huge = 1e10f; // hydro_std/momentum_energy_gpu.cu:115
+        SX_HIP(c, hipMemcpyAsync(c->minDt, &huge, 4, hipMemcpyHostToDevice, c->stream));
+        PairArgs a = pairArgs(c, g, f, p, box, r);
+        a.rs       = rs;
+        c->hydro().momentumStd(a, c->stream);
+        SX_HIP(c, hipGetLastError());
+        SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->minDt, 4, hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        if (minDtCourant) *minDtCourant = c->hostScalar[0];
+        return SX_OK;
+    }
+
     int sx_positions(sx_ctx* c, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
                      double gamma, float muiConst, const sx_box* box)
     {

@@ -52,6 +52,11 @@ struct __attribute__((aligned(16))) RecT
 {
     float xm, kx, prho, alpha;
 };
+//! std propagator (HydroProp): density and pressure of a neighbor (no xm/kx/prho/alpha there)
+struct __attribute__((aligned(16))) RecS
+{
+    float rho, p, pad0, pad1;
+};
 struct __attribute__((aligned(16))) RecC
 {
     float c11, c12, c13, c22, c23, c33, divv, pad;

@@ -147,23 +147,9 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(PairArgs a)
         t23 += ry * rz * volj_w;
         t33 += rz * rz * volj_w;
     }
-    auto getExp   = [](float v) { return v == 0.0f ? 0 : ilogbf(v); };
-    int  tauExpSum = getExp(t11) + getExp(t12) + getExp(t13) + getExp(t22) + getExp(t23) + getExp(t33);
-    float normalization = ldexpf(1.0f, -tauExpSum / 6);
-    t11 *= normalization;
-    t12 *= normalization;
-    t13 *= normalization;
-    t22 *= normalization;
-    t23 *= normalization;
-    t33 *= normalization;
-    float det = t11 * t22 * t33 + 2.0f * t12 * t23 * t13 - t11 * t23 * t23 - t22 * t13 * t13 - t33 * t12 * t12;
-    float factor = (float)((double)(normalization * (hi * hi * hi)) / ((double)det * a.K));
-    const float c11i = (t22 * t33 - t23 * t23) * factor;
-    const float c12i = (t13 * t23 - t33 * t12) * factor;
-    const float c13i = (t12 * t23 - t22 * t13) * factor;
-    const float c22i = (t11 * t33 - t13 * t13) * factor;
-    const float c23i = (t13 * t12 - t11 * t23) * factor;
-    const float c33i = (t11 * t22 - t12 * t12) * factor;
+    float cc[6];
+    iadInvert(t11, t12, t13, t22, t23, t33, hi, a.K, cc);
+    const float c11i = cc[0], c12i = cc[1], c13i = cc[2], c22i = cc[3], c23i = cc[4], c33i = cc[5];
     a.c11[i]         = c11i;
     a.c12[i]         = c12i;
     a.c13[i]         = c13i;
@@ -442,6 +428,148 @@ __global__ void eosKernel(EosArgs a)
     if (a.p) a.p[i] = (float)pi;
 }
 
+// ---- std propagator (HydroProp, std_hydro.hpp:124-184) ----------------------------------------------------------
+
+//! convertXmassToRho (hydro_ve/xmass_gpu.cu:134-148): the xmass kernel wrote m / rho0 into rho
+__global__ void xmassToRhoKernel(uint32_t first, uint32_t last, const float* m, float* rho)
+{
+    uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < last) rho[i] = m[i] / rho[i];
+}
+
+//! cudaEOS_HydroStd (hydro_std/eos_gpu.cu:43-52): idealGasEOS(temp, rho, mui, gamma) in double (sph/eos.hpp:31-40)
+__global__ void eosStdKernel(EosArgs a)
+{
+    uint32_t i = a.first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.last) return;
+    double tmp = (double)idealGasCv(a.mui, a.gamma) * a.temp[i] * (a.gamma - 1.0);
+    a.p[i]     = (float)((double)a.rho[i] * tmp);
+    a.c[i]     = (float)sqrt(tmp);
+}
+
+//! IADJLoopSTD (hydro_std/iad_kern.hpp:12-77): the IAD tensor with volumes m_j / rho_j
+__global__ __launch_bounds__(kBlock) void iadStdKernel(PairArgs a)
+{
+    SX_PAIR_PROLOGUE
+    if (!valid) return;
+    const RecX ri    = a.rx[i];
+    const float hi    = ri.h;
+    const float hiInv = 1.0f / hi;
+    float       t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
+    for (unsigned k = 0; k < cnt; ++k)
+    {
+        uint32_t   j  = nbj(k);
+        const RecX rj = a.rx[j];
+        float      rx = (float)(ri.x - rj.x);
+        float      ry = (float)(ri.y - rj.y);
+        float      rz = (float)(ri.z - rj.z);
+        applyPBC(a.box, 2.0f * hi, rx, ry, rz);
+        float dist     = sqrtf(rx * rx + ry * ry + rz * rz);
+        float w        = lookup(a.wh, dist * hiInv);
+        float mj_roj_w = rj.m / a.rs[j].rho * w;
+        t11 += rx * rx * mj_roj_w;
+        t12 += rx * ry * mj_roj_w;
+        t13 += rx * rz * mj_roj_w;
+        t22 += ry * ry * mj_roj_w;
+        t23 += ry * rz * mj_roj_w;
+        t33 += rz * rz * mj_roj_w;
+    }
+    float cc[6];
+    iadInvert(t11, t12, t13, t22, t23, t33, hi, a.K, cc);
+    a.c11[i] = cc[0], a.c12[i] = cc[1], a.c13[i] = cc[2], a.c22[i] = cc[3], a.c23[i] = cc[4], a.c33[i] = cc[5];
+}
+
+//! momentumAndEnergyJLoop of the std propagator (hydro_std/momentum_energy_kern.hpp:12-134): gradh = 1, alpha = 1
+//! with the halved AV; Courant time-step reduced as in cudaGradP (hydro_std/momentum_energy_gpu.cu:64-107)
+__global__ __launch_bounds__(kBlock) void momentumStdKernel(PairArgs a)
+{
+    SX_PAIR_PROLOGUE
+    float dt_lane = INFINITY;
+    if (valid)
+    {
+        const RecX ri  = a.rx[i];
+        const RecV vi  = a.rv[i];
+        const RecS si  = a.rs[i];
+        const RecC ci6 = a.rc[i];
+        const float hi = ri.h, roi = si.rho, pri = si.p, ci = vi.c;
+        const float mi_roi = ri.m / roi;
+        const float hiInv  = 1.0f / hi;
+        const float hiInv3 = hiInv * hiInv * hiInv;
+        float       maxvsignali = 0.0f;
+        float       mx = 0, my = 0, mz = 0, energy = 0;
+        for (unsigned k = 0; k < cnt; ++k)
+        {
+            uint32_t   j   = nbj(k);
+            const RecX rj  = a.rx[j];
+            const RecV vj  = a.rv[j];
+            const RecS sj  = a.rs[j];
+            const RecC cj6 = a.rc[j];
+            float      rx  = (float)(ri.x - rj.x);
+            float      ry  = (float)(ri.y - rj.y);
+            float      rz  = (float)(ri.z - rj.z);
+            applyPBC(a.box, 2.0f * hi, rx, ry, rz);
+            float r2     = rx * rx + ry * ry + rz * rz;
+            float dist   = sqrtf(r2);
+            float vx_ij  = vi.vx - vj.vx;
+            float vy_ij  = vi.vy - vj.vy;
+            float vz_ij  = vi.vz - vj.vz;
+            float hjInv  = 1.0f / rj.h;
+            float v1     = dist * hiInv;
+            float v2     = dist * hjInv;
+            float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+            float hjInv3 = hjInv * hjInv * hjInv;
+            float Wi     = hiInv3 * lookup(a.wh, v1);
+            float Wj     = hjInv3 * lookup(a.wh, v2);
+            float tA1i   = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
+            float tA2i   = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
+            float tA3i   = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;
+            float tA1j   = cj6.c11 * rx + cj6.c12 * ry + cj6.c13 * rz;
+            float tA2j   = cj6.c12 * rx + cj6.c22 * ry + cj6.c23 * rz;
+            float tA3j   = cj6.c13 * rx + cj6.c23 * ry + cj6.c33 * rz;
+            float roj    = sj.rho;
+            float cj     = vj.c;
+            float wij    = rv / dist;
+            // 0.5 * artificial_viscosity(1, 1, ci, cj, wij) (kernels.hpp:70-84): (1 + 1) / 4.0 is a double
+            float visc = 0.0f;
+            if (wij < 0.0f)
+            {
+                float vij_signal = (float)((double)(1.0f + 1.0f) / 4.0 * (double)(ci + cj) - (double)(2.0f * wij));
+                visc             = -vij_signal * wij;
+            }
+            const float viscosity_ij = 0.5f * visc;
+            const float vijsignal    = ci + cj - 3.0f * wij;
+            maxvsignali              = (vijsignal > maxvsignali) ? vijsignal : maxvsignali;
+            const float mj        = rj.m;
+            const float mj_roj_Wj = mj / roj * Wj;
+            const float mj_pro_i  = mj * pri / (roi * roi); // gradh_i = 1
+            const float am        = Wi * (mj_pro_i + viscosity_ij * mi_roi);
+            const float bm        = mj_roj_Wj * (sj.p / roj + viscosity_ij); // gradh_j = 1
+            mx += am * tA1i + bm * tA1j;
+            my += am * tA2i + bm * tA2j;
+            mz += am * tA3i + bm * tA3j;
+            const float ae = Wi * (2.0f * mj_pro_i + viscosity_ij * mi_roi);
+            const float be = viscosity_ij * mj_roj_Wj;
+            energy += vx_ij * (ae * tA1i + be * tA1j) + vy_ij * (ae * tA2i + be * tA2j) + vz_ij * (ae * tA3i + be * tA3j);
+        }
+        a.du[i] = -a.K * 0.5 * (double)energy;
+        a.ax[i] = (float)(a.K * (double)mx);
+        a.ay[i] = (float)(a.K * (double)my);
+        a.az[i] = (float)(a.K * (double)mz);
+        dt_lane = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+    }
+    float wmin = waveMin(dt_lane);
+    __shared__ float smin[kBlock / kWave];
+    if (lane == 0) smin[threadIdx.x >> 6] = wmin;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        float m = smin[0];
+        for (int w = 1; w < kBlock / kWave; ++w)
+            m = smin[w] < m ? smin[w] : m;
+        atomicMinPos(a.minDt, m);
+    }
+}
+
 //! positionUpdate + putInBox + energyUpdate (positions.hpp:54-139, F2-correct as positions_gpu.cu:118-165)
 __global__ void positionsKernel(PosArgs a)
 {
@@ -554,6 +682,27 @@ static void launchUpdateH(uint32_t first, uint32_t last, uint32_t ng0, const uin
     if (n) updateHKernel<<<(n + 255) / 256, 256, 0, s>>>(first, last, ng0, nc, h, powTab);
 }
 
+static void launchXmassToRho(uint32_t first, uint32_t last, const float* m, float* rho, hipStream_t s)
+{
+    uint32_t n = last - first;
+    if (n) xmassToRhoKernel<<<(n + 255) / 256, 256, 0, s>>>(first, last, m, rho);
+}
+static void launchEosStd(const EosArgs& a, hipStream_t s)
+{
+    uint32_t n = a.last - a.first;
+    if (n) eosStdKernel<<<(n + 255) / 256, 256, 0, s>>>(a);
+}
+static void launchIadStd(const PairArgs& a, hipStream_t s)
+{
+    if (kFastClusters && a.localLists) return cluster::iadStd(a, s);
+    if (a.numGroups) iadStdKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
+}
+static void launchMomentumStd(const PairArgs& a, hipStream_t s)
+{
+    if (kFastClusters && a.localLists) return cluster::momentumStd(a, s);
+    if (a.numGroups) momentumStdKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
+}
+
 } // namespace SX_VARIANT
 
 #define SX_CAT2(a, b) a##b
@@ -563,7 +712,9 @@ const HydroLaunch& SX_CAT(hydro_, SX_VARIANT)()
 {
     static const HydroLaunch t{SX_VARIANT::launchXmass,     SX_VARIANT::launchVeDefGradh, SX_VARIANT::launchIad,
                                SX_VARIANT::launchAv,        SX_VARIANT::launchMomentum,   SX_VARIANT::launchEos,
-                               SX_VARIANT::launchPositions, SX_VARIANT::launchUpdateH};
+                               SX_VARIANT::launchPositions, SX_VARIANT::launchUpdateH,
+                               SX_VARIANT::launchXmassToRho, SX_VARIANT::launchEosStd,
+                               SX_VARIANT::launchIadStd,    SX_VARIANT::launchMomentumStd};
     return t;
 }
 

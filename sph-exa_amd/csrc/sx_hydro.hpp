@@ -49,7 +49,28 @@ struct PairArgs
     // when dV11 != nullptr (doGradV, iad_divv_curlv_gpu.cu:96-97); momentum reads it when avClean != 0
     float *dV11, *dV12, *dV13, *dV22, *dV23, *dV33;
     int    avClean;
+    // std propagator (HydroProp, std_hydro.hpp:124-184): rho and p of every particle (IAD, momentumEnergySTD)
+    const RecS* rs;
 };
+
+//! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent
+//! normalisation of tau, then the cofactor inverse scaled by h^3 / K
+__device__ __forceinline__ void iadInvert(float t11, float t12, float t13, float t22, float t23, float t33, float hi,
+                                          double K, float (&c)[6])
+{
+    auto getExp    = [](float v) { return v == 0.0f ? 0 : ilogbf(v); };
+    int  tauExpSum = getExp(t11) + getExp(t12) + getExp(t13) + getExp(t22) + getExp(t23) + getExp(t33);
+    const float nrm = ldexpf(1.0f, -tauExpSum / 6);
+    t11 *= nrm, t12 *= nrm, t13 *= nrm, t22 *= nrm, t23 *= nrm, t33 *= nrm;
+    const float det    = t11 * t22 * t33 + 2.0f * t12 * t23 * t13 - t11 * t23 * t23 - t22 * t13 * t13 - t33 * t12 * t12;
+    const float factor = (float)((double)(nrm * (hi * hi * hi)) / ((double)det * K));
+    c[0]               = (t22 * t33 - t23 * t23) * factor;
+    c[1]               = (t13 * t23 - t33 * t12) * factor;
+    c[2]               = (t12 * t23 - t22 * t13) * factor;
+    c[3]               = (t11 * t33 - t13 * t13) * factor;
+    c[4]               = (t13 * t12 - t11 * t23) * factor;
+    c[5]               = (t11 * t22 - t12 * t12) * factor;
+}
 
 //! eta_crit of momentumAndEnergyJLoop<avClean> (momentum_energy_kern.hpp:112): formed in double, stored as float
 __device__ __forceinline__ float avEtaCrit(unsigned cnt)
@@ -120,6 +141,12 @@ struct HydroLaunch
     void (*positions)(const PosArgs&, hipStream_t);
     void (*updateH)(uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h, const float* powTab,
                     hipStream_t);
+    // std propagator (HydroProp): density = xmass written to rho then rho = m / rho (xmass_gpu.cu:134-164),
+    // EOS_HydroStd, IAD with m/rho volumes, momentumEnergySTD
+    void (*xmassToRho)(uint32_t first, uint32_t last, const float* m, float* rho, hipStream_t);
+    void (*eosStd)(const EosArgs&, hipStream_t);
+    void (*iadStd)(const PairArgs&, hipStream_t);
+    void (*momentumStd)(const PairArgs&, hipStream_t);
 };
 
 const HydroLaunch& hydro_exact();
@@ -134,6 +161,8 @@ void veDefGradh(const PairArgs&, hipStream_t);
 void iadDivvCurlv(const PairArgs&, hipStream_t);
 void avSwitches(const PairArgs&, hipStream_t);
 void momentumEnergy(const PairArgs&, hipStream_t);
+void iadStd(const PairArgs&, hipStream_t);
+void momentumStd(const PairArgs&, hipStream_t);
 } // namespace cluster
 
 } // namespace sx

@@ -332,26 +332,31 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
 }
 
 // ---- IAD + divv/curlv: IADJLoop (iad_kern.hpp:43-109) + divV_curlVJLoop (divv_curlv_kern.hpp:43-123) -------------
-template<int CH, int SPLIT>
+//! STD: IADJLoopSTD (hydro_std/iad_kern.hpp:12-77), volumes m/rho and no velocity derivatives
+template<int CH, int SPLIT, bool STD = false>
 __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
 {
-    __shared__ float4 sP[CH]; // x, y, z, vol = xm/kx
-    __shared__ float4 sV[CH]; // vx, vy, vz, xm
+    __shared__ float4 sP[CH];               // x, y, z, vol = xm/kx (std: m/rho)
+    __shared__ float4 sV[STD ? 1 : CH];     // vx, vy, vz, xm
     __shared__ float  s_red[kClusterWaves * SPLIT];
     __shared__ float  s_scr[SPLIT > 1 ? 9 * SPLIT * kCluster : 1];
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
-    const RecV  vi  = a.rv[cu.iSafe];
-    const float kxi = a.rt[cu.iSafe].kx;
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
     const float hi = ri.h, hiInv = 1.0f / hi, h2 = 2.0f * hi;
     auto        stage = [&](uint32_t j, uint32_t slot) {
         const RecX r = a.rx[j];
-        const RecV v = a.rv[j];
-        const RecT t = a.rt[j];
-        sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
-                               t.xm / t.kx);
-        sV[slot]     = make_float4(v.vx, v.vy, v.vz, t.xm);
+        if constexpr (STD)
+            sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
+                                   r.m / a.rs[j].rho);
+        else
+        {
+            const RecV v = a.rv[j];
+            const RecT t = a.rt[j];
+            sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
+                                   relc(r.z, cu.oz, a.box, 2), t.xm / t.kx);
+            sV[slot]     = make_float4(v.vx, v.vy, v.vz, t.xm);
+        }
     };
     float t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
     bool  res = false;
@@ -375,18 +380,20 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         combineShares<SPLIT>(cu, v, s_scr);
         t11 = v[0], t12 = v[1], t13 = v[2], t22 = v[3], t23 = v[4], t33 = v[5];
     }
-    auto  getExp    = [](float v) { return v == 0.0f ? 0 : ilogbf(v); };
-    int   tauExpSum = getExp(t11) + getExp(t12) + getExp(t13) + getExp(t22) + getExp(t23) + getExp(t33);
-    float nrm       = ldexpf(1.0f, -tauExpSum / 6);
-    t11 *= nrm, t12 *= nrm, t13 *= nrm, t22 *= nrm, t23 *= nrm, t33 *= nrm;
-    const float det = t11 * t22 * t33 + 2.0f * t12 * t23 * t13 - t11 * t23 * t23 - t22 * t13 * t13 - t33 * t12 * t12;
-    const float factor = (float)((double)(nrm * (hi * hi * hi)) / ((double)det * a.K));
-    const float c11i   = (t22 * t33 - t23 * t23) * factor;
-    const float c12i   = (t13 * t23 - t33 * t12) * factor;
-    const float c13i   = (t12 * t23 - t22 * t13) * factor;
-    const float c22i   = (t11 * t33 - t13 * t13) * factor;
-    const float c23i   = (t13 * t12 - t11 * t23) * factor;
-    const float c33i   = (t11 * t22 - t12 * t12) * factor;
+    float cc[6];
+    iadInvert(t11, t12, t13, t22, t23, t33, hi, a.K, cc);
+    const float c11i = cc[0], c12i = cc[1], c13i = cc[2], c22i = cc[3], c23i = cc[4], c33i = cc[5];
+    if constexpr (STD)
+    {
+        if (cu.valid && cu.part == 0)
+        {
+            const uint32_t i = cu.i;
+            a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
+        }
+        return;
+    }
+    const RecV  vi  = a.rv[cu.iSafe];
+    const float kxi = a.rt[cu.iSafe].kx;
 
     float dVx0 = 0, dVx1 = 0, dVx2 = 0, dVy0 = 0, dVy1 = 0, dVy2 = 0, dVz0 = 0, dVz1 = 0, dVz2 = 0;
     neighborLoop<CH, SPLIT>(
@@ -700,6 +707,115 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     }
 }
 
+// ---- std momentum + energy: momentumAndEnergyJLoop (hydro_std/momentum_energy_kern.hpp:12-134) ----------------
+struct RecMS
+{
+    float4 p, v, a, b;
+    float  m;
+};
+
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH]; // x, y, z, 1/h
+    __shared__ float4 sV[CH]; // vx, vy, vz, c
+    __shared__ float4 sA[CH]; // c11, c12, c13, m/rho
+    __shared__ float4 sB[CH]; // c22, c23, c33, p/rho
+    __shared__ float  sM[CH]; // m
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    const Clu   cu  = setup<SPLIT>(a, s_red);
+    const RecX  ri  = a.rx[cu.iSafe];
+    const RecV  vi  = a.rv[cu.iSafe];
+    const RecS  si  = a.rs[cu.iSafe];
+    const RecC  ci6 = a.rc[cu.iSafe];
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hi = ri.h, ci = vi.c, h2 = 2.0f * hi;
+    const float roi    = si.rho;
+    const float mi_roi = ri.m / roi;
+    const float prr_i  = si.p / (roi * roi); // gradh_i = 1
+    const float hiInv  = 1.0f / hi;
+    const float hiInv3 = hiInv * hiInv * hiInv;
+    float maxvsignali = 0.0f;
+    float mx = 0, my = 0, mz = 0, energy = 0;
+    bool  res = false;
+    neighborLoop<CH, SPLIT>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r  = a.rx[j];
+            const RecV v  = a.rv[j];
+            const RecS s  = a.rs[j];
+            const RecC c6 = a.rc[j];
+            sP[slot]      = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
+                                   relc(r.z, cu.oz, a.box, 2), 1.0f / r.h);
+            sV[slot]      = make_float4(v.vx, v.vy, v.vz, v.c);
+            sA[slot]      = make_float4(c6.c11, c6.c12, c6.c13, r.m / s.rho);
+            sB[slot]      = make_float4(c6.c22, c6.c23, c6.c33, s.p / s.rho);
+            sM[slot]      = r.m;
+        },
+        [&](uint32_t p) { return RecMS{sP[p], sV[p], sA[p], sB[p], sM[p]}; },
+        [&](const RecMS& r) {
+            const float4 &P = r.p, &V = r.v, &A = r.a, &B = r.b;
+            float         rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float r2     = rx * rx + ry * ry + rz * rz;
+            const float rinv   = rsqrtf(r2);
+            const float dist   = r2 * rinv;
+            const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
+            const float hjInv  = P.w;
+            const float Wi     = hiInv3 * kernelW(dist * hiInv);
+            const float Wj     = hjInv * hjInv * hjInv * kernelW(dist * hjInv);
+            const float tA1i   = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
+            const float tA2i   = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
+            const float tA3i   = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;
+            const float tA1j   = A.x * rx + A.y * ry + A.z * rz;
+            const float tA2j   = A.y * rx + B.x * ry + B.y * rz;
+            const float tA3j   = A.z * rx + B.y * ry + B.z * rz;
+            const float cj     = V.w;
+            const float wij    = (rx * vx_ij + ry * vy_ij + rz * vz_ij) * rinv;
+            // 0.5 * artificial_viscosity(1, 1, ci, cj, wij) (kernels.hpp:70-84)
+            const float visc   = wij < 0.0f ? -0.5f * (0.5f * (ci + cj) - 2.0f * wij) * wij : 0.0f;
+            maxvsignali        = fmaxf(maxvsignali, ci + cj - 3.0f * wij);
+            const float mj_pro_i  = r.m * prr_i;
+            const float mj_roj_Wj = A.w * Wj;
+            const float am        = Wi * fmaf(visc, mi_roi, mj_pro_i);
+            const float bm        = mj_roj_Wj * (B.w + visc);
+            mx += am * tA1i + bm * tA1j;
+            my += am * tA2i + bm * tA2j;
+            mz += am * tA3i + bm * tA3j;
+            const float ae = Wi * fmaf(visc, mi_roi, 2.0f * mj_pro_i);
+            const float be = visc * mj_roj_Wj;
+            energy += ae * (vx_ij * tA1i + vy_ij * tA2i + vz_ij * tA3i) +
+                      be * (vx_ij * tA1j + vy_ij * tA2j + vz_ij * tA3j);
+        },
+        res);
+    {
+        float v[5] = {mx, my, mz, energy, maxvsignali};
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 16u, true);
+        mx = v[0], my = v[1], mz = v[2], energy = v[3], maxvsignali = v[4];
+    }
+    float dt_lane = INFINITY;
+    if (cu.valid && cu.part == 0)
+    {
+        a.du[cu.i] = -a.K * 0.5 * (double)energy;
+        a.ax[cu.i] = (float)(a.K * (double)mx);
+        a.ay[cu.i] = (float)(a.K * (double)my);
+        a.az[cu.i] = (float)(a.K * (double)mz);
+        dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+    }
+    const float wmin = waveMin(dt_lane);
+    const int   wave = threadIdx.x >> 6;
+    __syncthreads(); // s_red is reused
+    if ((threadIdx.x & 63) == 0) s_red[wave] = wmin;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        float m = s_red[0];
+        for (int w = 1; w < kClusterWaves * SPLIT; ++w)
+            m = s_red[w] < m ? s_red[w] : m;
+        atomicMinPos(a.minDt, m);
+    }
+}
+
 // LDS capacity per kernel (records of 16 / 20 / 32 / 36 / 80 B): the momentum union fills the CU's 160 KiB with
 // one workgroup; the lighter kernels keep two or more workgroups per CU.  SPLIT waves share each group's lists so a
 // CU holds enough waves to reach the VALU's two-cycle issue (one wave alone issues every four cycles).
@@ -746,6 +862,16 @@ void momentumEnergy(const PairArgs& a, hipStream_t s)
     if (!a.numGroups) return;
     if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME, true><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
     else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+}
+// std propagator: the IAD kernel without velocity derivatives (16 B records), momentum with 68 B records
+constexpr int kChIadStd = 2048, kChMeStd = 2048;
+void iadStd(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) iadDivvCurlvKernel<kChIadStd, SX_SPLIT_IAD, true><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+}
+void momentumStd(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) momentumStdKernel<kChMeStd, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
 
 } // namespace cluster

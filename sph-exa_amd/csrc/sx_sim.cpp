@@ -117,12 +117,14 @@ struct __attribute__((aligned(16))) ReqBox
 // ---- time step --------------------------------------------------------------------------------------------
 
 //! rhoTimestep (ts_global.hpp:72-94) and the rank-local part of computeTimestep (:97-112)
-__global__ void dtCandidateKernel(Scalars* s, double Krho, double maxDtIncrease, double g, double eps, double etaAcc)
+//! useRho = 0: the std propagator, which never sets minDtRho (std_hydro.hpp:170-178: stays INFINITY)
+__global__ void dtCandidateKernel(Scalars* s, double Krho, double maxDtIncrease, double g, double eps, double etaAcc,
+                                  int useRho)
 {
     unsigned u = s->maxDivvU;
     u          = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
     float maxDivv   = __uint_as_float(u);
-    s->minDtRho     = Krho / (double)fabsf(maxDivv);
+    s->minDtRho     = useRho ? Krho / (double)fabsf(maxDivv) : INFINITY;
     s->minDtCourant = (double)s->courant;
     double minDtAcc = INFINITY;
     if (g != 0.0) minDtAcc = etaAcc * sqrt(eps / sqrt(__longlong_as_double((long long)s->maxAccSqBits)));
@@ -379,9 +381,11 @@ struct sx_sim
     float *   xm, *kx, *gradh, *prho, *c, *divv, *curlv, *c11, *c12, *c13, *c22, *c23, *c33, *ax, *ay, *az;
     double*   du;
     float*    dV[6]{}; // dV11, dV12, dV13, dV22, dV23, dV33 (avClean only)
+    float *   rho{nullptr}, *pres{nullptr}; // std propagator only (HydroProp DependentFields rho, p)
     RecX*     rx;
     RecV*     rv;
     RecT*     rt;
+    RecS*     rs; // std: {rho, p} records, aliasing rt (the std step has no xm/kx/prho/alpha)
     RecC*     rc;
     NbLists   nb;
     uint32_t* stats;
@@ -467,9 +471,15 @@ void allocFields(sx_sim* s, size_t cap)
         s->dV[4] = a.get<float>("dV23", cap);
         s->dV[5] = a.get<float>("dV33", cap);
     }
+    if (s->p.propagator == 1)
+    {
+        s->rho  = a.get<float>("rho", cap);
+        s->pres = a.get<float>("p", cap);
+    }
     s->rx    = a.get<RecX>("rx", cap);
     s->rv    = a.get<RecV>("rv", cap);
     s->rt    = a.get<RecT>("rt", cap);
+    s->rs    = reinterpret_cast<RecS*>(s->rt);
     s->rc    = a.get<RecC>("rc", cap);
     auto spare = [&](auto*& field, const char* tag) {
         using T = std::remove_reference_t<decltype(*field)>;
@@ -546,6 +556,7 @@ PairArgs simPairArgs(sx_sim* s)
     a.ramp           = s->p.ramp;
     a.Kcour          = (float)s->p.Kcour;
     a.dV11 = s->dV[0], a.dV12 = s->dV[1], a.dV13 = s->dV[2], a.dV22 = s->dV[3], a.dV23 = s->dV[4], a.dV33 = s->dV[5];
+    a.rs   = s->rs;
     a.avClean = s->p.avClean ? 1 : 0;
     return a;
 }
@@ -926,6 +937,8 @@ extern "C"
         f->vy    = s->vy + o;
         f->vz    = s->vz + o;
         f->prho  = s->prho + o;
+        f->rho   = s->rho ? s->rho + o : nullptr;
+        f->p     = s->pres ? s->pres + o : nullptr;
         f->h     = s->h + o;
         f->m     = s->m + o;
         f->c     = s->c + o;
@@ -1042,59 +1055,103 @@ extern "C"
 
         const size_t n  = s->n;
         PairArgs     pa = simPairArgs(s);
-        // ---- XMass
-        packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
-        SIM_HIP(hipEventRecord(s->kev[2], st));
-        H.xmass(pa, st);
-        SIM_HIP(hipEventRecord(s->kev[3], st));
-        if (int e = haloExchange(s, {{s->xm, 4}}, st)) return e;
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- VeDefGradh
-        packT(n, s->xm, nullptr, nullptr, nullptr, s->rt, st);
-        SIM_HIP(hipEventRecord(s->kev[4], st));
-        H.veDefGradh(pa, st);
-        SIM_HIP(hipEventRecord(s->kev[5], st));
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- EOS, then the v/prho/c/kx halo exchange
-        EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
-                   s->gradh, s->prho, s->c, nullptr, nullptr};
-        H.eos(ea, st);
-        if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}}, st))
-            return e;
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- IAD + divv/curlv, rho time-step, then the c_ij/divv exchange
-        packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
-        packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
-        SIM_HIP(hipEventRecord(s->kev[6], st));
-        H.iadDivvCurlv(pa, st);
-        SIM_HIP(hipEventRecord(s->kev[7], st));
-        SIM_HIP(maxFloat(s->divv, (uint32_t)s->first, (uint32_t)s->last, &s->sc->maxDivvU, st));
-        if (int e = haloExchange(
-                s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}}, st))
-            return e;
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- AV switches, then the alpha exchange
-        packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, s->divv, s->rc, st);
-        SIM_HIP(hipEventRecord(s->kev[8], st));
-        H.avSwitches(pa, st);
-        SIM_HIP(hipEventRecord(s->kev[9], st));
-        if (s->p.avClean)
+        if (s->p.propagator == 1)
         {
-            // the reference exchanges dV11,dV12,dV22,dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo
-            // dV13 undefined; all six are exchanged here so the result does not depend on the decomposition
-            if (int e = haloExchange(s, {{s->dV[0], 4}, {s->dV[1], 4}, {s->dV[2], 4}, {s->dV[3], 4}, {s->dV[4], 4},
-                                         {s->dV[5], 4}, {s->alpha, 4}},
+            // ---- HydroProp::computeForces (std_hydro.hpp:124-166): density, EOS, [v,rho,p,c] halos, IAD,
+            //      [c_ij] halos, momentum + energy.  The stage/kernel event slots follow the VE order:
+            //      density in "xmass", IAD in "iadDivvCurlv", momentumEnergySTD in "momentumEnergy".
+            packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+            SIM_HIP(hipEventRecord(s->kev[2], st));
+            PairArgs da = pa;
+            da.xm       = s->rho; // computeDensity: xmass written to rho (xmass_gpu.cu:151-153)
+            H.xmass(da, st);
+            H.xmassToRho((uint32_t)s->first, (uint32_t)s->last, s->m, s->rho, st);
+            SIM_HIP(hipEventRecord(s->kev[3], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            SIM_HIP(hipEventRecord(s->kev[4], st));
+            SIM_HIP(hipEventRecord(s->kev[5], st));
+            EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, nullptr, nullptr,
+                       nullptr, nullptr, s->c, s->rho, s->pres};
+            H.eosStd(ea, st);
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->rho, 4}, {s->pres, 4}, {s->c, 4}},
                                      st))
                 return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
+            packS(n, s->rho, s->pres, s->rs, st);
+            SIM_HIP(hipEventRecord(s->kev[6], st));
+            H.iadStd(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[7], st));
+            if (int e = haloExchange(s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}},
+                                     st))
+                return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, nullptr, s->rc, st);
+            SIM_HIP(hipEventRecord(s->kev[8], st));
+            SIM_HIP(hipEventRecord(s->kev[9], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            SIM_HIP(hipEventRecord(s->kev[10], st));
+            H.momentumStd(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[11], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
         }
-        else if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
-        // ---- momentum + energy
-        packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
-        SIM_HIP(hipEventRecord(s->kev[10], st));
-        H.momentumEnergy(pa, st);
-        SIM_HIP(hipEventRecord(s->kev[11], st));
-        SIM_HIP(hipEventRecord(s->ev[ev++], st));
+        else
+        {
+            // ---- XMass
+            packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+            SIM_HIP(hipEventRecord(s->kev[2], st));
+            H.xmass(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[3], st));
+            if (int e = haloExchange(s, {{s->xm, 4}}, st)) return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- VeDefGradh
+            packT(n, s->xm, nullptr, nullptr, nullptr, s->rt, st);
+            SIM_HIP(hipEventRecord(s->kev[4], st));
+            H.veDefGradh(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[5], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- EOS, then the v/prho/c/kx halo exchange
+            EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
+                       s->gradh, s->prho, s->c, nullptr, nullptr};
+            H.eos(ea, st);
+            if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}}, st))
+                return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- IAD + divv/curlv, rho time-step, then the c_ij/divv exchange
+            packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
+            packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
+            SIM_HIP(hipEventRecord(s->kev[6], st));
+            H.iadDivvCurlv(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[7], st));
+            SIM_HIP(maxFloat(s->divv, (uint32_t)s->first, (uint32_t)s->last, &s->sc->maxDivvU, st));
+            if (int e = haloExchange(
+                    s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}}, st))
+                return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- AV switches, then the alpha exchange
+            packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, s->divv, s->rc, st);
+            SIM_HIP(hipEventRecord(s->kev[8], st));
+            H.avSwitches(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[9], st));
+            if (s->p.avClean)
+            {
+                // the reference exchanges dV11,dV12,dV22,dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo
+                // dV13 undefined; all six are exchanged here so the result does not depend on the decomposition
+                if (int e = haloExchange(s, {{s->dV[0], 4}, {s->dV[1], 4}, {s->dV[2], 4}, {s->dV[3], 4}, {s->dV[4], 4},
+                                             {s->dV[5], 4}, {s->alpha, 4}},
+                                         st))
+                    return e;
+            }
+            else if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- momentum + energy
+            packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
+            SIM_HIP(hipEventRecord(s->kev[10], st));
+            H.momentumEnergy(pa, st);
+            SIM_HIP(hipEventRecord(s->kev[11], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+        }
         // ---- self-gravity (ve_hydro.hpp:193-202): upsweep + traversal on the step's tree, added to ax, ay, az
         SIM_HIP(hipEventRecord(s->kev[12], st));
         if (s->p.g != 0.0)
@@ -1127,7 +1184,8 @@ extern "C"
         SIM_HIP(hipEventRecord(s->kev[13], st));
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         // ---- integrate: global time-step, positions, h
-        dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease, s->p.g, s->p.eps, s->p.etaAcc);
+        dtCandidateKernel<<<1, 1, 0, st>>>(s->sc, s->p.Krho, s->p.maxDtIncrease, s->p.g, s->p.eps, s->p.etaAcc,
+                                           s->p.propagator != 1);
         if (dist) SIM_COMM(s->comm->allreduceMinF64(&s->sc->dtCand, 1, st));
         dtApplyKernel<<<1, 1, 0, st>>>(s->sc);
         PosArgs qa{};

@@ -543,6 +543,11 @@ void packT(size_t n, const float* xm, const float* kx, const float* prho, const 
 {
     if (n) packTKernel<<<grid(n), 256, 0, s>>>(n, xm, kx, prho, alpha, out);
 }
+void packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s)
+{
+    static_assert(sizeof(RecS) == sizeof(RecT) && alignof(RecS) == alignof(RecT), "RecS shares the RecT packer");
+    if (n) packTKernel<<<grid(n), 256, 0, s>>>(n, rho, p, nullptr, nullptr, reinterpret_cast<RecT*>(out));
+}
 void packC(size_t n, const float* c11, const float* c12, const float* c13, const float* c22, const float* c23,
            const float* c33, const float* divv, RecC* out, hipStream_t s)
 {

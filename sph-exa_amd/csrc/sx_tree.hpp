@@ -210,6 +210,7 @@ void       packT(size_t n, const float* xm, const float* kx, const float* prho, 
                  hipStream_t s);
 void       packC(size_t n, const float* c11, const float* c12, const float* c13, const float* c22, const float* c23,
                  const float* c33, const float* divv, RecC* out, hipStream_t s);
+void       packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s);
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
 //! floats of the prefilter record buffer for n particles (pairs of 8 floats + one padded chunk)

@@ -263,7 +263,63 @@ void computeMomentumEnergy(const GroupView& grp, float* groupDt, Dataset& d, con
     d.minDtCourant = minDt;
 }
 
-//! sph_gpu.hpp:78 (update_h_gpu.cu:49-60)
+//! sph_gpu.hpp:31-32 (hydro_ve/xmass_gpu.cu:150-164): std density -- search + h iteration, XMass into rho,
+//! rho = m / rho
+template<class GroupView, class Dataset, class Box>
+void computeDensity(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    auto t = sa::toTree(d.treeView);
+    sa::check(sx_density(sa::context(), &g, &f, &p, &b, &t), "computeDensity");
+}
+
+//! sph_gpu.hpp:46-47 (hydro_std/eos_gpu.cu:54-62)
+template<class Tu, class Trho, class Tp, class Tc>
+void computeEOS_HydroStd(size_t firstParticle, size_t lastParticle, Trho mui, Tu gamma, const Tu* temp, const Trho* m,
+                         Trho* rho, Tp* p, Tc* c)
+{
+    namespace sa = sphexa_amd;
+    sa::check(sx_eos_std(sa::context(), (uint32_t)firstParticle, (uint32_t)lastParticle, (float)mui, (double)gamma,
+                         temp, m, rho, p, c),
+              "computeEOS_HydroStd");
+}
+
+} // namespace sph::cuda
+
+namespace sph
+{
+
+//! sph_gpu.hpp:19-20 (hydro_std/iad_gpu.cu:111-124)
+template<class GroupView, class Dataset, class Box>
+void computeIADGpu(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    auto f = sa::toFields(d);
+    auto p = sa::toParams(d);
+    auto b = sa::toBox(box);
+    sa::check(sx_iad(sa::context(), &g, &f, &p, &b), "computeIADGpu");
+}
+
+//! sph_gpu.hpp:22-23 (hydro_std/momentum_energy_gpu.cu:109-129): writes ax,ay,az,du and d.minDtCourant
+template<class GroupView, class Dataset, class Box>
+void computeMomentumEnergyStdGpu(const GroupView& grp, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    auto  g = sa::toGroups(grp);
+    auto  f = sa::toFields(d);
+    auto  p = sa::toParams(d);
+    auto  b = sa::toBox(box);
+    float minDt;
+    sa::check(sx_momentum_energy_std(sa::context(), &g, &f, &p, &b, &minDt), "computeMomentumEnergyStdGpu");
+    d.minDtCourant = minDt;
+}
+
+//! sph_gpu.hpp:71-72 (update_h_gpu.cu:49-60)
 template<class GroupView, class Th>
 void updateSmoothingLengthGpu(const GroupView& grp, unsigned ng0, const unsigned* nc, Th* h)
 {
@@ -272,4 +328,4 @@ void updateSmoothingLengthGpu(const GroupView& grp, unsigned ng0, const unsigned
               "updateSmoothingLengthGpu");
 }
 
-} // namespace sph::cuda
+} // namespace sph

@@ -30,7 +30,8 @@ class SxParams(C.Structure):
                 ("Krho", C.c_double), ("gamma", C.c_double), ("muiConst", C.c_float), ("alphamin", C.c_float),
                 ("alphamax", C.c_float), ("decay_constant", C.c_float), ("Atmin", C.c_float),
                 ("Atmax", C.c_float), ("ramp", C.c_float), ("maxDtIncrease", C.c_double), ("avClean", C.c_int32),
-                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double)]
+                ("theta", C.c_float), ("g", C.c_double), ("eps", C.c_double), ("etaAcc", C.c_double),
+                ("propagator", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -139,6 +140,14 @@ def lib():
                                          C.POINTER(SxBox), C.POINTER(C.c_float)]),
         "sx_momentum_energy_avclean": (C.c_int, [vp, C.POINTER(SxGroups), vp, C.POINTER(SxFields),
                                                  C.POINTER(SxParams), C.POINTER(SxBox), C.POINTER(C.c_float)]),
+        "sx_density": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                 C.POINTER(SxBox), C.POINTER(SxTree)]),
+        "sx_density_only": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                      C.POINTER(SxBox)]),
+        "sx_eos_std": (C.c_int, [vp, u32, u32, C.c_float, C.c_double, vp, vp, vp, vp, vp]),
+        "sx_iad": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams), C.POINTER(SxBox)]),
+        "sx_momentum_energy_std": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                             C.POINTER(SxBox), C.POINTER(C.c_float)]),
         "sx_positions": (C.c_int, [vp, u32, u32, C.c_double, C.c_double, C.POINTER(SxFields), C.c_double,
                                    C.c_float, C.POINTER(SxBox)]),
         "sx_update_h": (C.c_int, [vp, u32, u32, u32, vp, vp]),
@@ -198,14 +207,16 @@ def halo_layout(recv_counts, rank, num_local):
     return off, tuple(int(v) for v in out)
 
 
-def default_params(K=None, ngmax=150, ng0=100, av_clean=False, g=0.0, theta=0.5):
-    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> in sx_sim."""
+def default_params(K=None, ngmax=150, ng0=100, av_clean=False, g=0.0, theta=0.5, std=False):
+    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> and std the std
+    propagator (HydroProp) in sx_sim."""
     if K is None:
         K = lib().sx_kernel_constant()
     return SxParams(K=K, ng0=ng0, ngmax=ngmax, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0, alphamin=0.05,
                     alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
                     ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
-                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2)
+                    avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2,
+                    propagator=1 if std else 0)
 
 
 def make_box(lim, bnd):
@@ -286,8 +297,9 @@ class DeviceArray:
 class DeviceState:
     """A full ParticlesData-like device field set built from a host dict of numpy arrays."""
 
-    def __init__(self, ctx, host, grad_v=False):
-        """grad_v: also allocate the velocity gradient dV11..dV33 (GradVFields of the avClean propagator)"""
+    def __init__(self, ctx, host, grad_v=False, std=False):
+        """grad_v: also allocate the velocity gradient dV11..dV33 (GradVFields of the avClean propagator);
+        std: also allocate rho and p (DependentFields of the std propagator, std_hydro.hpp:78-79)"""
         self.ctx = ctx
         n = len(host["x"])
         self.n = n
@@ -296,8 +308,8 @@ class DeviceState:
         self.fields.n = n
         grad = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
         for name, _ in FIELD_ORDER:
-            if name in ("rho", "p", "tdpdTrho", "u", "mue", "mui", "cv", "markRamp", "rung") or \
-                    (name in grad and not grad_v):
+            if name in ("tdpdTrho", "u", "mue", "mui", "cv", "markRamp", "rung") or \
+                    (name in grad and not grad_v) or (name in ("rho", "p") and not std):
                 continue
             dt = DTYPES[name]
             if name in host:

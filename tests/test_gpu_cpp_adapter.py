@@ -66,3 +66,55 @@ def test_cpp_adapter_compute_forces(tmp_path):
         tol = 2e-5 * scale + 1e-5 * field_max
         assert np.all(np.abs(a - b) <= tol), (k, np.max(np.abs(a - b) / (scale + 1e-300)))
     assert mdt == pytest.approx(rdt, rel=1e-6)
+
+
+F32_STD = ["h", "rho", "p", "c", "c11", "c12", "c13", "c22", "c23", "c33", "ax", "ay", "az"]
+
+
+def test_cpp_adapter_std_forces(tmp_path):
+    """HydroProp::computeForces through computeDensity / computeEOS_HydroStd / computeIADGpu /
+    computeMomentumEnergyStdGpu of the C++ mirror, against the oracle's std kernels"""
+    if not os.path.exists(EXE):
+        pytest.fail("ve_forces not built (make -C sph-exa_amd)")
+    ora = po.load_oracle()
+    p = ora.params(std=True)
+    st, obox = po.sedov_state(14)
+    ora.step(st, obox, params=p)
+    ora.step(st, obox, params=p)
+    gutil.sorted_state(st, obox, ora)
+    n = st.n
+    with open(tmp_path / "in.bin", "wb") as f:
+        f.write(np.uint64(n).tobytes())
+        for k in ("x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "alpha"):
+            f.write(st.arrays[k].tobytes())
+    r = subprocess.run([EXE, str(tmp_path / "in.bin"), str(tmp_path / "out.bin"), "std"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    raw = open(tmp_path / "out.bin", "rb").read()
+    got = {"nc": np.frombuffer(raw, np.uint32, n, 0)}
+    off = 4 * n
+    for k in F32_STD:
+        got[k] = np.frombuffer(raw, np.float32, n, off)
+        off += 4 * n
+    got["du"] = np.frombuffer(raw, np.float64, n, off)
+    off += 8 * n
+    mdt = np.frombuffer(raw, np.float64, 1, off)[0]
+
+    ref = st.copy()
+    nbr, nc = ora.find_neighbors(ref, obox, iterate_h=True)
+    ref.nc[:] = nc
+    ora.density(ref, obox, nbr, params=p)
+    ora.eos_std(ref, params=p)
+    ora.iad_std(ref, obox, nbr, params=p)
+    rdt = ora.momentum_energy_std(ref, obox, nbr, params=p)
+    assert np.array_equal(got["nc"], ref.nc) and np.array_equal(got["h"], ref.h)
+    for k in F32_STD[1:] + ["du"]:
+        a, b = got[k].astype(np.float64), ref.arrays[k].astype(np.float64)
+        scale = np.abs(b)
+        if k in ("c12", "c13", "c23"):
+            scale = np.maximum(np.abs(ref.c11), np.abs(ref.c22)).astype(np.float64)
+        if k in ("ax", "ay", "az"):
+            scale = np.sqrt(ref.ax.astype(np.float64) ** 2 + ref.ay ** 2 + ref.az ** 2)
+        tol = 2e-5 * scale + 1e-5 * np.max(np.abs(b))
+        assert np.all(np.abs(a - b) <= tol), (k, np.max(np.abs(a - b) / (scale + 1e-300)))
+    assert mdt == pytest.approx(rdt, rel=1e-6)
