@@ -129,9 +129,6 @@ def main():
 
         ic_arrays, lim, bnd, dt0 = getattr(ic, args.init)(side)
         n_total = ic_arrays["x"].size
-        if args.init == "evrard" and world > 1:
-            raise SystemExit("evrard (self-gravity) runs on one GPU: multi-rank gravity needs the global multipole "
-                             "exchange (DESIGN.md 9)")
     device = 0
     if args.backend != "host":
         import torch  # device_count() does not initialise the GPU runtime
@@ -233,6 +230,9 @@ def main():
                    "parallelism": "1 GPU" if world == 1 else
                    f"{world} GPUs: SFC domain decomposition, halo + particle exchange over {transport}",
                    "halos_per_gpu": sim.layout()["n"] - n_local,
+                   **({"gravity_halos_per_gpu": sim.gravity_stats()["halos"],
+                       "gravity_far_cells": sim.gravity_stats()["far_cells"]} if world > 1 and args.init == "evrard"
+                      else {}),
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
         "roofline": {"bound": "hbm", "kernel": mom_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(mom_kernel, n_local),

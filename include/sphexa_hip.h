@@ -328,6 +328,9 @@ int    sx_sim_scalars(sx_sim* sim, double out[6]);
 /*! per-stage device time of the last step (ms) measured with HIP events, names in stage order */
 int    sx_sim_stage_times(sx_sim* sim, float* ms, int cap, const char** names);
 int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);
+/*! multi-rank self-gravity of the last step: {gravity halos received, remote level-6 cells used as far-field
+ *  multipoles, remote cells in total} (zeros on one rank) */
+int    sx_sim_gravity_stats(sx_sim* sim, uint64_t out[3]);
 /*! device time (ms) of each hot kernel alone in the last step (HIP events on the launch stream, bracketing just the
  *  launch): findNeighbors, xmass, veDefGradh, iadDivvCurlv, avSwitches, momentumEnergy */
 int    sx_sim_kernel_times(sx_sim* sim, float* ms, int cap, const char** names);

@@ -417,3 +417,18 @@ def total_energy(st):
     v2 = st.vx.astype(np.float64) ** 2 + st.vy.astype(np.float64) ** 2 + st.vz.astype(np.float64) ** 2
     m = st.m.astype(np.float64)
     return float(np.sum(0.5 * m * v2) + np.sum(m * cv * st.temp))
+
+
+def converge_h(lib, st, box, bucket=64):
+    """set st.h to the smoothing lengths after the h-nc iteration of the first search (findNeighborsSph) on this
+    state, in the state's own order: the following steps then start from converged h, so a decomposed run (whose
+    halos keep the pre-iteration h, as in the reference) sees the same h as a single domain"""
+    tmp = st.copy()
+    keys = lib.sfc_keys(tmp, box).copy()
+    srt = np.argsort(keys, kind="stable")
+    for name in ("x", "y", "z", "h"):
+        tmp.arrays[name][:] = tmp.arrays[name][srt]
+    tmp.keys[:] = keys[srt]
+    lib.find_neighbors(tmp, box, bucket=bucket, iterate_h=True)
+    st.h[srt] = tmp.h
+    return st

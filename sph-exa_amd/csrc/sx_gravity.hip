@@ -245,10 +245,13 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
                             (((bv >> 32) & 0xffffull) ? 4u : 0u) | (((bv >> 48) & 0xffffull) ? 8u : 0u);
 
-    // evaluateMac: true = the target box is inside the node's acceptance radius (descend / P2P)
-    auto violates = [&](int node, unsigned mask) -> unsigned {
+    // evaluateMac: true = the target box is inside the node's acceptance radius (descend / P2P).  Massless nodes
+    // (mac^2 = 0, setMac) never violate and are dropped by the caller: their M2P adds exactly zero, and skipping it
+    // avoids 0 * inf when a target sits on the zero expansion center of an empty node.
+    auto violates = [&](int node, unsigned mask, bool& massless) -> unsigned {
         const double* com = a.centers4 + 4 * (size_t)node;
         const double  c0 = com[0], c1 = com[1], c2 = com[2], mac2 = fabs(com[3]);
+        massless          = mac2 == 0.0;
         unsigned      v   = 0;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq)
@@ -319,8 +322,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
 
     // root (singleTraversal, traversal.hpp:69-80)
     {
-        const unsigned v = violates(0, qValid);
-        if (qValid & ~v) { s_m2p[wave][0] = (0 << 4) | (int)(qValid & ~v), nM = 1; }
+        bool           massless;
+        const unsigned v = violates(0, qValid, massless);
+        if ((qValid & ~v) && !massless) { s_m2p[wave][0] = (0 << 4) | (int)(qValid & ~v), nM = 1; }
         if (v)
         {
             if (a.childOffsets[0] == 0) { s_p2p[wave][0] = (int)v, nP = 1; }
@@ -339,8 +343,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
         const int      parent = e >> 4;
         const unsigned pmask  = ok ? (unsigned)(e & 15) : 0u;
         const int      child  = ok ? a.childOffsets[parent] + oct : 0;
-        const unsigned v      = ok ? violates(child, pmask) : 0u;
-        const unsigned accept = pmask & ~v;
+        bool           massless = true;
+        const unsigned v        = ok ? violates(child, pmask, massless) : 0u;
+        const unsigned accept   = massless ? 0u : pmask & ~v;
         const bool     leaf   = ok && a.childOffsets[child] == 0;
         append(s_m2p[wave], nM, accept != 0, (child << 4) | (int)accept);
         append(s_p2p[wave], nP, v != 0 && leaf, (child << 4) | (int)v);
@@ -379,7 +384,146 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
 
 inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
+// ---- multi-rank gravity: level-6 cell multipoles, near/far classification, far tree --------------------------
+
+//! mass center, MAC radius (setMac with the cell's geometry from the far tree) and quadrupole of each local cell
+__global__ void cellMomentsKernel(const double* x, const double* y, const double* z, const float* m,
+                                  const uint32_t* cellBeg, const uint32_t* cellIds, int nCells,
+                                  const int32_t* farLeafToNode, const double* geoC, const double* geoS, float invTheta,
+                                  GCell* out)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nCells) return;
+    const uint32_t b = cellBeg[k], e = cellBeg[k + 1];
+    double         c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (uint32_t i = b; i < e; ++i)
+    {
+        const double w = (double)m[i];
+        c0 += w * x[i];
+        c1 += w * y[i];
+        c2 += w * z[i];
+        c3 += w;
+    }
+    const double invM = c3 != 0.0 ? 1.0 / c3 : 0.0;
+    GCell        g{};
+    g.com[0] = c0 * invM, g.com[1] = c1 * invM, g.com[2] = c2 * invM;
+    const int     node = farLeafToNode[cellIds[k]];
+    const double* gc   = geoC + 3 * (size_t)node;
+    const double* gs   = geoS + 3 * (size_t)node;
+    const double  dx = g.com[0] - gc[0], dy = g.com[1] - gc[1], dz = g.com[2] - gc[2];
+    const double  smax = fmax(fmax(gs[0], gs[1]), gs[2]);
+    const double  mac  = 2.0 * smax * (double)invTheta + sqrt(dx * dx + (dy * dy + dz * dz));
+    g.mac2             = c3 != 0.0 ? mac * mac : 0.0;
+    float gv[8]        = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = b; i < e; ++i)
+    {
+        const double m_i = (double)m[i];
+        const double rx = x[i] - g.com[0], ry = y[i] - g.com[1], rz = z[i] - g.com[2];
+        gv[0] = (float)((double)gv[0] + m_i);
+        gv[1] = (float)((double)gv[1] + rx * rx * m_i);
+        gv[2] = (float)((double)gv[2] + rx * ry * m_i);
+        gv[3] = (float)((double)gv[3] + rx * rz * m_i);
+        gv[4] = (float)((double)gv[4] + ry * ry * m_i);
+        gv[5] = (float)((double)gv[5] + ry * rz * m_i);
+        gv[6] = (float)((double)gv[6] + rz * rz * m_i);
+    }
+    const float traceQ = gv[1] + gv[4] + gv[6];
+    gv[7]              = traceQ;
+    gv[1]              = 3 * gv[1] - traceQ;
+    gv[4]              = 3 * gv[4] - traceQ;
+    gv[6]              = 3 * gv[6] - traceQ;
+    gv[2] *= 3;
+    gv[3] *= 3;
+    gv[5] *= 3;
+    for (int q = 0; q < 8; ++q)
+        g.q[q] = gv[q];
+    g.cell  = cellIds[k];
+    g.count = e - b;
+    out[k]  = g;
+}
+
+//! one wave per remote cell: near[k] = 1 if the cell violates the vector MAC for any target box (c, s: center and
+//! half-size, stride 8 doubles) -- such a cell's particles are needed as gravity halos
+__global__ void cellNearKernel(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near)
+{
+    const int k    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (k >= nCells) return;
+    const GCell& g   = cells[k];
+    bool         hit = false;
+    if (g.mac2 != 0.0)
+        for (int b = lane; b < nBoxes && !hit; b += 64)
+        {
+            const double* B  = boxes + 8 * (size_t)b;
+            double        d0 = fabs(B[0] - g.com[0]) - B[3], d1 = fabs(B[1] - g.com[1]) - B[4],
+                   d2 = fabs(B[2] - g.com[2]) - B[5];
+            d0 = d0 > 0 ? d0 : 0;
+            d1 = d1 > 0 ? d1 : 0;
+            d2 = d2 > 0 ? d2 : 0;
+            hit = d0 * d0 + (d1 * d1 + d2 * d2) < g.mac2;
+        }
+    const bool any = __ballot(hit) != 0;
+    if (lane == 0) near[k] = any ? 1u : 0u;
+}
+
+//! far-tree leaves: cells with far[k] set get their mass center / mass and quadrupole, all other leaves are massless
+__global__ void farLeavesKernel(GravArgs a, const GCell* cells, const uint32_t* far, int nCells)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nCells || !far[k]) return;
+    const GCell& g    = cells[k];
+    const int    node = a.leafToNode[g.cell];
+    double*      c    = a.centers4 + 4 * (size_t)node;
+    c[0] = g.com[0], c[1] = g.com[1], c[2] = g.com[2], c[3] = (double)g.q[0];
+    float* o = a.multipoles + 8 * (size_t)node;
+    for (int q = 0; q < 8; ++q)
+        o[q] = g.q[q];
+}
+
 } // namespace
+
+hipError_t cellMoments(const double* x, const double* y, const double* z, const float* m, const uint32_t* cellBeg,
+                       const uint32_t* cellIds, int nCells, const int32_t* farLeafToNode, const double* geoC,
+                       const double* geoS, float invTheta, GCell* out, hipStream_t s)
+{
+    if (nCells > 0)
+        cellMomentsKernel<<<grid(nCells), 256, 0, s>>>(x, y, z, m, cellBeg, cellIds, nCells, farLeafToNode, geoC, geoS,
+                                                       invTheta, out);
+    return hipGetLastError();
+}
+
+hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near, hipStream_t s)
+{
+    if (nCells > 0) cellNearKernel<<<grid((size_t)nCells * 64), 256, 0, s>>>(cells, nCells, boxes, nBoxes, near);
+    return hipGetLastError();
+}
+
+hipError_t farTreeLeafMap(const GravArgs& a, hipStream_t s)
+{
+    leafToNodeKernel<<<grid(a.numNodes), 256, 0, s>>>(a.childOffsets, a.internalToLeaf, a.numNodes, a.leafToNode);
+    return hipGetLastError();
+}
+
+hipError_t farUpsweep(const GravArgs& a, const GCell* cells, const uint32_t* far, int nCells,
+                      const int32_t* levelRangeHost, hipStream_t s)
+{
+    if (a.numNodes <= 0) return hipSuccess;
+    (void)hipMemsetAsync(a.centers4, 0, sizeof(double) * 4 * (size_t)a.numNodes, s);
+    (void)hipMemsetAsync(a.multipoles, 0, sizeof(float) * 8 * (size_t)a.numNodes, s);
+    if (nCells > 0) farLeavesKernel<<<grid(nCells), 256, 0, s>>>(a, cells, far, nCells);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
+        if (e > b) upsweepCentersKernel<<<grid(e - b), 256, 0, s>>>(a, b, e);
+    }
+    setMacKernel<<<grid(a.numNodes), 256, 0, s>>>(a);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
+        if (e > b) upsweepMultipolesKernel<<<grid(e - b), 256, 0, s>>>(a, b, e);
+    }
+    return hipGetLastError();
+}
 
 hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipStream_t s)
 {

@@ -31,6 +31,32 @@ struct GravArgs
     uint32_t* err;        // bit 0: traversal stack exhausted
 };
 
+//! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi
+//! order, q[0] = mass), cell index (key >> 45) and particle count
+struct __attribute__((aligned(16))) GCell
+{
+    double   com[3];
+    double   mac2;
+    float    q[8];
+    uint32_t cell, count;
+    uint32_t pad[2];
+};
+static_assert(sizeof(GCell) == 80, "GCell layout");
+
+//! cells [cellBeg[k], cellBeg[k+1]) of key-sorted particles; geometry from the far tree's leaf nodes
+hipError_t cellMoments(const double* x, const double* y, const double* z, const float* m, const uint32_t* cellBeg,
+                       const uint32_t* cellIds, int nCells, const int32_t* farLeafToNode, const double* geoC,
+                       const double* geoS, float invTheta, GCell* out, hipStream_t s);
+//! near[k] = 1 if cell k violates the vector MAC for any of the target boxes (center[3], half-size[3], stride 8)
+hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near,
+                         hipStream_t s);
+//! a.leafToNode of a tree (leaf index -> node index)
+hipError_t farTreeLeafMap(const GravArgs& a, hipStream_t s);
+//! far tree (uniform level-6 octree): leaves of the cells with far[k] set carry their moments, all others are
+//! massless; then the mass-center / MAC / M2M upsweep
+hipError_t farUpsweep(const GravArgs& a, const GCell* cells, const uint32_t* far, int nCells,
+                      const int32_t* levelRangeHost, hipStream_t s);
+
 //! expansion centers, MAC radii and multipoles of every node; levelRangeHost: kMaxLevel + 2 node offsets per level
 hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipStream_t s);
 //! adds G * (M2P + P2P) to ax, ay, az of [first, last) and 0.5 sum G m phi to *egrav

@@ -355,6 +355,113 @@ __global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, siz
 
 static inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
+// ---- multi-rank gravity helpers (distributedGravity) ----------------------------------------------------------
+
+constexpr int kCellShift = 63 - kHistBits; // level-6 cell of a key: the global histogram bins, one owner each
+
+//! source record of a gravity halo: coordinates, mass and smoothing length
+struct __attribute__((aligned(16))) GPart
+{
+    double x, y, z;
+    float  m, h;
+};
+
+__global__ void farKeysKernel(uint64_t* keys, size_t n)
+{
+    size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (c < n) keys[c] = (uint64_t)c << kCellShift;
+}
+
+__global__ void cellFlagKernel(const uint64_t* keys, size_t n, uint32_t* flag)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i > n) return;
+    flag[i] = (i < n && (i == 0 || (keys[i] >> kCellShift) != (keys[i - 1] >> kCellShift))) ? 1u : 0u;
+}
+
+__global__ void cellScatterKernel(const uint64_t* keys, const uint32_t* flag, const uint32_t* scan, size_t n,
+                                  uint32_t* cellBeg, uint32_t* cellIds)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i < n && flag[i])
+    {
+        cellBeg[scan[i]] = (uint32_t)i;
+        cellIds[scan[i]] = (uint32_t)(keys[i] >> kCellShift);
+    }
+    if (i == n) cellBeg[scan[n]] = (uint32_t)n;
+}
+
+__global__ void nearToFarKernel(const uint32_t* nearFlag, size_t n, uint32_t* farFlag, uint32_t* reqFlag)
+{
+    size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (k > n) return;
+    const uint32_t v = k < n ? nearFlag[k] : 0u;
+    if (k < n) farFlag[k] = 1u - v;
+    reqFlag[k] = v;
+}
+
+__global__ void reqScatterKernel(const GCell* cells, const uint32_t* reqFlag, const uint32_t* scan, size_t n,
+                                 uint32_t* reqIds)
+{
+    size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (k < n && reqFlag[k]) reqIds[scan[k]] = cells[k].cell;
+}
+
+//! v[q] = scan[off[q]] for the P+1 segment boundaries
+__global__ void segmentAtKernel(const uint32_t* scan, const uint64_t* off, int P, uint32_t* out)
+{
+    int q = threadIdx.x;
+    if (q <= P) out[q] = scan[off[q]];
+}
+
+//! owner side: requested cell -> particle range of the local cell (binary search over the sorted local cell ids)
+__global__ void reqLookupKernel(const uint32_t* req, size_t nReq, const uint32_t* cellIds, const uint32_t* cellBeg,
+                                int nCells, uint32_t* size, uint32_t* beg)
+{
+    size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (k > nReq) return;
+    if (k == nReq)
+    {
+        size[k] = 0;
+        return;
+    }
+    const uint32_t id = req[k];
+    int            lo = 0, hi = nCells;
+    while (lo < hi)
+    {
+        int mid = (lo + hi) >> 1;
+        if (cellIds[mid] < id) lo = mid + 1;
+        else hi = mid;
+    }
+    const bool found = lo < nCells && cellIds[lo] == id;
+    beg[k]           = found ? cellBeg[lo] : 0u;
+    size[k]          = found ? cellBeg[lo + 1] - cellBeg[lo] : 0u;
+}
+
+//! one wave per request: the cell's particles into the send buffer at its scanned offset
+__global__ void gatherCellsKernel(const uint32_t* beg, const uint32_t* size, const uint32_t* off, size_t nReq,
+                                  const double* x, const double* y, const double* z, const float* m, const float* h,
+                                  GPart* out)
+{
+    const size_t k    = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const int    lane = threadIdx.x & 63;
+    if (k >= nReq) return;
+    const uint32_t b = beg[k], c = size[k], o = off[k];
+    for (uint32_t t = lane; t < c; t += 64)
+    {
+        const uint32_t i = b + t;
+        out[o + t]       = GPart{x[i], y[i], z[i], m[i], h[i]};
+    }
+}
+
+__global__ void unpackGPartKernel(const GPart* in, size_t n, double* x, double* y, double* z, float* m, float* h)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GPart p = in[i];
+    x[i] = p.x, y[i] = p.y, z[i] = p.z, m[i] = p.m, h[i] = p.h;
+}
+
 } // namespace
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -372,6 +479,12 @@ struct sx_sim
     Arena          work;
     DevTree        tree;
     DevTree        localTree;
+    // multi-rank gravity: uniform level-6 far tree (built once, own arena) and the per-step near tree over the
+    // locals + gravity halos (own arena, so neither clobbers the SPH tree's "dt.*" buffers)
+    Arena          farMem;
+    Arena          gravWork;
+    DevTree        farTree;
+    DevTree        nearTree;
 
     double *  x, *y, *z, *temp;
     float *   h, *m, *vx, *vy, *vz, *xm1, *ym1, *zm1, *dum1, *alpha;
@@ -416,6 +529,9 @@ struct sx_sim
     std::vector<float>       stageMs;
     sx_nbstats               lastStats{};
     int                      haloRetries{0};
+    uint64_t                 gravHalos{0};    // gravity halos of the last multi-rank step
+    uint64_t                 gravFarCells{0}; // remote level-6 cells taken as far-field multipoles
+    uint64_t                 gravRemoteCells{0};
 
     Fields fields() const { return Fields{x, y, z, temp, h, m, vx, vy, vz, xm1, ym1, zm1, dum1, alpha, id}; }
 };
@@ -784,6 +900,236 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     return SX_OK;
 }
 
+/*! Self-gravity with several ranks (replaces syncGrav + MultipoleHolder::upsweep/traverse of the reference,
+ *  domain.hpp:246-372, multipole_holder.cuh:40-66, and the global multipole exchange of
+ *  ryoanji/interface/global_multipole.hpp).  Sources are split by level-6 SFC cells, each owned by one rank (the
+ *  splitters are histogram-bin boundaries):
+ *   1. every rank forms mass center, MAC radius and quadrupole of its own cells; all cells are all-gathered;
+ *   2. a remote cell that satisfies the vector MAC against every request box of this rank (each box contains 2048
+ *      SFC-consecutive locals) is "far": its multipole is a leaf of the uniform level-6 far tree, whose upsweep and
+ *      Barnes-Hut traversal give the far field (all other leaves massless);
+ *   3. the particles of the remaining ("near") remote cells are fetched from their owners as gravity halos, merged
+ *      with the locals in key order ([lower ranks | locals | higher ranks]) and traversed with the single-rank
+ *      upsweep + traversal on their own tree.
+ *  Each source is counted once (locals and near cells in the near tree, far cells in the far tree); every far-cell
+ *  multipole is accepted by the same MAC the reference applies, so the result matches the single-rank
+ *  Barnes-Hut field within its opening-angle error. */
+int distributedGravity(sx_sim* s, hipStream_t st)
+{
+    sx::Transport* T  = s->comm;
+    const int      P  = T->size(), r = T->rank();
+    const size_t   nl = s->last - s->first;
+    const float    invTheta = 1.0f / s->p.theta;
+    const size_t   nCellsAll = size_t(1) << kHistBits;
+
+    // --- far tree: uniform level-6 octree (one synthetic key per cell, bucket 1), built once
+    if (s->farTree.numLeaves != (int)nCellsAll)
+    {
+        uint64_t* fk = s->gravWork.get<uint64_t>("far.keys", nCellsAll);
+        farKeysKernel<<<grid(nCellsAll), 256, 0, st>>>(fk, nCellsAll);
+        SIM_HIP(buildTree(s->farMem, fk, nCellsAll, 1, s->dbox, s->farTree, st));
+        if (s->farTree.numLeaves != (int)nCellsAll) return SX_ERR_HIP;
+        GravArgs fa{};
+        fa.numLeaves      = s->farTree.numLeaves;
+        fa.numNodes       = s->farTree.numNodes;
+        fa.childOffsets   = s->farTree.childOffsets;
+        fa.internalToLeaf = s->farTree.internalToLeaf;
+        fa.leafToNode     = s->farMem.get<int32_t>("far.leafToNode", nCellsAll);
+        SIM_HIP(farTreeLeafMap(fa, st));
+        uint32_t* lay = s->farMem.get<uint32_t>("far.emptyLayout", nCellsAll + 1);
+        SIM_HIP(hipMemsetAsync(lay, 0, 4 * (nCellsAll + 1), st));
+    }
+    int32_t*  farL2N = s->farMem.get<int32_t>("far.leafToNode", nCellsAll);
+    uint32_t* farLay = s->farMem.get<uint32_t>("far.emptyLayout", nCellsAll + 1);
+    Arena&    W      = s->gravWork;
+
+    // --- 1. local cells: ranges of the key-sorted locals, moments
+    const uint64_t* lkeys = s->keys + s->first;
+    uint32_t*       flag  = W.get<uint32_t>("g.flag", nl + 1);
+    uint32_t*       scan  = W.get<uint32_t>("g.scan", nl + 1);
+    cellFlagKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, nl, flag);
+    size_t tmpB = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nl + 1, st);
+    SIM_HIP(hipcub::DeviceScan::ExclusiveSum(W.get<char>("g.scantmp", tmpB), tmpB, flag, scan, (int)nl + 1, st));
+    uint32_t* hw = W.pinned<uint32_t>("g.host", 2 * (P + 2));
+    SIM_HIP(hipMemcpyAsync(hw, scan + nl, 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    const int nCells  = (int)hw[0];
+    uint32_t* cellBeg = W.get<uint32_t>("g.cellBeg", nCells + 1);
+    uint32_t* cellIds = W.get<uint32_t>("g.cellIds", nCells);
+    cellScatterKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, flag, scan, nl, cellBeg, cellIds);
+    GCell* mine = W.get<GCell>("g.mine", nCells);
+    SIM_HIP(cellMoments(s->x + s->first, s->y + s->first, s->z + s->first, s->m + s->first, cellBeg, cellIds, nCells,
+                        farL2N, s->farTree.centers, s->farTree.sizes, invTheta, mine, st));
+
+    // --- 2. all-gather the cells (rank order = key order)
+    std::vector<uint64_t> cnt(P, (uint64_t)nCells), rcnt;
+    cnt[r] = 0;
+    SIM_COMM(T->exchangeCounts(cnt, rcnt, st, s->cntBuf));
+    std::vector<uint64_t> aOff(P + 1, 0);
+    for (int q = 0; q < P; ++q)
+        aOff[q + 1] = aOff[q] + rcnt[q];
+    const size_t nAll = aOff[P];
+    GCell*       all  = W.get<GCell>("g.all", nAll);
+    {
+        std::vector<uint64_t> sb(P), so(P, 0), rb(P), ro(P);
+        for (int q = 0; q < P; ++q)
+        {
+            sb[q] = cnt[q] * sizeof(GCell);
+            rb[q] = rcnt[q] * sizeof(GCell);
+            ro[q] = aOff[q] * sizeof(GCell);
+        }
+        SIM_COMM(T->alltoallv(mine, sb.data(), so.data(), all, rb.data(), ro.data(), st));
+    }
+
+    // --- 3. near / far classification against this rank's request boxes (distributedSync step 4)
+    const size_t  nChunks = (nl + kChunk - 1) / kChunk;
+    const ReqBox* boxes   = s->work.get<ReqBox>("dom.mybox", nChunks);
+    uint32_t*     nearF   = W.get<uint32_t>("g.near", nAll + 1);
+    uint32_t*     farF    = W.get<uint32_t>("g.far", nAll + 1);
+    uint32_t*     reqF    = W.get<uint32_t>("g.reqFlag", nAll + 1);
+    uint32_t*     reqS    = W.get<uint32_t>("g.reqScan", nAll + 1);
+    SIM_HIP(cellNearFlags(all, (int)nAll, reinterpret_cast<const double*>(boxes), (int)nChunks, nearF, st));
+    nearToFarKernel<<<grid(nAll + 1), 256, 0, st>>>(nearF, nAll, farF, reqF);
+    tmpB = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, reqF, reqS, (int)nAll + 1, st);
+    SIM_HIP(hipcub::DeviceScan::ExclusiveSum(W.get<char>("g.scantmp2", tmpB), tmpB, reqF, reqS, (int)nAll + 1, st));
+    uint32_t* reqIds = W.get<uint32_t>("g.reqIds", nAll);
+    reqScatterKernel<<<grid(nAll), 256, 0, st>>>(all, reqF, reqS, nAll, reqIds);
+    uint64_t* dOff = W.get<uint64_t>("g.aOff", P + 1);
+    uint32_t* dAt  = W.get<uint32_t>("g.at", P + 1);
+    SIM_HIP(hipMemcpyAsync(dOff, aOff.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
+    segmentAtKernel<<<1, 64 * ((P + 64) / 64), 0, st>>>(reqS, dOff, P, dAt);
+    SIM_HIP(hipMemcpyAsync(hw, dAt, 4 * (P + 1), hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> reqCnt(P), reqOff(P), reqRecv;
+    for (int q = 0; q < P; ++q)
+        reqCnt[q] = hw[q + 1] - hw[q], reqOff[q] = hw[q];
+    const uint64_t hwReq = hw[P]; // near (requested) remote cells
+
+    // --- 4. requests to the owners, owners send the cells' particles
+    SIM_COMM(T->exchangeCounts(reqCnt, reqRecv, st, s->cntBuf));
+    std::vector<uint64_t> rrOff(P + 1, 0);
+    for (int q = 0; q < P; ++q)
+        rrOff[q + 1] = rrOff[q] + reqRecv[q];
+    const size_t nReq = rrOff[P];
+    uint32_t*    req  = W.get<uint32_t>("g.req", nReq);
+    {
+        std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
+        for (int q = 0; q < P; ++q)
+            sb[q] = reqCnt[q] * 4, so[q] = reqOff[q] * 4, rb[q] = reqRecv[q] * 4, ro[q] = rrOff[q] * 4;
+        SIM_COMM(T->alltoallv(reqIds, sb.data(), so.data(), req, rb.data(), ro.data(), st));
+    }
+    uint32_t* rsize = W.get<uint32_t>("g.rsize", nReq + 1);
+    uint32_t* rbeg  = W.get<uint32_t>("g.rbeg", nReq + 1);
+    uint32_t* roff  = W.get<uint32_t>("g.roff", nReq + 1);
+    reqLookupKernel<<<grid(nReq + 1), 256, 0, st>>>(req, nReq, cellIds, cellBeg, nCells, rsize, rbeg);
+    tmpB = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, rsize, roff, (int)nReq + 1, st);
+    SIM_HIP(hipcub::DeviceScan::ExclusiveSum(W.get<char>("g.scantmp3", tmpB), tmpB, rsize, roff, (int)nReq + 1, st));
+    SIM_HIP(hipMemcpyAsync(dOff, rrOff.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
+    segmentAtKernel<<<1, 64 * ((P + 64) / 64), 0, st>>>(roff, dOff, P, dAt);
+    SIM_HIP(hipMemcpyAsync(hw, dAt, 4 * (P + 1), hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> pCnt(P), pOff(P), pRecv;
+    for (int q = 0; q < P; ++q)
+        pCnt[q] = hw[q + 1] - hw[q], pOff[q] = hw[q];
+    const size_t nSend = hw[P];
+    GPart*       psend = W.get<GPart>("g.psend", nSend);
+    if (nReq)
+        gatherCellsKernel<<<grid(nReq * 64), 256, 0, st>>>(rbeg, rsize, roff, nReq, s->x + s->first, s->y + s->first,
+                                                           s->z + s->first, s->m + s->first, s->h + s->first, psend);
+    SIM_COMM(T->exchangeCounts(pCnt, pRecv, st, s->cntBuf));
+    uint64_t nLow = 0, nHigh = 0;
+    for (int q = 0; q < P; ++q)
+        (q < r ? nLow : nHigh) += (q == r ? 0 : pRecv[q]);
+    const size_t nG    = nLow + nl + nHigh;
+    GPart*       precv = W.get<GPart>("g.precv", nLow + nHigh);
+    {
+        std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
+        uint64_t              acc = 0;
+        for (int q = 0; q < P; ++q)
+        {
+            sb[q] = pCnt[q] * sizeof(GPart), so[q] = pOff[q] * sizeof(GPart);
+            rb[q] = (q == r ? 0 : pRecv[q]) * sizeof(GPart), ro[q] = acc * sizeof(GPart);
+            acc += (q == r ? 0 : pRecv[q]);
+        }
+        SIM_COMM(T->alltoallv(psend, sb.data(), so.data(), precv, rb.data(), ro.data(), st));
+    }
+
+    // --- 5. near sources: [lower-rank halos | locals | higher-rank halos], key sorted by construction
+    double*   gx = W.get<double>("g.x", nG);
+    double*   gy = W.get<double>("g.y", nG);
+    double*   gz = W.get<double>("g.z", nG);
+    float*    gm = W.get<float>("g.m", nG);
+    float*    gh = W.get<float>("g.h", nG);
+    uint64_t* gk = W.get<uint64_t>("g.keys", nG);
+    if (nLow) unpackGPartKernel<<<grid(nLow), 256, 0, st>>>(precv, nLow, gx, gy, gz, gm, gh);
+    if (nHigh)
+        unpackGPartKernel<<<grid(nHigh), 256, 0, st>>>(precv + nLow, nHigh, gx + nLow + nl, gy + nLow + nl,
+                                                       gz + nLow + nl, gm + nLow + nl, gh + nLow + nl);
+    SIM_HIP(hipMemcpyAsync(gx + nLow, s->x + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
+    SIM_HIP(hipMemcpyAsync(gy + nLow, s->y + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
+    SIM_HIP(hipMemcpyAsync(gz + nLow, s->z + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
+    SIM_HIP(hipMemcpyAsync(gm + nLow, s->m + s->first, 4 * nl, hipMemcpyDeviceToDevice, st));
+    SIM_HIP(hipMemcpyAsync(gh + nLow, s->h + s->first, 4 * nl, hipMemcpyDeviceToDevice, st));
+    SIM_HIP(launchSfcKeys(gx, gy, gz, gk, nG, s->dbox, st));
+    SIM_HIP(buildTree(W, gk, nG, s->bucket, s->dbox, s->nearTree, st));
+
+    GravArgs ga{};
+    ga.first          = (uint32_t)nLow;
+    ga.last           = (uint32_t)(nLow + nl);
+    ga.numLeaves      = s->nearTree.numLeaves;
+    ga.numNodes       = s->nearTree.numNodes;
+    ga.childOffsets   = s->nearTree.childOffsets;
+    ga.internalToLeaf = s->nearTree.internalToLeaf;
+    ga.layout         = s->nearTree.layout;
+    ga.geoCenters     = s->nearTree.centers;
+    ga.geoSizes       = s->nearTree.sizes;
+    ga.leafToNode     = W.get<int32_t>("g.leafToNode", (size_t)s->nearTree.numLeaves);
+    ga.x = gx, ga.y = gy, ga.z = gz, ga.m = gm, ga.h = gh;
+    ga.centers4   = W.get<double>("g.centers", 4 * (size_t)s->nearTree.numNodes);
+    ga.multipoles = W.get<float>("g.multipoles", 8 * (size_t)s->nearTree.numNodes);
+    ga.G          = (float)s->p.g;
+    ga.invTheta   = invTheta;
+    // target i of the near arrays is local particle s->first + (i - nLow)
+    const ptrdiff_t shift = (ptrdiff_t)s->first - (ptrdiff_t)nLow;
+    ga.ax    = s->ax + shift;
+    ga.ay    = s->ay + shift;
+    ga.az    = s->az + shift;
+    ga.egrav = &s->sc->egrav;
+    ga.err   = &s->sc->gravErr;
+    SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
+    SIM_HIP(gravityTraverse(ga, st));
+
+    // --- 6. far field: far cells as leaves of the level-6 tree, traversed by the locals
+    GravArgs fa{};
+    fa.first          = (uint32_t)s->first;
+    fa.last           = (uint32_t)s->last;
+    fa.numLeaves      = s->farTree.numLeaves;
+    fa.numNodes       = s->farTree.numNodes;
+    fa.childOffsets   = s->farTree.childOffsets;
+    fa.internalToLeaf = s->farTree.internalToLeaf;
+    fa.layout         = farLay; // no particles: a far leaf is always accepted (MAC holds for every request box)
+    fa.geoCenters     = s->farTree.centers;
+    fa.geoSizes       = s->farTree.sizes;
+    fa.leafToNode     = farL2N;
+    fa.x = s->x, fa.y = s->y, fa.z = s->z, fa.m = s->m, fa.h = s->h;
+    fa.centers4   = s->farMem.get<double>("far.centers", 4 * (size_t)s->farTree.numNodes);
+    fa.multipoles = s->farMem.get<float>("far.multipoles", 8 * (size_t)s->farTree.numNodes);
+    fa.G          = (float)s->p.g;
+    fa.invTheta   = invTheta;
+    fa.ax = s->ax, fa.ay = s->ay, fa.az = s->az;
+    fa.egrav = &s->sc->egrav;
+    fa.err   = &s->sc->gravErr;
+    SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
+    SIM_HIP(gravityTraverse(fa, st));
+    s->gravHalos       = nLow + nHigh;
+    s->gravRemoteCells = nAll;
+    s->gravFarCells    = nAll - (reqOff.empty() ? 0 : hwReq);
+    return SX_OK;
+}
+
 int localSync(sx_sim* s, hipStream_t st)
 {
     const size_t n = s->n;
@@ -963,6 +1309,14 @@ extern "C"
         f->keys  = s->keys + o;
         f->nc    = s->nc + o;
         if (id) *id = s->id + o;
+        return SX_OK;
+    }
+
+    int sx_sim_gravity_stats(sx_sim* s, uint64_t out[3])
+    {
+        out[0] = s->gravHalos;
+        out[1] = s->gravFarCells;
+        out[2] = s->gravRemoteCells;
         return SX_OK;
     }
 
@@ -1156,7 +1510,12 @@ extern "C"
         SIM_HIP(hipEventRecord(s->kev[12], st));
         if (s->p.g != 0.0)
         {
-            if (dist) return SX_ERR_ARG; // multi-rank gravity needs the global multipole exchange
+            if (dist)
+            {
+                if (int e = distributedGravity(s, st)) return e;
+            }
+            else
+            {
             GravArgs ga{};
             ga.first          = (uint32_t)s->first;
             ga.last           = (uint32_t)s->last;
@@ -1178,6 +1537,7 @@ extern "C"
             ga.err   = &s->sc->gravErr;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
             SIM_HIP(gravityTraverse(ga, st));
+            }
             const size_t nl = s->last - s->first;
             if (nl) maxAccSqKernel<<<grid(nl), 256, 0, st>>>(s->ax, s->ay, s->az, s->first, s->last, &s->sc->maxAccSqBits);
         }

@@ -164,6 +164,7 @@ def lib():
         "sx_sim_last_stats": (C.c_int, [vp, C.POINTER(SxNbStats)]),
         "sx_sim_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_set_comm": (C.c_int, [vp, vp]),
+        "sx_sim_gravity_stats": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_sim_init_sedov_rank": (C.c_int, [vp, u32, C.c_int, C.c_int]),
         "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_comm_unique_id": (C.c_int, [vp]),
@@ -474,6 +475,11 @@ class Sim:
         self.L.sx_sim_last_stats(self.h, C.byref(s))
         return dict(sumNeighbors=s.sumNeighbors, maxNeighbors=s.maxNeighbors, numFailed=s.numFailed,
                     sumCandidates=s.sumCandidates, sumUnion=s.sumUnion)
+
+    def gravity_stats(self):
+        out = (C.c_uint64 * 3)()
+        self.L.sx_sim_gravity_stats(self.h, out)
+        return dict(halos=out[0], far_cells=out[1], remote_cells=out[2])
 
     def close(self):
         if self.h:

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--backend", default="host")
     ap.add_argument("--side", type=int, default=16)
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--ic", default="sedov")
+    ap.add_argument("--ic", default="sedov", help="sedov | sedov_dev | noh | evrard (self-gravity, G = 1)")
+    ap.add_argument("--std", action="store_true", help="std propagator (HydroProp)")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -39,9 +40,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ctx = sx.Context(0 if args.backend == "host" else local)
     comm = sx.Comm(args.backend)
-    st, obox = po.sedov_state(args.side)
+    ic = {"evrard": po.evrard_state, "noh": po.noh_state}.get(args.ic, po.sedov_state)
+    st, obox = ic(args.side)
+    if args.ic == "evrard":
+        po.converge_h(po.load_oracle(), st, obox)  # the lattice-contracted IC's h iterate in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
-    sim = sx.Sim(ctx, 2 * st.n // size + 4096, box)
+    params = sx.default_params(g=1.0 if args.ic == "evrard" else 0.0, std=args.std)
+    sim = sx.Sim(ctx, 2 * st.n // size + 4096, box, params=params)
     sim.set_comm(comm)
     if args.ic == "sedov_dev":
         sim.init_sedov(args.side, rank, size)
@@ -51,11 +56,13 @@ def main():
     out = {}
     for s in range(args.steps):
         sim.step()
-        got = sim.get(["id", "nc", "h"] + FIELDS)
+        got = sim.get(["id", "nc", "h"] + FIELDS + (["rho", "p"] if args.std else []))
         for k, v in got.items():
             out[f"s{s}_{k}"] = v
         sc = sim.scalars()
         out[f"s{s}_scalars"] = np.array([sc["minDt"], sc["minDt_m1"], sc["ttot"]])
+        gs = sim.gravity_stats()
+        out[f"s{s}_gravity"] = np.array([gs["halos"], gs["far_cells"], gs["remote_cells"]])
         lay = sim.layout()
         out[f"s{s}_layout"] = np.array([lay["first"], lay["last"], lay["n"], lay["haloRetries"]])
     np.savez(os.path.join(args.out, f"rank{rank}.npz"), **out)
