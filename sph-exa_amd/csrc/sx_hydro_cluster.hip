@@ -450,6 +450,109 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
     }
 }
 
+/*! IAD + divv/curlv in ONE neighbor pass.  divV_curlVJLoop's terms are linear in the fresh c_i:
+ *    dV_kb = sum_j -(c_i r)_k W_j f_jb = -sum_a c_ka M_ab,   M_ab = sum_j r_a W_j f_jb,  f_j = (v_j - v_i) xm_j,
+ *  so the pass accumulates tau (6) and M (9) together and applies c_i after the inversion: one kernel evaluation
+ *  and one record read per pair instead of two (same terms, different float summation order). */
+template<int CH, int SPLIT>
+__global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a)
+{
+    __shared__ float4 sP[CH]; // x, y, z, vol = xm/kx
+    __shared__ float4 sV[CH]; // vx, vy, vz, xm
+    __shared__ float  s_red[kClusterWaves * SPLIT];
+    __shared__ float  s_scr[SPLIT > 1 ? 6 * SPLIT * kCluster : 1];
+    const Clu   cu  = setup<SPLIT>(a, s_red);
+    const RecX  ri  = a.rx[cu.iSafe];
+    const RecV  vi  = a.rv[cu.iSafe];
+    const float kxi = a.rt[cu.iSafe].kx;
+    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+    const float hi = ri.h, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    float       t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
+    float       M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    bool        res = false;
+    neighborLoop<CH, SPLIT>(
+        cu,
+        [&](uint32_t j, uint32_t slot) {
+            const RecX r = a.rx[j];
+            const RecV v = a.rv[j];
+            const RecT t = a.rt[j];
+            sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
+                                   relc(r.z, cu.oz, a.box, 2), t.xm / t.kx);
+            sV[slot]     = make_float4(v.vx, v.vy, v.vz, t.xm);
+        },
+        [&](uint32_t p) { return Rec8{sP[p], sV[p]}; },
+        [&](const Rec8& rec) {
+            const float4& q  = rec.a;
+            const float4& v  = rec.b;
+            float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
+            pbcRule(cu, a.box, h2, rx, ry, rz);
+            const float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
+            const float W      = kernelW(dist * hiInv);
+            const float volj_w = q.w * W;
+            t11 += rx * rx * volj_w;
+            t12 += rx * ry * volj_w;
+            t13 += rx * rz * volj_w;
+            t22 += ry * ry * volj_w;
+            t23 += ry * rz * volj_w;
+            t33 += rz * rz * volj_w;
+            const float rW[3] = {rx * W, ry * W, rz * W};
+            const float f[3]  = {(v.x - vi.vx) * v.w, (v.y - vi.vy) * v.w, (v.z - vi.vz) * v.w};
+#pragma unroll
+            for (int aa = 0; aa < 3; ++aa)
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    M[aa][b] = fmaf(rW[aa], f[b], M[aa][b]);
+        },
+        res);
+    {
+        float v[6] = {t11, t12, t13, t22, t23, t33};
+        combineShares<SPLIT>(cu, v, s_scr);
+        t11 = v[0], t12 = v[1], t13 = v[2], t22 = v[3], t23 = v[4], t33 = v[5];
+        float w[9] = {M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1], M[2][2]};
+        combineShares<SPLIT>(cu, w, reinterpret_cast<float*>(sP), 0u, true);
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            M[k / 3][k % 3] = w[k];
+    }
+    float cc[6];
+    iadInvert(t11, t12, t13, t22, t23, t33, hi, a.K, cc);
+    const float c11i = cc[0], c12i = cc[1], c13i = cc[2], c22i = cc[3], c23i = cc[4], c33i = cc[5];
+    // dV_kb = -(c_k0 M_0b + c_k1 M_1b + c_k2 M_2b), rows of the symmetric c_i
+    float dV[3][3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+    {
+        dV[0][b] = -(c11i * M[0][b] + c12i * M[1][b] + c13i * M[2][b]);
+        dV[1][b] = -(c12i * M[0][b] + c22i * M[1][b] + c23i * M[2][b]);
+        dV[2][b] = -(c13i * M[0][b] + c23i * M[1][b] + c33i * M[2][b]);
+    }
+    // naming of divV_curlVJLoop: dVx{k} = dV[k][x], dVy{k} = dV[k][y], dVz{k} = dV[k][z]
+    const float dVx0 = dV[0][0], dVx1 = dV[1][0], dVx2 = dV[2][0];
+    const float dVy0 = dV[0][1], dVy1 = dV[1][1], dVy2 = dV[2][1];
+    const float dVz0 = dV[0][2], dVz1 = dV[1][2], dVz2 = dV[2][2];
+    if (cu.valid && cu.part == 0)
+    {
+        const uint32_t i = cu.i;
+        a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
+        const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
+        a.divv[i]            = norm_kxi * (dVx0 + dVy1 + dVz2);
+        if (a.curlv)
+        {
+            const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
+            a.curlv[i]      = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
+        }
+        if (a.dV11)
+        {
+            a.dV11[i] = norm_kxi * dVx0;
+            a.dV12[i] = norm_kxi * (dVx1 + dVy0);
+            a.dV13[i] = norm_kxi * (dVx2 + dVz0);
+            a.dV22[i] = norm_kxi * dVy1;
+            a.dV23[i] = norm_kxi * (dVy2 + dVz1);
+            a.dV33[i] = norm_kxi * dVz2;
+        }
+    }
+}
+
 // ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
 template<int CH, int SPLIT>
 __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
@@ -851,7 +954,11 @@ void veDefGradh(const PairArgs& a, hipStream_t s)
 }
 void iadDivvCurlv(const PairArgs& a, hipStream_t s)
 {
+#ifdef SX_IAD_TWO_PASS
     if (a.numGroups) iadDivvCurlvKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+#else
+    if (a.numGroups) iadDivvCurlvFusedKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+#endif
 }
 void avSwitches(const PairArgs& a, hipStream_t s)
 {
