@@ -260,6 +260,14 @@ int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double d
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
 int sx_max_divv(sx_ctx* ctx, uint32_t first, uint32_t last, const float* divv, float* maxDivv);
 
+/* ---- observables ---------------------------------------------------------------------------------------- */
+/*! conservedQuantitiesGpu (main/src/observables/conserved_gpu.cu:71-94) and the nc sum of
+ *  computeConservedQuantities (conserved_quantities.hpp:118-131) over [first, last) of f, in double:
+ *  out = {0.5 sum m v^2, internal energy, linear momentum x y z, angular momentum x y z, sum nc}.  Internal energy
+ *  is sum u m when f->u is set, else sum cv T m with cv = idealGasCv(muiConst, gamma).  Synchronises. */
+int sx_conserved_quantities(sx_ctx* ctx, const sx_fields* f, uint32_t first, uint32_t last, float muiConst,
+                            double gamma, double out[9]);
+
 /* ---- self-gravity: ryoanji MultipoleHolder seam (multipole_holder.cuh:40-66, gravity_wrapper.hpp:104-174) ----- */
 /*! expansion centers (mass centers, {x,y,z,mac^2}, numNodes x 4 doubles; mac = 2 max(node size)/theta + |com-geo|,
  *  setMac, source_center.hpp:130-143) and Cartesian quadrupoles (numNodes x 8 floats, Cqi order,
@@ -276,7 +284,7 @@ int sx_gravity_traverse(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, con
 /* ---- multi-GPU transport (replaces the reference's MPI calls, see sph-exa_amd/csrc/sx_comm.hpp) ---------- */
 typedef struct sx_comm sx_comm;
 /*! host-staged collectives supplied by the caller (e.g. torch.distributed gloo): buffers are host memory,
- *  send/recv segments contiguous in rank order; return 0 on success. op: 0 = u32 sum, 1 = f64 min. */
+ *  send/recv segments contiguous in rank order; return 0 on success. op: 0 = u32 sum, 1 = f64 min, 2 = f64 sum. */
 typedef int (*sx_alltoallv_cb)(void* user, const void* sendHost, const uint64_t* sendBytes, void* recvHost,
                                const uint64_t* recvBytes);
 typedef int (*sx_allreduce_cb)(void* user, void* bufHost, uint64_t count, int op);
@@ -331,6 +339,10 @@ int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);
 /*! multi-rank self-gravity of the last step: {gravity halos received, remote level-6 cells used as far-field
  *  multipoles, remote cells in total} (zeros on one rank) */
 int    sx_sim_gravity_stats(sx_sim* sim, uint64_t out[3]);
+/*! computeConservedQuantities (conserved_quantities.hpp:110-179) of the current state, summed over the ranks of the
+ *  communicator: {ecin, eint, egrav, etot, |linmom|, |angmom|, totalNeighbors, linmom x y z, angmom x y z}
+ *  (egrav of the last step; synchronises) */
+int    sx_sim_conserved(sx_sim* sim, double out[13]);
 /*! device time (ms) of each hot kernel alone in the last step (HIP events on the launch stream, bracketing just the
  *  launch): findNeighbors, xmass, veDefGradh, iadDivvCurlv, avSwitches, momentumEnergy */
 int    sx_sim_kernel_times(sx_sim* sim, float* ms, int cap, const char** names);

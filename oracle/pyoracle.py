@@ -432,3 +432,18 @@ def converge_h(lib, st, box, bucket=64):
     lib.find_neighbors(tmp, box, bucket=bucket, iterate_h=True)
     st.h[srt] = tmp.h
     return st
+
+
+def conserved_quantities(st, first=0, last=None, mui=np.float32(10.0), gamma=5.0 / 3.0):
+    """localConservedQuantities (main/src/observables/conserved_quantities.hpp:49-101) restated in numpy, float64:
+    (0.5 sum m |v|^2, sum cv T m, linear momentum, angular momentum, sum nc)"""
+    last = st.n if last is None else last
+    s = slice(first, last)
+    m = st.m[s].astype(np.float64)
+    X = np.stack([st.x[s], st.y[s], st.z[s]], 1).astype(np.float64)
+    V = np.stack([st.vx[s], st.vy[s], st.vz[s]], 1).astype(np.float64)
+    ekin = 0.5 * float(np.sum(m * np.sum(V * V, 1)))
+    eint = float(np.sum(np.float64(ideal_gas_cv(mui, gamma)) * st.temp[s] * m))
+    lin = np.sum(m[:, None] * V, 0)
+    ang = np.sum(m[:, None] * np.cross(X, V), 0)
+    return ekin, eint, lin, ang, int(np.sum(st.nc[s].astype(np.int64)))

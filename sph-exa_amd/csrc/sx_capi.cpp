@@ -15,6 +15,7 @@
 #include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
 #include "sx_kernel_poly.hpp"
+#include "sx_observables.hpp"
 #include "sx_tree.hpp"
 
 using namespace sx;
@@ -782,6 +783,24 @@ GravArgs gravArgs(sx_ctx* c, const sx_fields* f, const sx_tree* t)
 
 extern "C"
 {
+    int sx_conserved_quantities(sx_ctx* c, const sx_fields* f, uint32_t first, uint32_t last, float muiConst,
+                                double gamma, double out[9])
+    {
+        if (last > first && !(f->x && f->y && f->z && f->vx && f->vy && f->vz && f->m && (f->u || f->temp)))
+            return fail(c, SX_ERR_ARG, "sx_conserved_quantities: null field");
+        ConservedArgs a{first, last, f->x, f->y, f->z, f->vx, f->vy, f->vz, f->m, f->temp, f->u, f->nc,
+                        (double)idealGasCv(muiConst, gamma)};
+        double* scratch = c->arena.get<double>("obs.scratch", conservedScratch(last > first ? last - first : 0));
+        double* dout    = c->arena.get<double>("obs.out", 10);
+        double* hout    = c->arena.pinned<double>("obs.host", 10);
+        SX_HIP(c, conservedQuantities(a, scratch, dout, c->stream));
+        SX_HIP(c, hipMemcpyAsync(hout, dout, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        for (int k = 0; k < 9; ++k)
+            out[k] = hout[k];
+        return SX_OK;
+    }
+
     int sx_gravity_upsweep(sx_ctx* c, const sx_fields* f, const sx_tree* tree, float theta, double* centers,
                            float* multipoles)
     {

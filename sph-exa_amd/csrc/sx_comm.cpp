@@ -74,6 +74,10 @@ public:
     {
         return ncclAllReduce(dev, dev, count, ncclFloat64, ncclMin, comm_, s) == ncclSuccess;
     }
+    bool allreduceSumF64(double* dev, size_t count, hipStream_t s) override
+    {
+        return ncclAllReduce(dev, dev, count, ncclFloat64, ncclSum, comm_, s) == ncclSuccess;
+    }
 
 private:
     int          rank_, size_;
@@ -136,6 +140,7 @@ public:
     }
     bool allreduceSumU32(uint32_t* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 4, 0, s); }
     bool allreduceMinF64(double* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 8, 1, s); }
+    bool allreduceSumF64(double* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 8, 2, s); }
 
 private:
     int               rank_, size_;

@@ -31,6 +31,7 @@ public:
                            const uint64_t* recvBytes, const uint64_t* recvOff, hipStream_t s) = 0;
     virtual bool allreduceSumU32(uint32_t* dev, size_t count, hipStream_t s)                  = 0;
     virtual bool allreduceMinF64(double* dev, size_t count, hipStream_t s)                    = 0;
+    virtual bool allreduceSumF64(double* dev, size_t count, hipStream_t s)                    = 0;
 
     //! host-count convenience: exchange one u64 per peer (counts), synchronous
     bool exchangeCounts(const std::vector<uint64_t>& send, std::vector<uint64_t>& recv, hipStream_t s, uint64_t* devBuf);

@@ -36,6 +36,7 @@
 #include "sx_comm.hpp"
 #include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
+#include "sx_observables.hpp"
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
@@ -1309,6 +1310,30 @@ extern "C"
         f->keys  = s->keys + o;
         f->nc    = s->nc + o;
         if (id) *id = s->id + o;
+        return SX_OK;
+    }
+
+    int sx_sim_conserved(sx_sim* s, double out[13])
+    {
+        hipStream_t   st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        ConservedArgs a{s->first, s->last, s->x, s->y, s->z, s->vx, s->vy, s->vz, s->m, s->temp, nullptr, s->nc,
+                        (double)idealGasCv(s->p.muiConst, s->p.gamma)};
+        double* scratch = s->work.get<double>("obs.scratch", conservedScratch(s->last - s->first));
+        double* q       = s->work.get<double>("obs.q", 10);
+        SIM_HIP(conservedQuantities(a, scratch, q, st));
+        // egrav of the last step joins the sum (computeConservedQuantities, conserved_quantities.hpp:145-153)
+        SIM_HIP(hipMemcpyAsync(q + 9, &s->sc->egrav, 8, hipMemcpyDeviceToDevice, st));
+        if (s->comm && s->comm->size() > 1) SIM_COMM(s->comm->allreduceSumF64(q, 10, st));
+        double h[10];
+        SIM_HIP(hipMemcpyAsync(h, q, sizeof(h), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        const double ecin = h[0], eint = h[1], egrav = h[9];
+        out[0] = ecin, out[1] = eint, out[2] = egrav, out[3] = ecin + eint + egrav;
+        out[4] = std::sqrt(h[2] * h[2] + h[3] * h[3] + h[4] * h[4]);
+        out[5] = std::sqrt(h[5] * h[5] + h[6] * h[6] + h[7] * h[7]);
+        out[6] = h[8];
+        for (int k = 0; k < 6; ++k)
+            out[7 + k] = h[2 + k];
         return SX_OK;
     }
 

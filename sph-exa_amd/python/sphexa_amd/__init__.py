@@ -165,6 +165,9 @@ def lib():
         "sx_sim_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_set_comm": (C.c_int, [vp, vp]),
         "sx_sim_gravity_stats": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_sim_conserved": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "sx_conserved_quantities": (C.c_int, [vp, C.POINTER(SxFields), u32, u32, C.c_float, C.c_double,
+                                              C.POINTER(C.c_double)]),
         "sx_sim_init_sedov_rank": (C.c_int, [vp, u32, C.c_int, C.c_int]),
         "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_comm_unique_id": (C.c_int, [vp]),
@@ -377,7 +380,7 @@ class Comm:
                     else:
                         a = np.ctypeslib.as_array((C.c_double * count).from_address(buf))
                         t = torch.from_numpy(a.copy())
-                        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                        dist.all_reduce(t, op=dist.ReduceOp.MIN if op == 1 else dist.ReduceOp.SUM)
                         a[:] = t.numpy()
                     return 0
                 except Exception as e:  # noqa: BLE001
@@ -475,6 +478,14 @@ class Sim:
         self.L.sx_sim_last_stats(self.h, C.byref(s))
         return dict(sumNeighbors=s.sumNeighbors, maxNeighbors=s.maxNeighbors, numFailed=s.numFailed,
                     sumCandidates=s.sumCandidates, sumUnion=s.sumUnion)
+
+    def conserved(self):
+        """computeConservedQuantities over all ranks (sx_sim_conserved)"""
+        out = (C.c_double * 13)()
+        self.ctx.check(self.L.sx_sim_conserved(self.h, out), "conserved")
+        names = ["ecin", "eint", "egrav", "etot", "linmom", "angmom", "totalNeighbors", "px", "py", "pz", "Lx", "Ly",
+                 "Lz"]
+        return dict(zip(names, list(out)))
 
     def gravity_stats(self):
         out = (C.c_uint64 * 3)()

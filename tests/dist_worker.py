@@ -61,6 +61,8 @@ def main():
             out[f"s{s}_{k}"] = v
         sc = sim.scalars()
         out[f"s{s}_scalars"] = np.array([sc["minDt"], sc["minDt_m1"], sc["ttot"]])
+        cq = sim.conserved()
+        out[f"s{s}_conserved"] = np.array([cq[k] for k in ("ecin", "eint", "egrav", "etot", "totalNeighbors")])
         gs = sim.gravity_stats()
         out[f"s{s}_gravity"] = np.array([gs["halos"], gs["far_cells"], gs["remote_cells"]])
         lay = sim.layout()

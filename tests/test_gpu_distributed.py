@@ -61,6 +61,18 @@ def test_distributed_steps_match_oracle(tmp_path, nproc, port):
             assert np.all(np.abs(a - b) <= tol), (s, k, np.max(np.abs(a - b) / (np.abs(b) + 1e-300)))
         dts = {tuple(d[f"s{s}_scalars"]) for d in ranks}
         assert len(dts) == 1  # identical global time-step on every rank
+        # conserved quantities summed over ranks (computeConservedQuantities' MPI_Reduce): same on every rank and
+        # equal to the sums over the merged state
+        cqs = np.array([d[f"s{s}_conserved"] for d in ranks])
+        assert np.allclose(cqs, cqs[0], rtol=1e-12, atol=0)
+        hs = po.HostState(st.n)
+        for k in ("x", "y", "z", "vx", "vy", "vz", "temp"):
+            hs.arrays[k][:] = got[k]
+        hs.m[:] = st.m[0]
+        hs.nc[:] = got["nc"]
+        ek, ei, _, _, nc = po.conserved_quantities(hs)
+        assert cqs[0][0] == pytest.approx(ek, rel=1e-10) and cqs[0][1] == pytest.approx(ei, rel=1e-10)
+        assert cqs[0][4] == nc
         assert list(dts)[0][0] == pytest.approx(ref.minDt, rel=1e-5)
         # every rank holds halos and a non-empty local range
         for d in ranks:
