@@ -835,6 +835,7 @@ extern "C"
         uint32_t* er = c->arena.get<uint32_t>("grav.err", 1);
         a.egrav      = acc;
         a.err        = er;
+        a.fast       = c->exact ? 0 : 1; // exact: the reference's double M2P/P2P; fast: float expansions
         SX_HIP(c, hipMemsetAsync(acc, 0, sizeof(double), c->stream));
         SX_HIP(c, hipMemsetAsync(er, 0, sizeof(uint32_t), c->stream));
         SX_HIP(c, gravityTraverse(a, c->stream));

@@ -198,12 +198,49 @@ __device__ __forceinline__ void p2p(double (&acc)[4], double xi, double yi, doub
     acc[3] += dz * invR3m;
 }
 
+//! fast M2P: the displacement is formed in double and rounded once, the expansion evaluated in float (rsqrt)
+__device__ __forceinline__ void m2pFast(double (&acc)[4], double tx, double ty, double tz, const double* com,
+                                        const float* M)
+{
+    const float r0 = (float)(tx - com[0]), r1 = (float)(ty - com[1]), r2 = (float)(tz - com[2]);
+    const float rr       = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+    const float r_minus1 = rsqrtf(rr);
+    const float r_minus2 = r_minus1 * r_minus1;
+    const float r_minus5 = r_minus2 * r_minus2 * r_minus1;
+    const float Qrx      = fmaf(r0, M[1], fmaf(r1, M[2], r2 * M[3]));
+    const float Qry      = fmaf(r0, M[2], fmaf(r1, M[4], r2 * M[5]));
+    const float Qrz      = fmaf(r0, M[3], fmaf(r1, M[5], r2 * M[6]));
+    const float rQr      = fmaf(r0, Qrx, fmaf(r1, Qry, r2 * Qrz));
+    const float rQrAndMonopole = (-2.5f * rQr * r_minus5 - M[0] * r_minus1) * r_minus2;
+    acc[0] += (double)(-fmaf(M[0], r_minus1, 0.5f * r_minus5 * rQr));
+    acc[1] += (double)fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
+    acc[2] += (double)fmaf(r_minus5, Qry, rQrAndMonopole * r1);
+    acc[3] += (double)fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
+}
+
+//! fast P2P: displacement in double rounded to float, softened inverse distance by rsqrt
+__device__ __forceinline__ void p2pFast(double (&acc)[4], double xi, double yi, double zi, double xj, double yj,
+                                        double zj, float mj, float hi, float hj)
+{
+    const float dx = (float)(xj - xi), dy = (float)(yj - yi), dz = (float)(zj - zi);
+    const float R2     = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+    const float h_ij   = hi + hj;
+    const float R2eff  = fmaxf(R2, h_ij * h_ij);
+    const float invR   = rsqrtf(R2eff);
+    const float invR3m = mj * invR * invR * invR;
+    acc[0] -= (double)(invR3m * R2);
+    acc[1] += (double)(dx * invR3m);
+    acc[2] += (double)(dy * invR3m);
+    acc[3] += (double)(dz * invR3m);
+}
+
 struct __attribute__((aligned(16))) GSrc
 {
     double x, y, z;
     float  m, h;
 };
 
+template<bool FAST>
 __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
 {
     __shared__ int  s_stack[4][kGStack];
@@ -280,7 +317,11 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
             const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
             const int node = e >> 4;
             if (valid && (((e & 15) >> q) & 1))
-                m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+            {
+                if constexpr (FAST)
+                    m2pFast(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+                else m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+            }
         }
         nM = 0;
     };
@@ -307,7 +348,8 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
                     for (uint32_t s = 0; s < cnt; ++s)
                     {
                         const GSrc src = s_src[wave][s];
-                        p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
+                        if constexpr (FAST) p2pFast(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
+                        else p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
                     }
             }
         }
@@ -549,7 +591,8 @@ hipError_t gravityTraverse(const GravArgs& a, hipStream_t s)
 {
     if (a.last <= a.first) return hipSuccess;
     const uint32_t waves = (a.last - a.first + kWave - 1) / kWave;
-    gravityTraverseKernel<<<(waves + 3) / 4, 256, 0, s>>>(a);
+    if (a.fast) gravityTraverseKernel<true><<<(waves + 3) / 4, 256, 0, s>>>(a);
+    else gravityTraverseKernel<false><<<(waves + 3) / 4, 256, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ struct GravArgs
     float * ax, *ay, *az; // gravity is added
     double*   egrav;      // device accumulator (atomic), nullable
     uint32_t* err;        // bit 0: traversal stack exhausted
+    int       fast;       // 1: M2P/P2P in float with rsqrt (displacements formed in double, sums in double)
 };
 
 //! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi

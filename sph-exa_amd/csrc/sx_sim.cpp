@@ -1100,6 +1100,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     ga.az    = s->az + shift;
     ga.egrav = &s->sc->egrav;
     ga.err   = &s->sc->gravErr;
+    ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
     SIM_HIP(gravityTraverse(ga, st));
 
@@ -1123,6 +1124,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     fa.ax = s->ax, fa.ay = s->ay, fa.az = s->az;
     fa.egrav = &s->sc->egrav;
     fa.err   = &s->sc->gravErr;
+    fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
     SIM_HIP(gravityTraverse(fa, st));
     s->gravHalos       = nLow + nHigh;
@@ -1560,6 +1562,7 @@ extern "C"
             ga.ax = s->ax, ga.ay = s->ay, ga.az = s->az;
             ga.egrav = &s->sc->egrav;
             ga.err   = &s->sc->gravErr;
+            ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
             SIM_HIP(gravityTraverse(ga, st));
             }
