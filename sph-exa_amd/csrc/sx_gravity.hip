@@ -199,10 +199,11 @@ __device__ __forceinline__ void p2p(double (&acc)[4], double xi, double yi, doub
 }
 
 //! fast M2P: the displacement is formed in double and rounded once, the expansion evaluated in float (rsqrt)
-__device__ __forceinline__ void m2pFast(double (&acc)[4], double tx, double ty, double tz, const double* com,
-                                        const float* M)
+template<class A>
+__device__ __forceinline__ void m2pFastV(A (&acc)[4], double tx, double ty, double tz, double c0, double c1,
+                                         double c2, const float (&M)[8])
 {
-    const float r0 = (float)(tx - com[0]), r1 = (float)(ty - com[1]), r2 = (float)(tz - com[2]);
+    const float r0 = (float)(tx - c0), r1 = (float)(ty - c1), r2 = (float)(tz - c2);
     const float rr       = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
     const float r_minus1 = rsqrtf(rr);
     const float r_minus2 = r_minus1 * r_minus1;
@@ -212,10 +213,17 @@ __device__ __forceinline__ void m2pFast(double (&acc)[4], double tx, double ty, 
     const float Qrz      = fmaf(r0, M[3], fmaf(r1, M[5], r2 * M[6]));
     const float rQr      = fmaf(r0, Qrx, fmaf(r1, Qry, r2 * Qrz));
     const float rQrAndMonopole = (-2.5f * rQr * r_minus5 - M[0] * r_minus1) * r_minus2;
-    acc[0] += (double)(-fmaf(M[0], r_minus1, 0.5f * r_minus5 * rQr));
-    acc[1] += (double)fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
-    acc[2] += (double)fmaf(r_minus5, Qry, rQrAndMonopole * r1);
-    acc[3] += (double)fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
+    acc[0] += (A)(-fmaf(M[0], r_minus1, 0.5f * r_minus5 * rQr));
+    acc[1] += (A)fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
+    acc[2] += (A)fmaf(r_minus5, Qry, rQrAndMonopole * r1);
+    acc[3] += (A)fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
+}
+template<class A>
+__device__ __forceinline__ void m2pFast(A (&acc)[4], double tx, double ty, double tz, const double* com,
+                                        const float* M)
+{
+    const float Mv[8] = {M[0], M[1], M[2], M[3], M[4], M[5], M[6], M[7]};
+    m2pFastV(acc, tx, ty, tz, com[0], com[1], com[2], Mv);
 }
 
 //! fast P2P: displacement in double rounded to float, softened inverse distance by rsqrt
@@ -246,7 +254,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
     __shared__ int  s_p2p[4][kGList];
-    __shared__ GSrc s_src[4][kWave];
+    __shared__ GSrc   s_src[FAST ? 1 : 4][kWave];
+    __shared__ float4 s_srcF[FAST ? 4 : 1][2][kWave]; // fast P2P: source x, y, z relative to the wave origin, m
+    __shared__ float  s_hF[FAST ? 4 : 1][2][kWave];
 
     const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4;
     const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * 4 + wave;
@@ -258,6 +268,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     const double   xi = a.x[iS], yi = a.y[iS], zi = a.z[iS];
     const float    hi = a.h[iS];
     const uint64_t ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // fast variant: coordinates relative to the wave's first target, formed in double and rounded once
+    const double ox = __shfl(xi, 0), oy = __shfl(yi, 0), oz = __shfl(zi, 0);
+    const float  txr = (float)(xi - ox), tyr = (float)(yi - oy), tzr = (float)(zi - oz);
 
     // target box of each 16-lane quarter (computeCenterAndSize, traversal_cpu.hpp:43-59), over its valid targets
     double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
@@ -312,20 +325,104 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     bool   overflow = false;
 
     auto flushM2P = [&]() {
-        for (int k = 0; k < nM; ++k)
+        if constexpr (FAST)
         {
-            const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
-            const int node = e >> 4;
-            if (valid && (((e & 15) >> q) & 1))
+            float fa[4] = {0, 0, 0, 0};
+            for (int k = 0; k < nM; ++k)
             {
-                if constexpr (FAST)
-                    m2pFast(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
-                else m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+                const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
+                const int node = e >> 4;
+                if (valid && (((e & 15) >> q) & 1))
+                    m2pFast(fa, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+                if ((k & 31) == 31)
+                    for (int c = 0; c < 4; ++c)
+                        acc[c] += (double)fa[c], fa[c] = 0.0f;
             }
+            for (int c = 0; c < 4; ++c)
+                acc[c] += (double)fa[c];
         }
+        else
+            for (int k = 0; k < nM; ++k)
+            {
+                const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
+                const int node = e >> 4;
+                if (valid && (((e & 15) >> q) & 1))
+                    m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+            }
         nM = 0;
     };
+    // fast P2P: leaf sources converted to float relative coordinates while staged; the next leaf chunk (<= 64
+    // sources, one per lane) is loaded into registers while the current one is evaluated from LDS
+    auto flushP2PFast = [&]() {
+        int      ek = 0;
+        uint32_t ec0 = 0, js = 0, jn = 0;
+        unsigned jm = 0;
+        auto     nextChunk = [&]() -> bool {
+            while (ek < nP)
+            {
+                const int      e    = __builtin_amdgcn_readfirstlane(s_p2p[wave][ek]);
+                const int      lidx = a.internalToLeaf[e >> 4];
+                const uint32_t s0 = a.layout[lidx], s1 = a.layout[lidx + 1];
+                if (s0 + ec0 < s1)
+                {
+                    js = s0 + ec0;
+                    jn = min((uint32_t)kWave, s1 - js);
+                    jm = (unsigned)(e & 15);
+                    ec0 += kWave;
+                    if (s0 + ec0 >= s1) ++ek, ec0 = 0;
+                    return true;
+                }
+                ++ek, ec0 = 0;
+            }
+            return false;
+        };
+        float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+        float  ph = 0.f;
+        auto   loadRegs = [&]() {
+            if ((uint32_t)lane < jn)
+            {
+                const uint32_t j = js + lane;
+                pv = make_float4((float)(a.x[j] - ox), (float)(a.y[j] - oy), (float)(a.z[j] - oz), a.m[j]);
+                ph = a.h[j];
+            }
+        };
+        bool have = nextChunk();
+        if (have) loadRegs();
+        int buf = 0;
+        while (have)
+        {
+            const uint32_t cn = jn;
+            const unsigned cm = jm;
+            __builtin_amdgcn_wave_barrier();
+            if ((uint32_t)lane < cn) s_srcF[wave][buf][lane] = pv, s_hF[wave][buf][lane] = ph;
+            have = nextChunk();
+            if (have) loadRegs();
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
+            __builtin_amdgcn_wave_barrier();
+            if (valid && ((cm >> q) & 1u))
+            {
+                float fa0 = 0, fa1 = 0, fa2 = 0, fa3 = 0;
+                for (uint32_t s = 0; s < cn; ++s)
+                {
+                    const float4 src = s_srcF[wave][buf][s];
+                    const float  dx = src.x - txr, dy = src.y - tyr, dz = src.z - tzr;
+                    const float  R2    = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                    const float  h_ij  = hi + s_hF[wave][buf][s];
+                    const float  invR  = rsqrtf(fmaxf(R2, h_ij * h_ij));
+                    const float  invR3m = src.w * invR * invR * invR;
+                    fa0 = fmaf(-invR3m, R2, fa0);
+                    fa1 = fmaf(dx, invR3m, fa1);
+                    fa2 = fmaf(dy, invR3m, fa2);
+                    fa3 = fmaf(dz, invR3m, fa3);
+                }
+                acc[0] += (double)fa0, acc[1] += (double)fa1, acc[2] += (double)fa2, acc[3] += (double)fa3;
+            }
+            buf ^= 1;
+        }
+        nP = 0;
+    };
     auto flushP2P = [&]() {
+        if constexpr (FAST) return flushP2PFast();
         for (int k = 0; k < nP; ++k)
         {
             const int      e    = __builtin_amdgcn_readfirstlane(s_p2p[wave][k]);
