@@ -734,12 +734,14 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float v1     = dist * hiInv, v2 = dist * hjInv;
             const float Wi     = hiInv3 * kernelW(v1);
             const float Wj     = hjInv3 * kernelW(v2);
-            const float tA1i   = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
-            const float tA2i   = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
-            const float tA3i   = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
-            const float tA1j   = -(A.y * rx + A.z * ry + A.w * rz) * Wj;
-            const float tA2j   = -(A.z * rx + B.x * ry + B.y * rz) * Wj;
-            const float tA3j   = -(A.w * rx + B.y * ry + B.z * rz) * Wj;
+            // IAD directions u = c r; the reference's termA = -u W (momentum_energy_kern.hpp:134-146) is applied by
+            // folding -W into the per-side coefficients below
+            const float u1i = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
+            const float u2i = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
+            const float u3i = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;
+            const float u1j = A.y * rx + A.z * ry + A.w * rz;
+            const float u2j = A.z * rx + B.x * ry + B.y * rz;
+            const float u3j = A.w * rx + B.y * ry + B.z * rz;
             const float mj = T.x, rhoj = T.z, cj = V.w;
             float       rv = rx * vx_ij + ry * vy_ij + rz * vz_ij;
             if constexpr (AVC)
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float vij_signal = (alpha_i + A.x) * 0.25f * (ci + cj) - 2.0f * wij;
             const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
             const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
-            maxvsignali            = fmaxf(maxvsignali, vijsignal);
+            maxvsignali            = vijsignal > maxvsignali ? vijsignal : maxvsignali;
             const float Atwood = fabsf(rhoi - rhoj) * __frcp_rn(rhoi + rhoj);
             float       a_mom, b_mom;
             if (__ballot(Atwood >= Atmin) == 0)
@@ -761,18 +763,20 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
                 b_mom = T.y * T.y;
             }
             else atwoodWeights(Atwood, Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
-            const float a_visc   = mj * rhoiInv * halfVisc;
-            const float b_visc   = B.w * halfVisc;
-            const float a_visc_x = a_visc * tA1i + b_visc * tA1j;
-            const float a_visc_y = a_visc * tA2i + b_visc * tA2j;
-            const float a_visc_z = a_visc * tA3i + b_visc * tA3j;
-            a_visc_energy += a_visc_x * vx_ij + a_visc_y * vy_ij + a_visc_z * vz_ij;
-            energy += mj * a_mom * (vx_ij * tA1i + vy_ij * tA2i + vz_ij * tA3i);
+            const float a_visc     = mj * rhoiInv * halfVisc;
+            const float b_visc     = B.w * halfVisc;
             const float momentum_i = mj * prhoi * a_mom;
             const float momentum_j = T.w * b_mom;
-            mx += momentum_i * tA1i + momentum_j * tA1j + a_visc_x;
-            my += momentum_i * tA2i + momentum_j * tA2j + a_visc_y;
-            mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
+            // v_ij . termA_i and v_ij . termA_j
+            const float di = -Wi * (vx_ij * u1i + vy_ij * u2i + vz_ij * u3i);
+            const float dj = -Wj * (vx_ij * u1j + vy_ij * u2j + vz_ij * u3j);
+            energy += mj * a_mom * di;
+            a_visc_energy += a_visc * di + b_visc * dj;
+            // momentum_i termA_i + momentum_j termA_j + a_visc (a_visc termA_i + b_visc termA_j)
+            const float ki = -(momentum_i + a_visc) * Wi, kj = -(momentum_j + b_visc) * Wj;
+            mx += ki * u1i + kj * u1j;
+            my += ki * u2i + kj * u2j;
+            mz += ki * u3i + kj * u3j;
         },
         res);
     {
