@@ -244,3 +244,131 @@ def C_byref(s):
     import ctypes
 
     return ctypes.byref(s)
+
+
+# ---- multi-rank self-gravity (restates distributedGravity, sph-exa_amd/csrc/sx_sim.cpp) ----------------------------
+CELL_SHIFT = 63 - HIST_BITS  # level-6 SFC cells = the splitter bins: one owner per cell
+
+
+def _cell_geometry(st, box, sel):
+    """geometric center and half size of the level-6 cell holding the particles sel (all in one cell)"""
+    c, s = np.zeros(3), np.zeros(3)
+    for k, name in enumerate(("x", "y", "z")):
+        lo, hi = box.lim[2 * k], box.lim[2 * k + 1]
+        L = (hi - lo) / float(1 << (HIST_BITS // 3))
+        ic = np.floor((st.arrays[name][sel][0] - lo) / L)
+        c[k], s[k] = lo + (ic + 0.5) * L, 0.5 * L
+    return c, s
+
+
+def _cell_moments(st, box, idx, inv_theta):
+    """com, mass, MAC radius^2 (setMac) and traceless quadrupole (Cqi order) of one cell, float64"""
+    x, y, z = st.x[idx], st.y[idx], st.z[idx]
+    m = st.m[idx].astype(np.float64)
+    M = m.sum()
+    com = np.array([np.sum(m * x), np.sum(m * y), np.sum(m * z)]) / M
+    gc, gs = _cell_geometry(st, box, idx)
+    mac = 2.0 * gs.max() * inv_theta + np.linalg.norm(com - gc)
+    r = np.stack([x - com[0], y - com[1], z - com[2]], 1)
+    Q = np.einsum("i,ia,ib->ab", m, r, r)
+    tr = np.trace(Q)
+    q = np.array([M, 3 * Q[0, 0] - tr, 3 * Q[0, 1], 3 * Q[0, 2], 3 * Q[1, 1] - tr, 3 * Q[1, 2], 3 * Q[2, 2] - tr, tr])
+    return np.concatenate([com, [mac * mac], q])
+
+
+def _m2p(targets, cells):
+    """quadrupole M2P (cartesian_qpole.hpp:175-201) of every cell on every target, float64; returns (n, 4)"""
+    out = np.zeros((targets.shape[0], 4))
+    for c in cells:
+        r = targets - c[0:3]
+        rr = np.sum(r * r, 1)
+        rm1 = 1.0 / np.sqrt(rr)
+        rm2 = rm1 * rm1
+        rm5 = rm2 * rm2 * rm1
+        M = c[4:12]
+        Qr = np.stack([r[:, 0] * M[1] + r[:, 1] * M[2] + r[:, 2] * M[3],
+                       r[:, 0] * M[2] + r[:, 1] * M[4] + r[:, 2] * M[5],
+                       r[:, 0] * M[3] + r[:, 1] * M[5] + r[:, 2] * M[6]], 1)
+        rQr = np.sum(r * Qr, 1)
+        mono = (-2.5 * rQr * rm5 - M[0] * rm1) * rm2
+        out[:, 0] += -(M[0] * rm1 + 0.5 * rm5 * rQr)
+        out[:, 1:] += rm5[:, None] * Qr + mono[:, None] * r
+    return out
+
+
+def distributed_gravity(d, full, G, theta):
+    """gravity of the locals [d.first, d.last) of `full` (key sorted, after DistOracle._discover): own level-6 cells'
+    moments all-gathered; remote cells passing the vector MAC against every request box of this rank are far-field
+    multipoles, the particles of the others are fetched from their owners and traversed with the locals (oracle
+    Barnes-Hut on their own tree).  Returns accelerations (nl, 3), egrav and {halos, far_cells, remote_cells}."""
+    import torch
+
+    dist = _dist()
+    P, r = d.size, d.rank
+    f, l = d.first, d.last
+    nl = l - f
+    keys = full.keys[f:l]
+    cells = (keys >> np.uint64(CELL_SHIFT)).astype(np.int64)
+    ucell, start = np.unique(cells, return_index=True)
+    ends = np.append(start[1:], nl)
+    inv_theta = 1.0 / theta
+    mine = np.array([np.concatenate([[c], _cell_moments(full, d.box, np.arange(f + b, f + e), inv_theta)])
+                     for c, b, e in zip(ucell, start, ends)]).reshape(-1, 13)
+    # all-gather (rank order = key order)
+    cnt = torch.tensor([mine.shape[0]], dtype=torch.int64)
+    allc = [torch.zeros(1, dtype=torch.int64) for _ in range(P)]
+    dist.all_gather(allc, cnt)
+    mx = max(int(c) for c in allc)
+    pad = np.zeros((mx, 13))
+    pad[: mine.shape[0]] = mine
+    gathered = [torch.zeros((mx, 13), dtype=torch.float64) for _ in range(P)]
+    dist.all_gather(gathered, torch.from_numpy(pad))
+    remote = [gathered[q].numpy()[: int(allc[q])] for q in range(P)]
+    # near / far against the request boxes of this rank (center, half size + search radius)
+    boxes = d.my_boxes
+    near = []
+    for q in range(P):
+        if q == r:
+            near.append(np.zeros(0, bool))
+            continue
+        nq = np.zeros(remote[q].shape[0], bool)
+        for b in boxes:
+            dd = np.maximum(np.abs(b[0:3][None, :] - remote[q][:, 1:4]) - b[3:6][None, :], 0.0)
+            nq |= np.sum(dd * dd, 1) < remote[q][:, 4]
+        near.append(nq)
+    # requests: cell ids to each owner; owners answer with x, y, z, m, h of those cells (ascending = key order)
+    req = [remote[q][near[q], 0].astype(np.int64) if q != r else np.zeros(0, np.int64) for q in range(P)]
+    got, rcounts = _a2a_bytes(np.concatenate(req) if req else np.zeros(0, np.int64), [len(x) for x in req], 8)
+    pos = np.cumsum([0] + rcounts)
+    send = []
+    for q in range(P):
+        ids = got[pos[q]:pos[q + 1]]
+        sel = [np.arange(f + start[k], f + ends[k]) for k in np.searchsorted(ucell, ids)] if len(ids) else []
+        send.append(np.concatenate(sel) if sel else np.zeros(0, np.int64))
+    parts = {}
+    for name in ("x", "y", "z", "m", "h"):
+        a = full.arrays[name]
+        src = np.concatenate([a[s] for s in send]) if send else a[:0]
+        parts[name], pc = _a2a_bytes(src, [len(s) for s in send], a.itemsize)
+    po_ = np.cumsum([0] + pc)
+    nlow = int(sum(pc[:r]))
+    nh = int(sum(pc)) - nlow
+    g = po.HostState(nlow + nl + nh)
+    for name in ("x", "y", "z", "m", "h"):
+        g.arrays[name][:nlow] = parts[name][:nlow]
+        g.arrays[name][nlow:nlow + nl] = full.arrays[name][f:l]
+        g.arrays[name][nlow + nl:] = parts[name][nlow:]
+    d.ora.sfc_keys(g, d.box)
+    assert np.all(np.diff(g.keys.astype(np.float64)) >= 0), "gravity sources not key sorted"
+    prm = d.ora.params(g=G, theta=theta)
+    eg, _, _ = d.ora.gravity(g, d.box, prm, first=nlow, last=nlow + nl)
+    acc = np.stack([g.ax[nlow:nlow + nl], g.ay[nlow:nlow + nl], g.az[nlow:nlow + nl]], 1).astype(np.float64)
+    far = [remote[q][~near[q]] for q in range(P) if q != r]
+    far = np.concatenate(far) if far else np.zeros((0, 13))
+    tg = np.stack([full.x[f:l], full.y[f:l], full.z[f:l]], 1)
+    fa = _m2p(tg, far[:, 1:]) if far.shape[0] else np.zeros((nl, 4))
+    acc += G * fa[:, 1:]
+    eg += 0.5 * G * float(np.sum(full.m[f:l].astype(np.float64) * fa[:, 0]))
+    stats = {"halos": nlow + nh, "far_cells": int(far.shape[0]), "remote_cells": int(sum(x.shape[0] for x in remote))
+             - mine.shape[0]}
+    return acc, eg, stats

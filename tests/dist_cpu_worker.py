@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--ic", default="sedov")
     ap.add_argument("--side", type=int, default=16)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--gravity", action="store_true", help="only the multi-rank gravity of the IC (G = 1)")
     args = ap.parse_args()
     import torch.distributed as dist
 
@@ -32,7 +33,8 @@ def main():
     import dist_oracle as do
     import pyoracle as po
 
-    st, box = po.sedov_state(args.side) if args.ic == "sedov" else po.noh_state(args.side)
+    ic = {"sedov": po.sedov_state, "noh": po.noh_state, "evrard": po.evrard_state}[args.ic]
+    st, box = ic(args.side)
     f, l = st.n * args.rank // args.size, st.n * (args.rank + 1) // args.size
     local = po.HostState(l - f)
     for k in po.CONSERVED:
@@ -40,6 +42,14 @@ def main():
     local.minDt, local.minDt_m1 = st.minDt, st.minDt_m1
     d = do.DistOracle(po.load_oracle(), box, local)
     out = {}
+    if args.gravity:
+        full = d._discover(d._exchange_particles(d._sort(d.local)), do.HALO_MARGIN)
+        acc, eg, stats = do.distributed_gravity(d, full, 1.0, 0.5)
+        np.savez(os.path.join(args.out, f"rank{args.rank}.npz"), id=full.id[d.first:d.last], acc=acc,
+                 egrav=np.array([eg]), stats=np.array([stats["halos"], stats["far_cells"], stats["remote_cells"]]))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     for s in range(args.steps):
         loc = d.step()
         for k in ("id", "nc", "h", "x", "y", "z", "vx", "vy", "vz", "temp", "du", "ax", "ay", "az", "alpha",
