@@ -625,7 +625,18 @@ findNeighborsKernel(NsArgs a)
         // union entries: candidate index -> global index, through the leaf it belongs to
         uint32_t* uni = a.uni + (size_t)c * a.ucap;
         run           = off + incl - sum;
-        int cc        = 0;
+        // first candidate leaf of this thread's words by binary search (s_cOff ascending), then walk forward
+        int cc = 0;
+        {
+            int lo = 0, hi = numCand; // last cc with s_cOff[cc] <= w0 * 32
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_cOff[mid] <= w0 * 32) lo = mid;
+                else hi = mid - 1;
+            }
+            cc = lo;
+        }
         for (uint32_t w = w0; w < w1; ++w)
         {
             uint32_t bits = s_bits[w];
@@ -642,13 +653,27 @@ findNeighborsKernel(NsArgs a)
         }
         __syncthreads();
         // candidate indices -> union positions (ascending either way)
+        // batches of 8 list words: the 8 loads are issued together (one L2 round trip per batch instead of one per
+        // word), then ranked in LDS and stored
         const uint32_t nwl = (stored + 1) >> 1;
-        for (uint32_t k = 0; k < nwl; ++k)
+        constexpr int  kRB = 8;
+        for (uint32_t k0 = 0; k0 < nwl; k0 += kRB)
         {
-            const uint32_t v  = ll[(size_t)k * kWave];
-            const uint32_t lo = bitRank(s_bits, s_pre, v & 0xffffu);
-            const uint32_t hp = (2 * k + 1 < stored) ? bitRank(s_bits, s_pre, v >> 16) : 0u;
-            ll[(size_t)k * kWave] = lo | (hp << 16);
+            uint32_t v[kRB];
+#pragma unroll
+            for (int u = 0; u < kRB; ++u)
+                v[u] = (k0 + u < nwl) ? ll[(size_t)(k0 + u) * kWave] : 0u;
+#pragma unroll
+            for (int u = 0; u < kRB; ++u)
+            {
+                const uint32_t k = k0 + u;
+                if (k < nwl)
+                {
+                    const uint32_t lo = bitRank(s_bits, s_pre, v[u] & 0xffffu);
+                    const uint32_t hp = (2 * k + 1 < stored) ? bitRank(s_bits, s_pre, v[u] >> 16) : 0u;
+                    ll[(size_t)k * kWave] = lo | (hp << 16);
+                }
+            }
         }
         if (threadIdx.x == 0) a.ucount[c] = ucnt;
     }
