@@ -432,6 +432,24 @@ class Sim:
         self.ctx.check(self.L.sx_sim_set_state(self.h, arrs[0].size, *[a.ctypes.data for a in arrs],
                                                float(minDt), float(minDt_m1)), "set_state")
 
+    CONSERVED = ["x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "id"]
+
+    def save_checkpoint(self, path):
+        """restart file of this rank: the conserved fields under the reference's field names
+        (ParticlesData::fieldNames, particles_data.hpp:247-251; the set HydroVeProp restarts from,
+        ve_hydro.hpp:74 + x,y,z,h,m) and the time-step scalars, as an .npz (HDF5/H5Part is not in this image)"""
+        st = self.get(self.CONSERVED)
+        sc = self.scalars()
+        np.savez(path, **st, minDt=np.float64(sc["minDt"]), minDt_m1=np.float64(sc["minDt_m1"]),
+                 ttot=np.float64(sc["ttot"]))
+
+    def load_checkpoint(self, path):
+        """continue from save_checkpoint's file: set_state with the saved fields and time-steps"""
+        with np.load(path, allow_pickle=False) as d:
+            st = {k: d[k] for k in self.CONSERVED}
+            self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
+            return float(d["ttot"])
+
     def step(self):
         rc = self.L.sx_sim_step(self.h)
         if rc != SX_OK:
