@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)
     const Clu  cu = setup<SPLIT>(a, s_red);
     const RecX ri = a.rx[cu.iSafe];
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
+    const float hInv = 1.0f / ri.h, hInv2 = hInv * hInv, h2 = 2.0f * ri.h;
     float       rho0 = cu.part == 0 ? ri.m : 0.0f;
     bool        res  = false;
     neighborLoop<CH, SPLIT>(
@@ -259,8 +259,7 @@ __global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)
         [&](const float4& q) {
             float rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-            rho0 += kernelW(dist * hInv) * q.w;
+            rho0 += kernelWt((rx * rx + ry * ry + rz * rz) * hInv2) * q.w;
         },
         res);
     float v[1] = {rho0};
@@ -283,7 +282,7 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
     const RecX  ri     = a.rx[cu.iSafe];
     const float xmassi = a.rt[cu.iSafe].xm;
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hInv = 1.0f / ri.h, h2 = 2.0f * ri.h;
+    const float hInv = 1.0f / ri.h, hInv2 = hInv * hInv, h2 = 2.0f * ri.h;
     const bool  own = cu.part == 0; // the self terms go to share 0
     float       kxi = own ? xmassi : 0.0f, whomegai = own ? -3.0f * xmassi : 0.0f, wrho0i = own ? -3.0f * ri.m : 0.0f;
     bool        res = false;
@@ -300,11 +299,9 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
             const float   xmassj = r.s;
             float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float vloc = dist * hInv;
-            float       w, dw;
-            kernelWdW(vloc, w, dw);
-            const float dterh = -(3.0f * w + vloc * dw);
+            float w, vdw;
+            kernelWvdWt((rx * rx + ry * ry + rz * rz) * hInv2, w, vdw);
+            const float dterh = -(3.0f * w + vdw);
             kxi += w * xmassj;
             whomegai += dterh * xmassj;
             wrho0i += dterh * q.w;
@@ -343,7 +340,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hi = ri.h, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    const float hi = ri.h, hiInv = 1.0f / hi, hiInv2 = hiInv * hiInv, h2 = 2.0f * hi;
     auto        stage = [&](uint32_t j, uint32_t slot) {
         const RecX r = a.rx[j];
         if constexpr (STD)
@@ -365,8 +362,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         [&](const float4& q) {
             float rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float volj_w = q.w * kernelW(dist * hiInv);
+            const float volj_w = q.w * kernelWt((rx * rx + ry * ry + rz * rz) * hiInv2);
             t11 += rx * rx * volj_w;
             t12 += rx * ry * volj_w;
             t13 += rx * rz * volj_w;
@@ -403,8 +399,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
             const float4& v  = r.b;
             float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float dist = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float Wi   = kernelW(dist * hiInv);
+            const float Wi   = kernelWt((rx * rx + ry * ry + rz * rz) * hiInv2);
             const float tA0  = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
             const float tA1  = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
             const float tA2  = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
@@ -466,7 +461,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
     const RecV  vi  = a.rv[cu.iSafe];
     const float kxi = a.rt[cu.iSafe].kx;
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hi = ri.h, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    const float hi = ri.h, hiInv = 1.0f / hi, hiInv2 = hiInv * hiInv, h2 = 2.0f * hi;
     float       t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
     float       M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     bool        res = false;
@@ -486,8 +481,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
             const float4& v  = rec.b;
             float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float dist   = sqrtf(rx * rx + ry * ry + rz * rz);
-            const float W      = kernelW(dist * hiInv);
+            const float W      = kernelWt((rx * rx + ry * ry + rz * rz) * hiInv2);
             const float volj_w = q.w * W;
             t11 += rx * rx * volj_w;
             t12 += rx * ry * volj_w;
@@ -566,7 +560,7 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
     const RecV  vi  = a.rv[cu.iSafe];
     const RecC  ci6 = a.rc[cu.iSafe];
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hi = ri.h, ci = vi.c, hiInv = 1.0f / hi, h2 = 2.0f * hi;
+    const float hi = ri.h, ci = vi.c, hiInv = 1.0f / hi, hiInv2 = hiInv * hiInv, h2 = 2.0f * hi;
     const float hiInv3K     = (float)a.K * (hiInv * hiInv * hiInv);
     const float divv_i      = ci6.divv;
     float       vijsignal_i = 1.e-40f * ci;
@@ -591,12 +585,11 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float r2    = rx * rx + ry * ry + rz * rz;
             const float rinv  = rsqrtf(r2);
-            const float dist  = r2 * rinv;
             const float vx_ij = vi.vx - v.x, vy_ij = vi.vy - v.y, vz_ij = vi.vz - v.z;
             const float rv    = rx * vx_ij + ry * vy_ij + rz * vz_ij;
             const float vsig  = rv < 0.0f ? ci + v.w - 3.0f * rv * rinv : 0.0f;
             vijsignal_i       = fmaxf(vijsignal_i, vsig);
-            const float Wi     = hiInv3K * kernelW(dist * hiInv);
+            const float Wi     = hiInv3K * kernelWt(r2 * hiInv2);
             const float termA1 = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
             const float termA2 = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
             const float termA3 = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
@@ -681,8 +674,9 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     const float lxi     = __log2f(xmassi);
     const float xmi2    = xmassi * xmassi;
     const float hiInv   = 1.0f / hi;
-    const float hiInv3  = hiInv * hiInv * hiInv;
-    const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp;
+    const float hiInv2  = hiInv * hiInv;
+    const float hiInv3  = hiInv2 * hiInv;
+    const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp, AtminLo = a.Atmin * (1.0f - 0x1p-20f);
     float maxvsignali = 0.0f;
     float mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
     bool  res = false;
@@ -727,13 +721,13 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float r2     = rx * rx + ry * ry + rz * rz;
             const float rinv   = rsqrtf(r2);
-            const float dist   = r2 * rinv;
             const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
             const float hjInv  = P.w;
-            const float hjInv3 = hjInv * hjInv * hjInv;
-            const float v1     = dist * hiInv, v2 = dist * hjInv;
-            const float Wi     = hiInv3 * kernelW(v1);
-            const float Wj     = hjInv3 * kernelW(v2);
+            const float hjInv2 = hjInv * hjInv;
+            const float hjInv3 = hjInv2 * hjInv;
+            const float t1 = r2 * hiInv2, t2 = r2 * hjInv2; // squares of v1 = r/h_i, v2 = r/h_j
+            const float Wi     = hiInv3 * kernelWt(t1);
+            const float Wj     = hjInv3 * kernelWt(t2);
             // IAD directions u = c r; the reference's termA = -u W (momentum_energy_kern.hpp:134-146) is applied by
             // folding -W into the per-side coefficients below
             const float u1i = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
@@ -747,7 +741,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             if constexpr (AVC)
             {
                 const float gj[6] = {r.g.x, r.g.y, r.g.z, r.g.w, r.g2.x, r.g2.y};
-                rv += avRvCorrection<false>(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gj);
+                rv += avRvCorrection<false>(rx, ry, rz, r2 * rinv * fminf(hiInv, hjInv), eta_crit, gradV_i, gj);
             }
             const float wij = rv * rinv;
             // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
@@ -755,14 +749,17 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
             const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
             const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
             maxvsignali            = vijsignal > maxvsignali ? vijsignal : maxvsignali;
-            const float Atwood = fabsf(rhoi - rhoj) * __frcp_rn(rhoi + rhoj);
+            // Atwood = |rho_i - rho_j| / (rho_i + rho_j); the wave-uniform test of the common case (below Atmin
+            // everywhere) multiplies instead of dividing, against a threshold lowered by 2^-20 so that every lane
+            // whose rounded quotient reaches Atmin takes the exact branch
+            const float drho = fabsf(rhoi - rhoj), srho = rhoi + rhoj;
             float       a_mom, b_mom;
-            if (__ballot(Atwood >= Atmin) == 0)
+            if (__ballot(drho >= AtminLo * srho) == 0)
             {
                 a_mom = xmi2; // the common case: below Atmin in every lane
                 b_mom = T.y * T.y;
             }
-            else atwoodWeights(Atwood, Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
+            else atwoodWeights(drho * __frcp_rn(srho), Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
             const float a_visc     = mj * rhoiInv * halfVisc;
             const float b_visc     = B.w * halfVisc;
             const float momentum_i = mj * prhoi * a_mom;
@@ -866,11 +863,10 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float r2     = rx * rx + ry * ry + rz * rz;
             const float rinv   = rsqrtf(r2);
-            const float dist   = r2 * rinv;
             const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
-            const float hjInv  = P.w;
-            const float Wi     = hiInv3 * kernelW(dist * hiInv);
-            const float Wj     = hjInv * hjInv * hjInv * kernelW(dist * hjInv);
+            const float hjInv  = P.w, hjInv2 = hjInv * hjInv;
+            const float Wi     = hiInv3 * kernelWt(r2 * (hiInv * hiInv));
+            const float Wj     = hjInv2 * hjInv * kernelWt(r2 * hjInv2);
             const float tA1i   = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
             const float tA2i   = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
             const float tA3i   = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;

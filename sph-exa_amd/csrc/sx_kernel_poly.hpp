@@ -38,23 +38,40 @@ __host__ __device__ __forceinline__ float dsincPolyOverV(float t)
     s       = fmaf(s, t, 0.20293137431144714f);
     return fmaf(s, t, -0.8224664926528931f);
 }
-//! W(v) = sinc6 (sph_kernel_tables.hpp:27-40); 0 beyond the support like lt::lookup's last interval
+//! W(v) = sinc6 (sph_kernel_tables.hpp:27-40); 0 beyond the support like lt::lookup's last interval: t = v^2 is
+//! clamped to 4, where sincPoly evaluates to exactly 0.0f (with or without FMA), so no compare/select is needed
 __host__ __device__ __forceinline__ float kernelW(float v)
 {
-    float s  = sincPoly(v * v);
+    float s  = sincPoly(fminf(v * v, 4.0f));
     float s2 = s * s;
-    return v < 2.0f ? s2 * s2 * s2 : 0.0f;
+    return s2 * s2 * s2;
 }
-//! W and dW/dv = 6 sinc^5 sinc' (sinc6d)
-__host__ __device__ __forceinline__ void kernelWdW(float v, float& w, float& dw)
+//! W as a function of t = v^2 = r^2 / h^2: the pair kernels that need no |r| skip the square root
+__host__ __device__ __forceinline__ float kernelWt(float t)
 {
-    float t  = v * v;
+    float s  = sincPoly(fminf(t, 4.0f));
+    float s2 = s * s;
+    return s2 * s2 * s2;
+}
+//! W and v dW/dv = 6 sinc^5 t sinc'/v as functions of t = v^2
+__host__ __device__ __forceinline__ void kernelWvdWt(float t, float& w, float& vdw)
+{
+    t        = fminf(t, 4.0f);
     float s  = sincPoly(t);
     float s2 = s * s;
     float s4 = s2 * s2;
-    bool  in = v < 2.0f;
-    w        = in ? s4 * s2 : 0.0f;
-    dw       = in ? 6.0f * s4 * s * v * dsincPolyOverV(t) : 0.0f;
+    w        = s4 * s2;
+    vdw      = 6.0f * s4 * s * t * dsincPolyOverV(t);
+}
+//! W and dW/dv = 6 sinc^5 sinc' (sinc6d); both exactly 0 for v >= 2 through the same clamp (s = 0)
+__host__ __device__ __forceinline__ void kernelWdW(float v, float& w, float& dw)
+{
+    float t  = fminf(v * v, 4.0f);
+    float s  = sincPoly(t);
+    float s2 = s * s;
+    float s4 = s2 * s2;
+    w        = s4 * s2;
+    dw       = 6.0f * s4 * s * v * dsincPolyOverV(t);
 }
 
 } // namespace sx
