@@ -938,9 +938,13 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #define SX_SPLIT_AV 2
 #endif
 #ifndef SX_SPLIT_ME
-#define SX_SPLIT_ME 2
+#define SX_SPLIT_ME 3 // 12 waves on the CU's one momentum workgroup (152 VGPRs fit three waves per SIMD)
 #endif
-constexpr int kChXm = 2048, kChVd = 2048, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME, kChMeAvc = 1536;
+#ifndef SX_SPLIT_ME_AVC
+#define SX_SPLIT_ME_AVC 2 // the avClean variant needs 190 VGPRs: two waves per SIMD
+#endif
+// kChVd = 2000: 40 KB of records, four VeDefGradh workgroups per CU (eight waves per SIMD)
+constexpr int kChXm = 2048, kChVd = 2000, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME, kChMeAvc = 1536;
 
 static inline unsigned clusters(const PairArgs& a) { return (a.numGroups + kClusterWaves - 1) / kClusterWaves; }
 
@@ -967,7 +971,7 @@ void avSwitches(const PairArgs& a, hipStream_t s)
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
     if (!a.numGroups) return;
-    if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME, true><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME_AVC, true><<<clusters(a), kB * SX_SPLIT_ME_AVC, 0, s>>>(a);
     else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
 // std propagator: the IAD kernel without velocity derivatives (16 B records), momentum with 68 B records
