@@ -457,6 +457,7 @@ Records records(sx_ctx* c, size_t n)
 
 int checkList(sx_ctx* c, const sx_groups* g, const sx_params* p)
 {
+    if (g->firstBody >= g->lastBody) return SX_OK; // empty range: zero groups, nothing is launched
     if (!c->nbValid || g->firstBody != c->nbFirst || g->lastBody != c->nbLast || p->ngmax != c->nbNgmax)
         return fail(c, SX_ERR_ARG, "no neighbor list for this range: call sx_xmass or sx_find_neighbors first");
     return SX_OK;

@@ -662,6 +662,7 @@ static void launchMomentum(const PairArgs& a, hipStream_t s)
 {
     if (kFastClusters && a.localLists) return cluster::momentumEnergy(a, s);
     if (!a.numGroups) return;
+    if (!a.numGroups) return;
     if (a.avClean) momentumEnergyKernel<true><<<pairGrid(a), kBlock, 0, s>>>(a);
     else momentumEnergyKernel<false><<<pairGrid(a), kBlock, 0, s>>>(a);
 }

@@ -343,3 +343,42 @@ def test_device_sedov_ic_matches_numpy(ctx):
         assert np.array_equal(got[k], st.arrays[k]), k
     assert np.allclose(got["temp"], st.temp, rtol=2e-15, atol=0)  # device exp vs glibc exp: <= 2 ulp
     sim.close()
+
+
+def test_empty_ranges(ctx):
+    """empty target ranges (first == last, zero groups, n == 0) are no-ops that succeed, like the reference's
+    kernels launched on an empty [first, last) (e.g. a rank without particles in a range)"""
+    n = 16
+    st = rand_state(n, 7, clustered=False)
+    obox = po.make_box(-0.5, 0.5, True)
+    box = gutil.box_to_sx(obox)
+    ds = sx.DeviceState(ctx, gutil.host_dict(st))
+    f = ds.fields
+    p = sx.default_params()
+    L, h = ctx.L, ctx.h
+    before = {k: ds.get(k).copy() for k in ("x", "h", "du", "ax", "prho", "c")}
+    g = sx.SxGroups()
+    ctx.check(L.sx_compute_groups(h, 5, 5, C.byref(g)), "groups")
+    assert g.numGroups == 0
+    ctx.check(L.sx_eos(h, 5, 5, 10.0, 5.0 / 3.0, f.temp, f.m, f.kx, f.xm, f.gradh, f.prho, f.c, None, None), "eos")
+    ctx.check(L.sx_xmass_only(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box)), "xmass")
+    ctx.check(L.sx_ve_def_gradh(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box)), "gradh")
+    ctx.check(L.sx_iad_divv_curlv(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box)), "iad")
+    ctx.check(L.sx_av_switches(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box), 1e-6), "av")
+    mdt = C.c_float(0.0)
+    ctx.check(L.sx_momentum_energy(h, C.byref(g), None, C.byref(f), C.byref(p), C.byref(box), C.byref(mdt)), "mom")
+    ctx.check(L.sx_positions(h, 5, 5, 1e-6, 1e-6, C.byref(f), 5.0 / 3.0, 10.0, C.byref(box)), "positions")
+    ctx.check(L.sx_update_h(h, 5, 5, 100, f.nc, f.h), "updateH")
+    out = np.full(9, 7.0)
+    ctx.check(L.sx_conserved_quantities(h, C.byref(f), 5, 5, 10.0, 5.0 / 3.0,
+                                        out.ctypes.data_as(C.POINTER(C.c_double))), "conserved")
+    assert np.all(out == 0.0)
+    keys = ctx.alloc(n, np.uint64)
+    order = ctx.alloc(n, np.uint32)
+    ctx.check(L.sx_sfc_keys(h, f.x, f.y, f.z, keys.ptr, 0, C.byref(box)), "keys")
+    ctx.check(L.sx_sort_keys(h, keys.ptr, order.ptr, 0), "sort")
+    ctx.check(L.sx_gather(h, order.ptr, 0, f.x, f.y, 8), "gather")
+    ctx.check(L.sx_synchronize(h), "sync")
+    for k, v in before.items():
+        assert np.array_equal(ds.get(k), v, equal_nan=True), k
+    ctx.free_all()
