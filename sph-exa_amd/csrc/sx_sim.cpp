@@ -705,11 +705,19 @@ double quantMargin(const DevBox& b)
 int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
 {
     SIM_HIP(sortKeys(s->work, s->keys, s->order, nl, st));
+    GatherSet set{};
     for (auto& sp : s->spares)
     {
-        SIM_HIP(gather(s->order, nl, *sp.field, sp.alt, sp.elemBytes, st));
+        if (set.count == kMaxGatherFields)
+        {
+            SIM_HIP(gatherMany(s->order, nl, set, st));
+            set.count = 0;
+        }
+        set.src[set.count] = *sp.field, set.dst[set.count] = sp.alt, set.bytes[set.count] = sp.elemBytes;
+        ++set.count;
         std::swap(*sp.field, sp.alt);
     }
+    SIM_HIP(gatherMany(s->order, nl, set, st));
     return SX_OK;
 }
 

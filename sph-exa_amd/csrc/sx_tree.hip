@@ -387,6 +387,27 @@ hipError_t gather(const uint32_t* order, size_t n, const void* src, void* dst, i
     return hipGetLastError();
 }
 
+__global__ void gatherManyKernel(const uint32_t* __restrict__ order, size_t n, GatherSet set)
+{
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = order[i];
+    for (int f = 0; f < set.count; ++f) // uniform: every lane walks the same field list
+    {
+        if (set.bytes[f] == 8) static_cast<uint64_t*>(set.dst[f])[i] = static_cast<const uint64_t*>(set.src[f])[o];
+        else static_cast<uint32_t*>(set.dst[f])[i] = static_cast<const uint32_t*>(set.src[f])[o];
+    }
+}
+
+hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hipStream_t s)
+{
+    if (!n || !set.count) return hipSuccess;
+    for (int f = 0; f < set.count; ++f)
+        if (set.bytes[f] != 4 && set.bytes[f] != 8) return hipErrorInvalidValue;
+    gatherManyKernel<<<grid(n), 256, 0, s>>>(order, n, set);
+    return hipGetLastError();
+}
+
 template<class T>
 static hipError_t exclusiveScan(Arena& arena, const char* tag, const T* in, T* out, int n, hipStream_t s)
 {

@@ -197,6 +197,16 @@ hipError_t launchSfcKeys(const double* x, const double* y, const double* z, uint
                          const DevBox& b, hipStream_t s);
 hipError_t sortKeys(Arena& arena, uint64_t* keys, uint32_t* order, size_t n, hipStream_t s);
 hipError_t gather(const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes, hipStream_t s);
+//! up to kMaxGatherFields fields of 4 or 8 bytes reordered by one kernel (the index is read once per particle)
+constexpr int kMaxGatherFields = 16;
+struct GatherSet
+{
+    int         count;
+    const void* src[kMaxGatherFields];
+    void*       dst[kMaxGatherFields];
+    int         bytes[kMaxGatherFields];
+};
+hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hipStream_t s);
 hipError_t buildTree(Arena& arena, const uint64_t* keys, size_t n, uint32_t bucket, const DevBox& box, DevTree& t,
                      hipStream_t s);
 hipError_t nodeCenters(const uint64_t* prefixes, int numNodes, const DevBox& b, double* centers, double* sizes,
