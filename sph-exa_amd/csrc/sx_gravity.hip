@@ -205,7 +205,7 @@ __device__ __forceinline__ void m2pFastV(A (&acc)[4], double tx, double ty, doub
 {
     const float r0 = (float)(tx - c0), r1 = (float)(ty - c1), r2 = (float)(tz - c2);
     const float rr       = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-    const float r_minus1 = rsqrtf(rr);
+    const float r_minus1 = __builtin_amdgcn_rsqf(rr); // raw v_rsq_f32: rr > mac^2 > 0, never denormal
     const float r_minus2 = r_minus1 * r_minus1;
     const float r_minus5 = r_minus2 * r_minus2 * r_minus1;
     const float Qrx      = fmaf(r0, M[1], fmaf(r1, M[2], r2 * M[3]));
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
                     const float  dx = src.x - txr, dy = src.y - tyr, dz = src.z - tzr;
                     const float  R2    = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
                     const float  h_ij  = hi + s_hF[wave][buf][s];
-                    const float  invR  = rsqrtf(fmaxf(R2, h_ij * h_ij));
+                    const float  invR  = __builtin_amdgcn_rsqf(fmaxf(R2, h_ij * h_ij)); // >= h^2: no denormals
                     const float  invR3m = src.w * invR * invR * invR;
                     fa0 = fmaf(-invR3m, R2, fa0);
                     fa1 = fmaf(dx, invR3m, fa1);
