@@ -45,6 +45,12 @@ def test_kernel_poly_matches_sinc6_and_tables():
     dw_ex = np.where(inside, 6 * s ** 5 * ds, 0.0)
     assert np.max(np.abs(w - w_ex)) < 4e-7  # tables: 1.1e-7 (float interpolation of float samples)
     assert np.max(np.abs(dw - dw_ex)) < 1e-6  # tables: 2.2e-7
+    # outside the support both are exactly zero (v^2 clamped to 4, where the polynomial is exactly 0.0f), and so
+    # are NaN arguments (fminf returns the number)
+    far = np.array([2.0, 2.0000002, 2.5, 7.0, 1e30, np.inf, np.nan], np.float32)
+    wf, dwf = np.ones_like(far), np.ones_like(far)
+    assert L.sx_kernel_poly(far.ctypes.data, far.size, wf.ctypes.data, dwf.ctypes.data) == 0
+    assert np.all(wf == 0.0) and np.all(dwf[:-2] == 0.0)
     # the reference tables (linear interpolation, lt::lookup) differ from the exact function by the same order
     wh = np.zeros(sx.KTABLE, np.float32)
     whd = np.zeros(sx.KTABLE, np.float32)
