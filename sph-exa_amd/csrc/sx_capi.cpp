@@ -108,6 +108,7 @@ double quantMargin(const DevBox& b)
 struct sx_ctx
 {
     int         device{0};
+    int         nsLargeRuns{0}; // neighbor search: calls left on the large build after a compact-build overflow
     hipStream_t own{nullptr};
     hipStream_t stream{nullptr};
     bool        exact{false};
@@ -387,6 +388,9 @@ extern "C"
         a.powTab         = ensurePowTab(c, p->ng0);
         a.numLeaves      = tree->numLeafNodes;
         a.qrel           = c->arena.get<float>("ns.qrel", qrelFloats(f->n));
+        a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(1u, last - first));
+        a.flagHost       = c->statsHost;
+        a.largeRuns      = &c->nsLargeRuns;
         if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);

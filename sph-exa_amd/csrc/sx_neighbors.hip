@@ -30,15 +30,29 @@
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
+// Two builds of this file: the default one (large capacities: 2048 candidate leaves, 2^16 candidate particles per
+// cluster, 53 KB of LDS, three workgroups per CU) and, with SX_NS_SMALL, a compact one in namespace sx::small
+// (1024 leaves, 2^14 particles, 28 KB, four workgroups per CU; Makefile).  findNeighbors runs the compact one
+// and falls back to the large one when a cluster exceeds its capacities.
+#ifdef SX_NS_SMALL
 namespace sx
 {
+namespace small
+{
+#else
+namespace sx
+{
+#endif
 
 #ifndef SX_NS_GROUP
 #define SX_NS_GROUP 4
 #endif
 constexpr int kNsGroup = SX_NS_GROUP;
 
-constexpr int kCandSpace = 1 << 16; //!< candidate particles per cluster (u16 list entries)
+#ifndef SX_NS_CAND_LOG2
+#define SX_NS_CAND_LOG2 16
+#endif
+constexpr int kCandSpace = 1 << SX_NS_CAND_LOG2; //!< candidate particles per cluster (u16 list entries)
 constexpr int kSubGroups  = kCluster / 16; //!< 16-particle sub-groups per cluster
 constexpr int kMaxRegions = 128;           //!< search regions per cluster (boxes or particle spheres)
 constexpr int kCandWords = kCandSpace / 32;
@@ -51,7 +65,8 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-constexpr int kDCap = kCandWords * 4 / 16; //!< leaf frames cached in LDS (aliasing s_pre)
+constexpr int kPreWords = kCandWords > 2048 ? kCandWords : 2048; //!< s_pre, also the leaf-frame cache
+constexpr int kDCap     = kPreWords * 4 / 16; //!< leaf frames cached in LDS (aliasing s_pre): 512 in both builds
 
 /*! Frame of a candidate leaf for the float prefilter: d = fold(anchor - o) with anchor = the leaf's first particle
  *  (the frame of the qrel records, leafFrameKernel), o = the cluster origin; .w = Qd + 2|d| (Qd = diagonal of
@@ -107,7 +122,7 @@ findNeighborsKernel(NsArgs a)
     __shared__ uint32_t s_p0[kCCap];    // first particle of candidate leaf cc
     __shared__ uint8_t  s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
     __shared__ uint32_t s_bits[kCandWords];
-    __shared__ uint32_t s_pre[kCandWords];
+    __shared__ uint32_t s_pre[kPreWords];
     __shared__ int      s_nreg;
     __shared__ int      s_again[kClusterWaves];
     __shared__ uint32_t s_wsum[kClusterWaves];
@@ -739,15 +754,53 @@ __global__ void importKernel(uint32_t* nidx, uint32_t first, uint32_t last, uint
         nidx[((size_t)g * ngmax + k) * kWave + lane] = in[(size_t)ni * ngmax + k];
 }
 
-hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
+//! this build's search over [first, last); frames: also (re)compute the float prefilter records
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, bool frames)
 {
     if (a.numGroups == 0) return hipSuccess;
     unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    if (a.qrel && a.numLeaves > 0)
+    if (frames && a.qrel && a.numLeaves > 0)
         leafFrameKernel<<<(a.numLeaves + 3) / 4, 256, 0, s>>>(a.layout, a.numLeaves, a.x, a.y, a.z, a.qrel);
     findNeighborsKernel<<<clusters, kCluster, 0, s>>>(a);
     return hipGetLastError();
 }
+
+#ifndef SX_NS_SMALL
+namespace small
+{
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, bool frames);
+}
+
+hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
+{
+    if (a.numGroups == 0) return hipSuccess;
+    if (!a.hSave || !a.flagHost) return findNeighborsOnce(a, s, true);
+    // after an overflow the next searches go straight to the large build (particle distributions change slowly),
+    // then the compact one is tried again
+    if (a.largeRuns && *a.largeRuns > 0)
+    {
+        --*a.largeRuns;
+        return findNeighborsOnce(a, s, true);
+    }
+    // the compact build spills registers in the hit-append loop: with many neighbors per target (the previous
+    // search's mean, still in flagHost[4..5]) the large build is faster (Noh, ~120: 19 vs 25 ms; Sedov, ~92:
+    // 6.7 vs 5.6 ms).  Both builds give identical results.
+    const uint64_t prevSum = *reinterpret_cast<const uint64_t*>(a.flagHost + 4);
+    if (prevSum > 105ull * (a.last - a.first)) return findNeighborsOnce(a, s, true);
+    const size_t bytes = (size_t)(a.last - a.first) * sizeof(float);
+    hipError_t   e;
+    if ((e = hipMemcpyAsync(a.hSave, a.h + a.first, bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if ((e = small::findNeighborsOnce(a, s, true)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(a.flagHost, a.stats, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if (!(a.flagHost[0] & 6u)) return hipSuccess; // bits 2 / 4: candidate leaves or candidate space exceeded
+    if (a.largeRuns) *a.largeRuns = 64;
+    // redo the whole range with the large build from the saved h (the h-nc iteration mutates h in place)
+    if ((e = hipMemcpyAsync(a.h + a.first, a.hSave, bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.stats, 0, kStatsWords * 4, s)) != hipSuccess) return e;
+    return findNeighborsOnce(a, s, false);
+}
+#endif
 
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s)
 {
@@ -764,4 +817,7 @@ hipError_t importNeighbors(uint32_t* nidx, uint32_t first, uint32_t last, uint32
     return hipGetLastError();
 }
 
+#ifdef SX_NS_SMALL
+} // namespace small
+#endif
 } // namespace sx

@@ -479,6 +479,7 @@ __global__ void unpackGPartKernel(const GPart* in, size_t n, double* x, double* 
 struct sx_sim
 {
     sx_ctx*        ctx;
+    int            nsLargeRuns{0}; // neighbor search: steps left on the large build after a compact-build overflow
     sx::Transport* comm{nullptr};
     sx_params      p;
     sx_box         box;
@@ -1423,7 +1424,10 @@ extern "C"
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
             na.numLeaves      = s->tree.numLeaves;
             na.qrel           = s->mem.get<float>("ns.qrel", qrelFloats(s->n));
-            if (!na.qrel) return SX_ERR_NOMEM;
+            na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(1, s->last - s->first));
+            na.flagHost       = s->statsHost;
+            na.largeRuns      = &s->nsLargeRuns;
+            if (!na.qrel || !na.hSave) return SX_ERR_NOMEM;
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));

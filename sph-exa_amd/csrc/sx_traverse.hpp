@@ -15,7 +15,10 @@ namespace sx
 {
 
 constexpr int kQCap = 512;  //!< internal-node ring per wave (power of 2)
-constexpr int kCCap = 2048; //!< candidate leaves per wave
+#ifndef SX_NS_CCAP
+#define SX_NS_CCAP 2048
+#endif
+constexpr int kCCap = SX_NS_CCAP; //!< candidate leaves per wave
 
 /*! Collect every leaf node passing `overlaps` (whose ancestors all pass) into cand[0..return).
  *  Sets `overflow` if the queue or the candidate list ran out of space (the caller reports an error). */

@@ -181,6 +181,12 @@ struct NsArgs
     int             numLeaves;
     float*          qrel;
     uint32_t*       stats;  // kStatsWords words, see above
+    // optional (both non-null): the search first runs the compact variant (four workgroups per CU) and, if one of its
+    // capacities was exceeded, restores h from hSave (last - first floats) and redoes the range with the large one;
+    // flagHost: one pinned word
+    float*          hSave;
+    uint32_t*       flagHost;
+    int*            largeRuns; // host counter owned by the caller: searches left that go straight to the large build
 
     void setLists(const NbLists& L)
     {
