@@ -6,9 +6,12 @@ A step is one full HydroVeProp step (ve_hydro.hpp:132-218): sync (keys, sort, re
 h iteration, XMass, VeDefGradh, EOS, IAD+divv/curlv, AV switches, momentum/energy, [self-gravity], time-step,
 positions, h update.  --init noh|evrard run BASELINE configs 3 and 5 (lattice substitutes for the glass block).
 Inputs are generated and kept in HBM; nothing leaves the device inside the timed region except the per-step
-4-byte tree-level counts and stats.  Weak scaling: side = round(200 * N^(1/3)) particles^(1/3) in total
-(N=1: Sedov -n 200 = BASELINE config 2; N=8: Sedov -n 400 = config 4).
-Rank 0 prints ONE JSON line.
+4-byte tree-level counts and stats.  The workload is the metric's own: Sedov -n 400 (64M particles) in total at every
+N (strong scaling: N=1 holds all 64M particles on one MI355X, N=8 holds 8M + halos per GPU); --side 200 gives
+BASELINE config 2.
+Rank 0 prints ONE JSON line.  Its "roofline" is the dominant kernel's (largest share of the step): HBM bytes per
+launch from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_latest.json) over the kernel's
+average launch time measured here with HIP events on its stream.
 """
 import argparse
 import json
@@ -23,12 +26,26 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (packed) peak
-MOM_OWN_BYTES = 108    # momentum kernel own record R+W
-MOM_EDGE_BYTES = 4 + 88  # index + neighbor record per edge
+NUM_CU = 256
+CLOCK_HZ = 2.4e9
+# wave64 VALU instructions per second the chip can issue: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 op
+# (measured: VeDefGradh issues faster than one op per 4 cycles per SIMD)
+VALU_ISSUE_PEAK = NUM_CU * 4 * CLOCK_HZ / 2
 MOM_FLOP_PER_PAIR = 150  # SURVEY.md 8(d) secondary VALU figure
-# compulsory HBM bytes of one momentum launch per target, as implemented: own packed records 96 B,
-# nc 4 B, outputs 20 B, u16 neighbor positions 2 B/neighbor, union index 4 B per union entry
-MOM_COMPULSORY_OWN = 96 + 4 + 20
+# SURVEY.md 8(d) edge model per kernel: own record R+W, and index + neighbor record per edge.  Reads of neighbor
+# records come from LDS/L2, so edge-model bytes / time is an EFFECTIVE bandwidth, reported as effective_gbs only.
+EDGE_MODEL = {"findNeighbors": (32, 28), "xmass": (44, 32), "veDefGradh": (48, 36), "iadDivvCurlv": (80, 48),
+              "avSwitches": (88, 52), "momentumEnergy": (108, 92)}
+# compulsory (unique-field) HBM bytes per target as implemented: packed own records + outputs, plus
+# 2 B per stored neighbor (u16 union positions) and 4 B per union entry; the search reads x,y,z,h (28 B) and the
+# tree, writes h, nc and the lists
+COMPULSORY_OWN = {"findNeighbors": 28 + 8, "xmass": 32 + 4 + 4, "veDefGradh": 48 + 4 + 8,
+                  "iadDivvCurlv": 80 + 4 + 28, "avSwitches": 96 + 4 + 4, "momentumEnergy": 96 + 4 + 20}
+# kernel-time slot -> rocprofv3 kernel-name fragments it launches (sx_sim.cpp kev slots)
+PMC_KERNELS = {"findNeighbors": ("findNeighborsKernel", "leafFrameKernel"), "xmass": ("xmassKernel",),
+               "veDefGradh": ("veDefGradhKernel",), "iadDivvCurlv": ("iadDivvCurlv",),
+               "avSwitches": ("avSwitchesKernel",), "momentumEnergy": ("momentumEnergyKernel",),
+               "gravity": ("gravityTraverseKernel",)}
 # std propagator momentum (hydro_std/momentum_energy_kern.hpp): own x,y,z,v,h,m,rho,p,c,c_ij + nc read, a,du written;
 # per edge the index + x,y,z (24) v (12) h m rho p c (20) c_ij (24)
 MOM_STD_OWN_BYTES = 24 + 12 + 20 + 24 + 4 + 12 + 8
@@ -39,23 +56,63 @@ STD_KERNEL_NAMES = {"findNeighbors": "findNeighbors", "xmass": "density", "iadDi
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def pmc_traffic(kernel_prefix, particles):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 --pmc summary of the same workload
-    (scripts/gpu_pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None
-    when the summary was taken on another particle count."""
+def load_pmc(particles, workload):
+    """per-kernel rocprofv3 --pmc summary of the same workload (scripts/gpu_pmc.sh + scripts/pmc_summary.py:
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None when it was taken on another workload"""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("_meta", {}).get("particles_per_gpu") != particles:
+    meta = d.get("_meta", {})
+    if meta.get("particles_per_gpu") != particles or meta.get("workload", "").split(",")[0] != workload.split(",")[0]:
         return None
-    for k, v in d.items():
-        if k == "_meta":
+    return d
+
+
+def pmc_slot(pmc, slot):
+    """counters of one kernel-time slot, summed over the kernels it launches, per launch of the slot"""
+    if pmc is None:
+        return None
+    frags = PMC_KERNELS.get(slot, ())
+    tot, hit = {}, False
+    for k, v in pmc.items():
+        if k == "_meta" or not any(f in k for f in frags):
             continue
-        if kernel_prefix in k and "hbm_read_bytes_est" in v and "hbm_write_bytes_est" in v:
-            return v["hbm_read_bytes_est"] + v["hbm_write_bytes_est"]
-    return None
+        hit = True
+        calls = v.get("calls_per_step", 1.0)
+        for c in ("hbm_read_bytes_est", "hbm_write_bytes_est", "SQ_INSTS_VALU", "SQ_LDS_BANK_CONFLICT",
+                  "profiled_ms"):
+            if c in v:
+                tot[c] = tot.get(c, 0.0) + v[c] * calls
+    return tot if hit else None
+
+
+def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
+    """roofline entry of one kernel-time slot: HBM counter bytes / measured time vs the 8 TB/s peak, VALU issue and
+    LDS conflict shares from the same counters, edge-model effective bandwidth"""
+    own, edge = EDGE_MODEL.get(slot, (0, 0))
+    r = {"avg_launch_ms": ms}
+    if own:
+        r["effective_gbs"] = n_local * (own + ng * edge) / (ms * 1e-3) / 1e9
+    if slot in COMPULSORY_OWN:
+        r["algorithmic_bytes_per_launch"] = n_local * (COMPULSORY_OWN[slot] + 2 * ng + 4 * union_pp)
+        r["algorithmic_frac"] = r["algorithmic_bytes_per_launch"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    c = pmc_slot(pmc, slot)
+    if c and "hbm_read_bytes_est" in c and "hbm_write_bytes_est" in c:
+        traffic = c["hbm_read_bytes_est"] + c["hbm_write_bytes_est"]
+        r["traffic"] = traffic
+        r["achieved"] = traffic / (ms * 1e-3) / 1e9
+        r["frac"] = r["achieved"] / HBM_PEAK_GBS
+    else:
+        r["traffic"] = r["achieved"] = r["frac"] = None
+    if c and "SQ_INSTS_VALU" in c:
+        r["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (ms * 1e-3 * VALU_ISSUE_PEAK)
+    if c and "SQ_LDS_BANK_CONFLICT" in c:
+        r["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / NUM_CU / (ms * 1e-3 * CLOCK_HZ)
+    if c and "profiled_ms" in c:
+        r["pmc_profiled_ms"] = c["profiled_ms"]
+    return r
 
 
 def parse():
@@ -63,12 +120,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--side", type=int, default=0, help="total lattice side (default weak scaling from 200)")
+    ap.add_argument("--side", type=int, default=0,
+                    help="total lattice side (default: the metric's Sedov -n 400 at every N; noh/evrard 300)")
     ap.add_argument("--bucket", type=int, default=64)
     ap.add_argument("--exact", action="store_true", help="use the no-FMA (bit-reproducible) kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="rccl", help="rccl (one GPU per rank) or host (staged, tests)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--cpu-side", type=int, default=200, help="Sedov lattice side of the CPU baseline sample")
     ap.add_argument("--init", default="sedov", choices=["sedov", "noh", "evrard"],
                     help="sedov (BASELINE metric, device IC), noh (config 3), evrard (config 5: VE + self-gravity)")
     ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
@@ -77,8 +136,21 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
-    """Reference CPU path (oracle/_ref, OpenMP) timed on this host on a bounded Sedov sample."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds, side):
+    """Reference CPU path (oracle/_ref, OpenMP) timed on this host on a bounded sample of the same Sedov workload:
+    the lattice of side `side` (n=200: 8M particles, one step ~4 s on 16 cores), one warm-up step, then whole steps
+    until `seconds` have passed (at least one)."""
     import pyoracle as po
 
     kind = "reference"
@@ -88,7 +160,6 @@ def cpu_baseline(seconds):
     if not os.path.exists(path):
         path, kind = po.ORACLE_SO, "port"
     lib = po.Lib(path)
-    side = 50
     st, box = po.sedov_state(side)
     lib.step(st, box)  # warm-up (first touch, thread pool)
     steps, t0 = 0, time.perf_counter()
@@ -100,8 +171,10 @@ def cpu_baseline(seconds):
             break
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     return {"value": st.n * steps / el, "unit": "particle-updates/s", "cores": cores, "kind": kind,
-            "sample": f"Sedov lattice -n {side} ({st.n} particles), {steps} VE steps after 1 warm-up, "
-                      f"{os.path.basename(path)}, OMP threads={cores}"}
+            "cpu_model": cpu_model(),
+            "sample": f"Sedov lattice -n {side} ({st.n} particles, the metric's Sedov IC at 1/8 the particles), "
+                      f"{steps} VE steps after 1 warm-up, {os.path.basename(path)} (the reference's own CPU "
+                      f"loops, -O3 -march=x86-64-v3), OMP threads={cores}"}
 
 
 def main():
@@ -120,8 +193,7 @@ def main():
 
     import sphexa_amd as sx
 
-    default_side = {"sedov": 200, "noh": 300, "evrard": 300}[args.init]
-    side = args.side or int(round(default_side * n_gpus ** (1.0 / 3.0)))
+    side = args.side or {"sedov": 400, "noh": 300, "evrard": 300}[args.init]
     n_total = side ** 3
     ic_arrays = None
     if args.init != "sedov":
@@ -198,15 +270,44 @@ def main():
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
     ng = stats["sumNeighbors"] / max(1, n_local)
-    mom_ms = kern_sum.get("momentumEnergy", float("nan")) / args.steps
-    std_prop = args.prop == "std"
-    own_b, edge_b = (MOM_STD_OWN_BYTES, MOM_STD_EDGE_BYTES) if std_prop else (MOM_OWN_BYTES, MOM_EDGE_BYTES)
-    mom_kernel = "momentumStdKernel" if std_prop else "momentumEnergyKernel"
-    mom_bytes = n_local * (own_b + ng * edge_b)
-    achieved = mom_bytes / (mom_ms * 1e-3) / 1e9
     union_pp = stats["sumUnion"] / max(1, n_local)
-    comp_bytes = n_local * (MOM_COMPULSORY_OWN + 2 * ng + 4 * union_pp)
-    mom_tflops = n_local * ng * MOM_FLOP_PER_PAIR / (mom_ms * 1e-3) / 1e12
+    std_prop = args.prop == "std"
+    kern_ms = {k: v / args.steps for k, v in kern_sum.items()}
+    workload = (f"{args.init.capitalize()} -n {side} ({n_total} particles), "
+                f"{'std (HydroProp)' if std_prop else 'VE'} propagator"
+                f"{' + self-gravity' if args.init == 'evrard' else ''}"
+                f"{' + AV cleaning' if args.av_clean else ''}, {args.steps} steps")
+    pmc = load_pmc(n_local, workload) if not std_prop else None
+    per_kernel = {}
+    for k, ms in kern_ms.items():
+        if ms > 0.01 and (k in EDGE_MODEL or k == "gravity"):
+            per_kernel[k] = kernel_roofline(k, ms, n_local, ng, union_pp, pmc)
+    dominant = max(per_kernel, key=lambda k: per_kernel[k]["avg_launch_ms"]) if per_kernel else "momentumEnergy"
+    dom = per_kernel.get(dominant, {})
+    roofline = {"bound": "hbm", "kernel": dominant, "achieved": dom.get("achieved"), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": dom.get("frac"), "traffic": dom.get("traffic"),
+                "avg_launch_ms": dom.get("avg_launch_ms"),
+                "share_of_step": dom.get("avg_launch_ms", 0.0) / ms_step,
+                "binding": ("valu-issue/latency (HBM frac < 0.5; see valu_issue_frac, lds_conflict_frac)"
+                            if (dom.get("frac") or 0) < 0.5 else "hbm"),
+                "traffic_source": os.path.relpath(PMC_FILE, ROOT) if pmc else None,
+                "definition": "achieved = rocprofv3 PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, same "
+                              "workload) / avg launch time measured live with HIP events; frac = achieved / 8 TB/s; "
+                              "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); lds_conflict_frac = "
+                              "SQ_LDS_BANK_CONFLICT / 256 CUs / (time x 2.4 GHz); effective_gbs = SURVEY 8(d) edge "
+                              "model (neighbor records served from LDS/L2, not a roofline)",
+                **{k: dom[k] for k in ("valu_issue_frac", "lds_conflict_frac", "effective_gbs",
+                                       "algorithmic_bytes_per_launch", "algorithmic_frac") if k in dom},
+                "per_kernel": per_kernel}
+    mom = per_kernel.get("momentumEnergy")
+    if mom and not std_prop:
+        roofline["momentum_valu"] = {"flop_per_pair": MOM_FLOP_PER_PAIR,
+                                     "achieved_tflops": n_local * ng * MOM_FLOP_PER_PAIR /
+                                     (mom["avg_launch_ms"] * 1e-3) / 1e12, "peak_tflops": FP32_PEAK_TFLOPS}
+    if std_prop:
+        mom_ms = kern_ms.get("momentumEnergy", float("nan"))
+        roofline["effective_gbs_momentumStd"] = n_local * (MOM_STD_OWN_BYTES + ng * MOM_STD_EDGE_BYTES) / \
+            (mom_ms * 1e-3) / 1e9
     sc = sim.scalars()
     out = {
         "metric": "particle-updates/sec (whole node), Sedov -n 400, 1/2/4/8 MI355X + HBM roofline %",
@@ -217,15 +318,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32 hydro / f64 coordinates (sph::SphTypes)",
         "data": "synthetic Sedov lattice generated on device (sedov_init.hpp), no checkpoint" if ic_arrays is None
                 else f"synthetic {args.init} lattice substitute for the glass block (SURVEY F6), sphexa_amd/ic.py",
-        "config": {"workload": f"{args.init.capitalize()} -n {side} ({n_total} particles), "
-                               f"{'std (HydroProp)' if std_prop else 'VE'} propagator"
-                               f"{' + self-gravity' if args.init == 'evrard' else ''}"
-                               f"{' + AV cleaning' if args.av_clean else ''}, {args.steps} steps",
+        "config": {"workload": workload,
                    "particles_per_gpu": n_local, "bucket": args.bucket, "ngmax": 150, "ng0": 100,
                    "parallelism": "1 GPU" if world == 1 else
                    f"{world} GPUs: SFC domain decomposition, halo + particle exchange over {transport}",
@@ -234,26 +332,17 @@ def main():
                        "gravity_far_cells": sim.gravity_stats()["far_cells"]} if world > 1 and args.init == "evrard"
                       else {}),
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
-        "roofline": {"bound": "hbm", "kernel": mom_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(mom_kernel, n_local),
-                     "algorithmic_bytes_per_launch": mom_bytes, "avg_launch_ms": mom_ms,
-                     "model": f"edge model (SURVEY.md 8(d)): {own_b} B own + {ng:.1f} neighbors x "
-                              f"{edge_b} B; effective bandwidth, neighbor records come from LDS",
-                     "compulsory_bytes_per_launch": comp_bytes,
-                     "compulsory_frac": comp_bytes / (mom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "valu": {"flop_per_pair": MOM_FLOP_PER_PAIR, "achieved_tflops": mom_tflops,
-                              "peak_tflops": FP32_PEAK_TFLOPS, "frac": mom_tflops / FP32_PEAK_TFLOPS},
-                     "traffic_source": os.path.relpath(PMC_FILE, ROOT)},
-        "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v / args.steps for k, v in kern_sum.items()
+        "roofline": roofline,
+        "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_ms.items()
                        if not std_prop or k in STD_KERNEL_NAMES},
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
         "neighbors_per_particle": ng,
         "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),
-        "union_per_particle": stats["sumUnion"] / max(1, n_local),
+        "union_per_particle": union_pp,
         "minDt": sc["minDt"],
     }
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_side)
     sim.close()
     if comm is not None:
         comm.close()

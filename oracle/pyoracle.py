@@ -398,6 +398,11 @@ class Lib:
         return r
 
 
+def ref_available():
+    """oracle/_ref was built here (checked without mapping the library into the process)"""
+    return os.path.exists(REF_SO)
+
+
 def load_ref():
     """The reference's own CPU path, or None when it was not built (e.g. on the GPU box without the .so)."""
     if not os.path.exists(REF_SO):

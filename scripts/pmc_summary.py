@@ -10,7 +10,7 @@ from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "p*", "pmc_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -19,6 +19,7 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "pmc_counter_collection.csv")
 out = {}
 for k, cs in acc.items():
     d = {c: sum(v) / len(v) for c, v in cs.items()}
+    d["dispatches"] = max(len(v) for v in cs.values())  # per pass: each counter is collected in one pass
     if "FETCH_SIZE" in d:
         d["hbm_read_bytes_est"] = 2 * d["FETCH_SIZE"] * 1024  # KB units, x2 gfx950 correction
     if "WRITE_SIZE" in d:
@@ -42,8 +43,12 @@ if len(sys.argv) > 2:
             if line.startswith("{"):
                 try:
                     d = json.loads(line)
-                    meta = {"particles_per_gpu": d["config"]["particles_per_gpu"], "workload": d["config"]["workload"]}
+                    meta = {"particles_per_gpu": d["config"]["particles_per_gpu"], "workload": d["config"]["workload"],
+                            "steps_per_pass": d["steps"] + d["warmup"]}
                 except (ValueError, KeyError):
                     pass
+    for k, d in out.items():
+        if meta.get("steps_per_pass"):
+            d["calls_per_step"] = d["dispatches"] / meta["steps_per_pass"]
     out["_meta"] = meta
     json.dump(out, open(sys.argv[2], "w"), indent=1)

@@ -59,7 +59,7 @@ def test_gravity_steps_golden(ora):
 
 
 @pytest.mark.ref
-@pytest.mark.skipif(po.load_ref() is None, reason="oracle/_ref not built (no /root/reference here)")
+@pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built (no /root/reference here)")
 @pytest.mark.parametrize("side,theta", [(16, 0.5), (20, 0.3), (20, 0.8)])
 def test_gravity_vs_reference(ora, side, theta):
     ref = po.load_ref()

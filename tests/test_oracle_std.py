@@ -11,8 +11,12 @@ import pytest
 import golden_util as gu
 import pyoracle as po
 
-ref = po.load_ref()
-needs_ref = pytest.mark.skipif(ref is None, reason="oracle/_ref not built")
+needs_ref = pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built")
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return po.load_ref()  # loaded only by the tests that need it (never on the GPU box, where it is absent)
 
 # sph/test/std.cpp:57-87 -- five particles in the open box [0,6]^3, particle 0 against neighbors 1..4 (data)
 KAT = {
@@ -109,7 +113,7 @@ def test_std_kernels_golden():
 
 
 @needs_ref
-def test_reference_std_kat_double():
+def test_reference_std_kat_double(ref):
     """the reference's own std loops (T=double) reproduce the std.cpp assertions with their tolerances"""
     cols = np.array([[KAT[c][i] for c in COLS] + [0.0, 0.0] for i in range(5)], np.float64)
     out = np.zeros(11)
@@ -125,7 +129,7 @@ def test_reference_std_kat_double():
 
 @needs_ref
 @pytest.mark.parametrize("ic,side,steps", [("sedov", 12, 4), ("noh", 14, 4)])
-def test_full_steps_std(ic, side, steps):
+def test_full_steps_std(ref, ic, side, steps):
     """HydroProp steps: density, EOS_HydroStd, IAD, momentumEnergySTD, time-step without the rho limit"""
     ora = po.load_oracle()
     st, box = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
@@ -161,7 +165,7 @@ def random_sorted_state(lib, n, seed):
 
 
 @needs_ref
-def test_std_kernels_random():
+def test_std_kernels_random(ref):
     """each std kernel alone on a clustered periodic state with random masses and velocities"""
     ora = po.load_oracle()
     st, box = random_sorted_state(ora, 3000, 11)

@@ -8,8 +8,12 @@ import pytest
 
 import pyoracle as po
 
-ref = po.load_ref()
-pytestmark = [pytest.mark.ref, pytest.mark.skipif(ref is None, reason="oracle/_ref not built")]
+pytestmark = [pytest.mark.ref, pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built")]
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return po.load_ref()
 
 
 @pytest.fixture(scope="module")
@@ -17,7 +21,7 @@ def ora():
     return po.load_oracle()
 
 
-def test_tables_and_update_h(ora):
+def test_tables_and_update_h(ora, ref):
     assert ora.K == ref.K
     assert np.array_equal(ora.wh, ref.wh) and np.array_equal(ora.whd, ref.whd)
     for nc in range(1, 2500):
@@ -36,7 +40,7 @@ def rand_state(n, seed, clustered=True):
 
 @pytest.mark.parametrize("bucket", [64, 16, 1])
 @pytest.mark.parametrize("periodic", [True, False])
-def test_tree_neighbors(ora, bucket, periodic):
+def test_tree_neighbors(ora, ref, bucket, periodic):
     st = rand_state(6000, 7 + bucket)
     box = po.make_box(-0.5, 0.5, periodic)
     keys = ref.sfc_keys(st, box).copy()
@@ -60,7 +64,7 @@ def test_tree_neighbors(ora, bucket, periodic):
 
 
 @pytest.mark.parametrize("ic,side,steps", [("sedov", 12, 4), ("noh", 14, 4)])
-def test_full_steps(ora, ic, side, steps):
+def test_full_steps(ora, ref, ic, side, steps):
     st, box = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
     a, b = st.copy(), st.copy()
     for _ in range(steps):
@@ -72,7 +76,7 @@ def test_full_steps(ora, ic, side, steps):
 
 
 @pytest.mark.parametrize("ic,side,steps", [("sedov", 12, 4), ("noh", 14, 4)])
-def test_full_steps_av_clean(ora, ic, side, steps):
+def test_full_steps_av_clean(ora, ref, ic, side, steps):
     """HydroVeProp<avClean=true>: IAD writes the velocity gradient (divv_curlv_kern.hpp:113-121), momentum adds
     avRvCorrection (momentum_energy_kern.hpp:43-63, 157-161); bit-exact against the reference's template"""
     st, box = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
