@@ -161,6 +161,8 @@ typedef struct sx_nbstats
     uint32_t numFailed;      /* h-nc iteration failures */
     uint64_t sumCandidates;  /* candidate particles tested (per target, summed) */
     uint64_t sumUnion;       /* cluster neighbor-union entries, summed over 256-particle clusters */
+    uint32_t build;          /* search build used: 0 compact, 1 large, 2 compact overflowed and redone by the large */
+    uint32_t reserved;
 } sx_nbstats;
 
 typedef struct sx_ctx sx_ctx;

@@ -108,7 +108,7 @@ double quantMargin(const DevBox& b)
 struct sx_ctx
 {
     int         device{0};
-    int         nsLargeRuns{0}; // neighbor search: calls left on the large build after a compact-build overflow
+    NsPolicy    nsPolicy;       // neighbor search: compact or large build (sx_tree.hpp)
     hipStream_t own{nullptr};
     hipStream_t stream{nullptr};
     bool        exact{false};
@@ -207,6 +207,7 @@ extern "C"
         tablePairs(tmp + kTableSize, c->whd, c->stream);
         c->stats      = c->arena.get<uint32_t>("stats", kStatsWords);
         c->statsHost  = c->arena.pinned<uint32_t>("statsHost", kStatsWords);
+        if (c->statsHost) std::fill(c->statsHost, c->statsHost + kStatsWords, 0u);
         c->minDt      = c->arena.get<float>("minDt", 1);
         c->maxU       = c->arena.get<unsigned>("maxU", 1);
         c->hostScalar = c->arena.pinned<float>("hostScalar", 2);
@@ -386,11 +387,9 @@ extern "C"
         a.margin         = quantMargin(a.box);
         a.stats          = c->stats;
         a.powTab         = ensurePowTab(c, p->ng0);
-        a.numLeaves      = tree->numLeafNodes;
-        a.qrel           = c->arena.get<float>("ns.qrel", qrelFloats(f->n));
+        a.prefilter      = 1;
         a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(1u, last - first));
-        a.flagHost       = c->statsHost;
-        a.largeRuns      = &c->nsLargeRuns;
+        a.policy         = &c->nsPolicy;
         if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);
@@ -398,6 +397,7 @@ extern "C"
         SX_HIP(c, findNeighbors(a, c->stream));
         SX_HIP(c, hipMemcpyAsync(c->statsHost, c->stats, kStatsWords * 4, hipMemcpyDeviceToHost, c->stream));
         SX_HIP(c, hipStreamSynchronize(c->stream));
+        c->nsPolicy.observe(c->statsHost, last - first);
         c->nbFirst = first;
         c->nbLast  = last;
         c->nbNgmax = p->ngmax;
@@ -409,6 +409,8 @@ extern "C"
             stats->sumNeighbors  = *reinterpret_cast<uint64_t*>(c->statsHost + 4);
             stats->sumCandidates = *reinterpret_cast<uint64_t*>(c->statsHost + 6);
             stats->sumUnion      = *reinterpret_cast<uint64_t*>(c->statsHost + 8);
+            stats->build         = c->nsPolicy.lastBuild;
+            stats->reserved      = 0;
         }
         if (c->statsHost[0] & 1u) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in neighbor search");
         if (iterate_h && c->statsHost[1]) return fail(c, SX_ERR_NOT_CONVERGED, "coupled nc/h-updated failed to converge");

@@ -65,50 +65,6 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-constexpr int kPreWords = kCandWords > 2048 ? kCandWords : 2048; //!< s_pre, also the leaf-frame cache
-constexpr int kDCap     = kPreWords * 4 / 16; //!< leaf frames cached in LDS (aliasing s_pre): 512 in both builds
-
-/*! Frame of a candidate leaf for the float prefilter: d = fold(anchor - o) with anchor = the leaf's first particle
- *  (the frame of the qrel records, leafFrameKernel), o = the cluster origin; .w = Qd + 2|d| (Qd = diagonal of
- *  the leaf box inflated by the key-quantisation margin, bounding |x_j - anchor|), or -1 when on some periodic
- *  axis |d| + width reaches L/2 (the records might then sit in another image than the fold picks). */
-__device__ __forceinline__ float4 leafFrame(const NsArgs& a, int node, uint32_t p0, double ox, double oy, double oz)
-{
-    const double dx = foldPbc(a.x[p0] - ox, a.box, 0), dy = foldPbc(a.y[p0] - oy, a.box, 1),
-                 dz = foldPbc(a.z[p0] - oz, a.box, 2);
-    const double wx = 2.0 * (a.sizes[3 * (size_t)node] + a.margin),
-                 wy = 2.0 * (a.sizes[3 * (size_t)node + 1] + a.margin),
-                 wz = 2.0 * (a.sizes[3 * (size_t)node + 2] + a.margin);
-    bool ok = true;
-    if (a.box.pbc[0] && fabs(dx) + wx >= 0.499 * a.box.l[0]) ok = false;
-    if (a.box.pbc[1] && fabs(dy) + wy >= 0.499 * a.box.l[1]) ok = false;
-    if (a.box.pbc[2] && fabs(dz) + wz >= 0.499 * a.box.l[2]) ok = false;
-    const double E0 = (sqrt(wx * wx + wy * wy + wz * wz) + 2.0 * sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-5);
-    return make_float4((float)dx, (float)dy, (float)dz, ok ? (float)E0 : -1.0f);
-}
-
-//! per-particle records of the float prefilter in pair layout: pair p = particles (2p, 2p+1) holds
-//! {qx_a, qx_b, qy_a, qy_b, qz_a, qz_b, qw_a, qw_b} with q = x - anchor(leaf) in f32 and qw = |q|^2; one wave per leaf
-__global__ void leafFrameKernel(const uint32_t* __restrict__ layout, int numLeaves, const double* __restrict__ x,
-                                const double* __restrict__ y, const double* __restrict__ z, float* __restrict__ q)
-{
-    const int L    = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (L >= numLeaves) return;
-    const uint32_t p0 = layout[L], p1 = layout[L + 1];
-    if (p1 <= p0) return;
-    const double ax = x[p0], ay = y[p0], az = z[p0];
-    for (uint32_t j = p0 + lane; j < p1; j += 64)
-    {
-        const float qx = (float)(x[j] - ax), qy = (float)(y[j] - ay), qz = (float)(z[j] - az);
-        float*      P  = q + (size_t)(j >> 1) * 8 + (j & 1);
-        P[0]           = qx;
-        P[2]           = qy;
-        P[4]           = qz;
-        P[6]           = qx * qx + qy * qy + qz * qz;
-    }
-}
-
 #ifndef SX_NS_WAVES_PER_EU
 #define SX_NS_WAVES_PER_EU 3
 #endif
@@ -122,21 +78,25 @@ findNeighborsKernel(NsArgs a)
     __shared__ uint32_t s_p0[kCCap];    // first particle of candidate leaf cc
     __shared__ uint8_t  s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
     __shared__ uint32_t s_bits[kCandWords];
-    __shared__ uint32_t s_pre[kPreWords];
+    __shared__ uint32_t s_pre[kCandWords];
     __shared__ int      s_nreg;
     __shared__ int      s_again[kClusterWaves];
     __shared__ uint32_t s_wsum[kClusterWaves];
-    __shared__ float4   s_chunk[kClusterWaves][2][kWave]; // per wave: double-buffered leaf-frame pair records
+    // per wave: [0] 64 staged candidate records (pair layout), [1] the candidate index of each staged slot
+    __shared__ float4   s_chunk[kClusterWaves][2][kWave];
     __shared__ int      s_numCand;
-    // leaf frames of the first kDCap candidate leaves; s_pre is only used after the last stream
-    float4* const s_d = reinterpret_cast<float4*>(s_pre);
     // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}; s_chunk is only used inside the stream
     double4* const s_reg = reinterpret_cast<double4*>(&s_chunk[0][0][0]);
     static_assert(sizeof(s_chunk) >= 2 * kMaxRegions * sizeof(double4), "search regions alias s_chunk");
 
+    // the fallback launch (a.gate) is a small persistent grid that exits at once unless the compact build overflowed
+    if (a.gate && *a.gate == 0u) return;
+    const uint32_t numClusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    for (uint32_t blk = blockIdx.x; blk < numClusters; blk += gridDim.x)
+    {
     const int      wave  = threadIdx.x >> 6;
     const int      lane  = threadIdx.x & 63;
-    const uint32_t c     = xcdBlock(blockIdx.x, gridDim.x);
+    const uint32_t c     = gridDim.x >= numClusters ? xcdBlock(blk, numClusters) : blk;
     const uint32_t g     = c * kClusterWaves + wave;
     const uint32_t c0    = a.first + c * kCluster;
     const uint32_t i     = c0 + threadIdx.x;
@@ -294,7 +254,6 @@ findNeighborsKernel(NsArgs a)
         {
             const int node = s_cand[cc];
             s_reach[cc]    = (uint8_t)reachMask(node, false);
-            if (cc < kDCap && a.qrel) s_d[cc] = leafFrame(a, node, s_p0[cc], ox, oy, oz);
         }
         if (local)
         {
@@ -309,15 +268,15 @@ findNeighborsKernel(NsArgs a)
         const uint64_t tS = __builtin_readcyclecounter();
 #endif
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
-        const float  r2f       = 4.0f * hi * hi;
-        const double radSq     = (double)r2f;
-        const double tw        = 2.0 * (double)hi;
-        const bool   inside    = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) &&
-                            (zi - tw >= a.box.lim[4]) && (xi + tw <= a.box.lim[1]) &&
-                            (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
-        const bool   usePbc    = a.box.anyPbc && !inside;
-        // float prefilter: cluster-relative minimum-image coordinates are exact displacements for every pair
-        // closer than 2h when |x_i - o| + 2h < L/2 on the periodic axes
+        const float  r2f    = 4.0f * hi * hi;
+        const double radSq  = (double)r2f;
+        const double tw     = 2.0 * (double)hi;
+        const bool   inside = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) && (zi - tw >= a.box.lim[4]) &&
+                            (xi + tw <= a.box.lim[1]) && (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
+        const bool   usePbc = a.box.anyPbc && !inside;
+        // float prefilter in the cluster frame: p = fold(x - o) (minimum image relative to the cluster origin).  For
+        // a lane with |r| + 2h < L/2 on the periodic axes (r = its own p) every neighbor closer than 2h sits at
+        // p_j = r + d with d the minimum-image displacement, and any other image is farther: |p_j - r| >= distance
         const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
                     zr = (float)foldPbc(zi - oz, a.box, 2);
         bool safe = true;
@@ -326,14 +285,57 @@ findNeighborsKernel(NsArgs a)
             const float rd = d == 0 ? xr : (d == 1 ? yr : zr);
             if (a.box.pbc[d] && (fabsf(rd) + 2.05f * hi) >= 0.49f * (float)a.box.l[d]) safe = false;
         }
-        const bool  fastWave = a.qrel != nullptr && __ballot(valid && !safe) == 0;
+        const bool  fastWave = a.prefilter != 0 && __ballot(valid && !safe) == 0;
         const float thr      = valid ? r2f : -1e30f; // invalid lanes: t ~ +1e30, never a hit, never ambiguous
-        const float rn2      = 2.0f * sqrtf(xr * xr + yr * yr + zr * zr);
+        // per-candidate cull against the wave's box of r grown by 2 hmax (exact displacement argument above, with a
+        // relative margin for the f32 rounding of p and r); a culled candidate is farther than 2h from every lane
+        float blo[3] = {valid ? xr : 3e38f, valid ? yr : 3e38f, valid ? zr : 3e38f};
+        float bhi[3] = {valid ? xr : -3e38f, valid ? yr : -3e38f, valid ? zr : -3e38f};
+        float hw     = valid ? hi : 0.0f;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1)
+        {
+            for (int d = 0; d < 3; ++d)
+            {
+                blo[d] = fminf(blo[d], __shfl_xor(blo[d], o, kWave));
+                bhi[d] = fmaxf(bhi[d], __shfl_xor(bhi[d], o, kWave));
+            }
+            hw = fmaxf(hw, __shfl_xor(hw, o, kWave));
+        }
+        const float bcx = 0.5f * (blo[0] + bhi[0]), bcy = 0.5f * (blo[1] + bhi[1]), bcz = 0.5f * (blo[2] + bhi[2]);
+        const float bsx = 0.5f * (bhi[0] - blo[0]), bsy = 0.5f * (bhi[1] - blo[1]), bsz = 0.5f * (bhi[2] - blo[2]);
+        const float bmag  = fmaxf(fabsf(blo[0]), fabsf(bhi[0])) + fmaxf(fabsf(blo[1]), fabsf(bhi[1])) +
+                           fmaxf(fabsf(blo[2]), fabsf(bhi[2]));
+        const float cullR = 2.0f * hw * (1.0f + 0x1p-12f) + 0x1p-16f * (bmag + 2.0f * hw);
+        const float cullR2 = (fastWave && hw > 0.0f) ? cullR * cullR : 3e38f;
+        // bound on |p| + |r| over every staged candidate and lane: the error scale of the packed test
+        const float E   = bmag + cullR + sqrtf(xr * xr + yr * yr + zr * zr);
+        const float tol = valid ? 0x1p-19f * fmaf(E, E, thr) : 0.0f;
+        const float cr  = fmaf(xr, xr, fmaf(yr, yr, fmaf(zr, zr, -thr))); // |r|^2 - 4h^2
+        const v2f   mrx = {-2.0f * xr, -2.0f * xr}, mry = {-2.0f * yr, -2.0f * yr}, mrz = {-2.0f * zr, -2.0f * zr},
+                  c2 = {cr, cr};
+        float*         srec   = reinterpret_cast<float*>(&s_chunk[wave][0]); // 64 slots, pair layout
+        uint32_t*      sci    = reinterpret_cast<uint32_t*>(&s_chunk[wave][1][0]); // candidate index per slot
 
-        // the reference criterion in double for candidates [s0, s0 + m): this lane's hits as bits from s0
-        auto exactChunk = [&](uint32_t s0, int m) -> uint64_t {
+        // candidate index -> global particle index (s_cOff ascending in cc): only for the rare exact chunks
+        auto globalOf = [&](uint32_t ci) -> uint32_t {
+            int lo = 0, hi2 = numCand - 1;
+            while (lo < hi2)
+            {
+                const int mid = (lo + hi2 + 1) >> 1;
+                if (s_cOff[mid] <= ci) lo = mid;
+                else hi2 = mid - 1;
+            }
+            return s_p0[lo] + (ci - s_cOff[lo]);
+        };
+        // the reference criterion in double for the m staged slots: this lane's hits as slot bits
+        auto exactChunk = [&](int m) -> uint64_t {
             double xj = 0, yj = 0, zj = 0;
-            if (lane < m) xj = a.x[s0 + lane], yj = a.y[s0 + lane], zj = a.z[s0 + lane];
+            if (lane < m)
+            {
+                const uint32_t j = globalOf(sci[lane]);
+                xj = a.x[j], yj = a.y[j], zj = a.z[j];
+            }
             uint64_t hm = 0;
             for (int k = 0; k < m; ++k)
             {
@@ -346,7 +348,7 @@ findNeighborsKernel(NsArgs a)
                     dy = foldPbc(dy, a.box, 1);
                     dz = foldPbc(dz, a.box, 2);
                 }
-                if (valid && (dx * dx + dy * dy + dz * dz < radSq) && s0 + k != i) hm |= 1ull << k;
+                if (valid && (dx * dx + dy * dy + dz * dz < radSq)) hm |= 1ull << k;
             }
             return hm;
         };
@@ -354,106 +356,34 @@ findNeighborsKernel(NsArgs a)
         count         = 0;
         stored        = 0;
         uint32_t pend = 0; // low half of the next u16-pair word
-        // chunk sequence of this wave: (candidate leaf cc, even start s0a) in stream order, chunks of 64 candidate
-        // slots aligned to particle pairs; the next chunk's leaf-frame pairs are prefetched into registers.
-        // Reachable non-empty leaves are found 64 at a time: lane l of the window holds leaf wb + l, a ballot gives
-        // the window's reachable set (wave-uniform scalar iteration, no dependent LDS reads per leaf)
-        const uint32_t wbit = 1u << wave;
-        struct Chunk
-        {
-            int      cc;
-            uint32_t s0a, p0, p1, base;
-        };
-        int      wb  = -kWave;
-        uint64_t rm  = 0;
-        uint32_t wp0 = 0, wcnt = 0, wco = 0;
-        auto     advance = [&](Chunk& q) {
-            if (q.cc >= 0 && q.cc < numCand && q.s0a + kWave < q.p1)
-            {
-                q.s0a += kWave;
-                return;
-            }
-            while (rm == 0)
-            {
-                wb += kWave;
-                if (wb >= numCand)
-                {
-                    q.cc = numCand;
-                    return;
-                }
-                const int l = wb + lane;
-                wp0 = 0, wcnt = 0, wco = 0;
-                bool r = false;
-                if (l < numCand)
-                {
-                    wp0  = s_p0[l];
-                    wco  = s_cOff[l];
-                    wcnt = s_cOff[l + 1] - wco;
-                    r    = (s_reach[l] & wbit) && wcnt > 0;
-                }
-                rm = __ballot(r);
-            }
-            const int k = __builtin_ctzll(rm);
-            rm &= rm - 1ull;
-            q.cc   = wb + k;
-            q.p0   = __builtin_amdgcn_readlane(wp0, k);
-            q.p1   = q.p0 + __builtin_amdgcn_readlane(wcnt, k);
-            q.base = __builtin_amdgcn_readlane(wco, k) - q.p0;
-            q.s0a  = q.p0 & ~1u;
-        };
-        auto fetchPairs = [&](const Chunk& q) -> float4 {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (fastWave && q.cc < numCand)
-            {
-                const uint32_t e = min(q.s0a + kWave, q.p1);
-                if ((uint32_t)lane < 2 * ((e - q.s0a + 1) >> 1))
-                    v = reinterpret_cast<const float4*>(a.qrel)[(size_t)(q.s0a >> 1) * 2 + lane];
-            }
-            return v;
-        };
-        // software pipeline: chunk k is tested from LDS buffer k%2 while chunk k+1 (loaded into registers during
-        // chunk k-1) is staged into the other buffer, and the load of chunk k+2 is issued before chunk k's list
-        // stores (vmcnt also counts stores: a load issued after them would make its wait cover them too)
-        Chunk cur{-1, 0, 0, 0, 0};
-        advance(cur);
-        Chunk nxt = cur;
-        advance(nxt);
-        int buf = 0;
-        s_chunk[wave][0][lane] = fetchPairs(cur);
-        float4 pfn             = fetchPairs(nxt);
-        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-        while (cur.cc < numCand)
-        {
-            const int      cc = cur.cc;
-            const uint32_t p0 = cur.p0, p1 = cur.p1, s0a = cur.s0a;
-            const uint32_t base = cur.base; // candidate index of particle j = base + j
-            const uint32_t s0 = max(s0a, p0), e = min(s0a + kWave, p1);
-            const int      m  = (int)(e - s0);
-            candTested += m;
+        uint32_t seq     = 0;           // candidates tested before the current chunk (wave-uniform)
+        uint32_t selfSeq = 0xffffffffu; // stream sequence number of this lane's own particle once staged
+        int      fill    = 0;
 
-            // leaf frame: d = fold(anchor - o) (anchor = the leaf's first particle), w = error-bound extent, < 0 when
-            // the leaf may straddle a periodic image
-            float4 dd = make_float4(0.f, 0.f, 0.f, -1.f);
-            if (fastWave) dd = cc < kDCap ? s_d[cc] : leafFrame(a, s_cand[cc], p0, ox, oy, oz);
+        // test the fill staged slots, update counts, union bitmap and this lane's list
+        auto testChunk = [&]() {
+            const int m = fill;
+            candTested += m;
+            // pad the group of 8 with far-away records (t ~ 1e36: no hit, not ambiguous)
+            const int mp = (m + 7) & ~7;
+            if (lane >= m && lane < mp)
+            {
+                float* P = srec + (lane >> 1) * 8 + (lane & 1);
+                P[0] = 1e18f, P[2] = 1e18f, P[4] = 1e18f, P[6] = 3e36f;
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): staged and padded slots have landed
+            __builtin_amdgcn_wave_barrier();
             uint64_t hm;
-            bool     exact = !(fastWave && dd.w >= 0.0f);
+            bool     exact = !fastWave;
             if (!exact)
             {
-                // t = |q - r'|^2 - 4h^2 = qw + (r'.r' - 4h^2) - 2 q.r' per candidate pair (packed f32, q from LDS);
-                // hit = sign bit of t, gathered by v_alignbit; |t| < tol (error bound) defers the chunk to the exact
-                // double test
-                const float rx = xr - dd.x, ry = yr - dd.y, rz = zr - dd.z;
-                const float c  = fmaf(rx, rx, fmaf(ry, ry, fmaf(rz, rz, -thr)));
-                const float E  = dd.w + rn2;
-                const float tol = valid ? 0x1p-19f * fmaf(E, E, thr) : 0.0f;
-                const v2f   mrx = {-2.0f * rx, -2.0f * rx}, mry = {-2.0f * ry, -2.0f * ry},
-                          mrz = {-2.0f * rz, -2.0f * rz}, c2 = {c, c};
-                const float4* sc = s_chunk[wave][buf];
+                // t = |p - r|^2 - 4h^2 = pw + (|r|^2 - 4h^2) - 2 p.r per candidate pair (packed f32, p from LDS);
+                // hit = sign bit of t, gathered by v_alignbit; |t| < tol defers the chunk to the exact double test
+                const float4* sc = reinterpret_cast<const float4*>(srec);
 #ifdef SX_NS_PROFILE
                 const uint64_t tT = __builtin_readcyclecounter();
 #endif
-                const int ng = (int)((e - s0a + 7) >> 3); // groups of 8 candidates (4 pairs)
+                const int ng  = mp >> 3; // groups of 8 candidates (4 pairs)
                 uint32_t  acc = 0, wlo = 0, whi = 0;
                 float     am  = 3.0e38f;
                 for (int g = 0; g < ng; ++g)
@@ -482,18 +412,13 @@ findNeighborsKernel(NsArgs a)
                 if (__ballot(am < tol)) exact = true;
                 else
                 {
-                    hm = ((uint64_t)wlo | ((uint64_t)whi << 32)) >> (s0 - s0a);
+                    hm = (uint64_t)wlo | ((uint64_t)whi << 32);
                     if (m < 64) hm &= (1ull << m) - 1ull;
-                    if (i >= s0 && i < e) hm &= ~(1ull << (i - s0)); // j != i
                 }
             }
-            if (exact) hm = exactChunk(s0, m); // (its loads complete before the prefetch below is issued)
-            // stage chunk k+1, issue the load of chunk k+2
-            __builtin_amdgcn_wave_barrier();
-            s_chunk[wave][buf ^ 1][lane] = pfn;
-            cur                          = nxt;
-            advance(nxt);
-            pfn = fetchPairs(nxt);
+            if (exact) hm = exactChunk(m);
+            const uint32_t sd = selfSeq - seq;
+            if (sd < (uint32_t)m) hm &= ~(1ull << sd); // j != i
 #ifdef SX_NS_PROFILE
             const uint64_t tP = __builtin_readcyclecounter();
             prof[5] += (exact ? (1ull << 32) : 0ull) + 1ull;
@@ -516,30 +441,43 @@ findNeighborsKernel(NsArgs a)
             uint64_t lm = hm;
             if (local)
             {
-                const uint32_t b0 = base + s0; // candidate index of the chunk's first particle
+                // union bitmap: slot k hit by some lane -> its candidate bit
                 const uint64_t wm = waveOr64(lm);
-                if (wm && lane < 3)
+                if (lane < m && ((wm >> lane) & 1ull))
                 {
-                    // bits [b0, b0+64) of the bitmap span up to three words
-                    const uint32_t sh = b0 & 31, w0 = b0 >> 5;
-                    uint32_t       part;
-                    if (lane == 0) part = (uint32_t)(wm << sh);
-                    else if (lane == 1) part = sh ? (uint32_t)(wm >> (32 - sh)) : (uint32_t)(wm >> 32);
-                    else part = sh ? (uint32_t)(wm >> (64 - sh)) : 0u;
-                    if (part) atomicOr(&s_bits[w0 + lane], part);
+                    const uint32_t ci = sci[lane];
+                    atomicOr(&s_bits[ci >> 5], 1u << (ci & 31));
                 }
+#ifdef SX_NS_UAPPEND
+                // append by a wave-uniform walk over the slots some lane hit: the slot's candidate index is
+                // broadcast from the lane that staged it (v_readlane), each hitting lane appends it
+                const uint32_t ciLane = lane < m ? sci[lane] : 0u;
+                uint64_t       wr     = wm;
+                while (wr)
+                {
+                    const int      k = __builtin_ctzll(wr);
+                    wr &= wr - 1ull;
+                    const uint32_t e = __builtin_amdgcn_readlane(ciLane, k);
+                    if ((lm >> k) & 1ull)
+                    {
+                        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend | (e << 16);
+                        pend = e;
+                        stored++;
+                    }
+                }
+#else
                 // append two hits per iteration (one u16-pair word per iteration), 32-bit halves
 #pragma unroll
                 for (int half = 0; half < 2; ++half)
                 {
                     uint32_t       hb  = half ? (uint32_t)(lm >> 32) : (uint32_t)lm;
-                    const uint32_t hb0 = b0 + 32u * half;
+                    const uint32_t hb0 = 32u * half;
                     while (hb)
                     {
-                        const uint32_t e1 = hb0 + __builtin_ctz(hb);
+                        const uint32_t e1 = sci[hb0 + __builtin_ctz(hb)];
                         hb &= hb - 1u;
                         const bool     two = hb != 0u;
-                        const uint32_t e2  = hb0 + (two ? __builtin_ctz(hb) : 0u);
+                        const uint32_t e2  = two ? sci[hb0 + __builtin_ctz(hb)] : 0u;
                         if (two) hb &= hb - 1u;
                         uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
                         if (stored & 1u)
@@ -552,6 +490,7 @@ findNeighborsKernel(NsArgs a)
                         stored += two ? 2u : 1u;
                     }
                 }
+#endif
             }
             else
             {
@@ -559,16 +498,117 @@ findNeighborsKernel(NsArgs a)
                 {
                     const int k = __builtin_ctzll(lm);
                     lm &= lm - 1ull;
-                    gl[(size_t)stored * kWave] = s0 + k;
+                    gl[(size_t)stored * kWave] = globalOf(sci[k]);
                     stored++;
                 }
             }
 #ifdef SX_NS_PROFILE
             prof[3] += __builtin_readcyclecounter() - tP;
 #endif
-            buf ^= 1;
-            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
-            __builtin_amdgcn_wave_barrier();
+            seq += m;
+            fill = 0;
+            __builtin_amdgcn_wave_barrier(); // every lane's slot reads precede the next staging writes
+        };
+
+        // blocks of up to 64 consecutive particles of the reachable candidate leaves, in candidate order; the next
+        // block's coordinates are loaded while the current one is culled, staged and (when the chunk fills) tested.
+        // Reachable non-empty leaves are found 64 at a time: lane l of the window holds leaf wb + l, a ballot gives
+        // the window's reachable set (wave-uniform scalar iteration).  (Packing several small leaves into one block
+        // measured 2.2x slower: the segment selection costs registers and spills in this loop.)
+        const uint32_t wbit = 1u << wave;
+        struct Blk
+        {
+            int      cc;
+            uint32_t s, p1, base;
+        };
+        int      wb  = -kWave;
+        uint64_t rm  = 0;
+        uint32_t wp0 = 0, wcnt = 0, wco = 0;
+        auto     advance = [&](Blk& q) {
+            if (q.cc >= 0 && q.cc < numCand && q.s + kWave < q.p1)
+            {
+                q.s += kWave;
+                return;
+            }
+            while (rm == 0)
+            {
+                wb += kWave;
+                if (wb >= numCand)
+                {
+                    q.cc = numCand;
+                    return;
+                }
+                const int l = wb + lane;
+                wp0 = 0, wcnt = 0, wco = 0;
+                bool r = false;
+                if (l < numCand)
+                {
+                    wp0  = s_p0[l];
+                    wco  = s_cOff[l];
+                    wcnt = s_cOff[l + 1] - wco;
+                    r    = (s_reach[l] & wbit) && wcnt > 0;
+                }
+                rm = __ballot(r);
+            }
+            const int k = __builtin_ctzll(rm);
+            rm &= rm - 1ull;
+            q.cc   = wb + k;
+            q.s    = __builtin_amdgcn_readlane(wp0, k);
+            q.p1   = q.s + __builtin_amdgcn_readlane(wcnt, k);
+            q.base = __builtin_amdgcn_readlane(wco, k) - q.s;
+        };
+        auto load = [&](const Blk& q, double& X, double& Y, double& Z) {
+            if (q.cc < numCand && q.s + lane < q.p1)
+            {
+                const uint32_t j = q.s + lane;
+                X = a.x[j], Y = a.y[j], Z = a.z[j];
+            }
+        };
+        Blk cur{-1, 0, 0, 0};
+        advance(cur);
+        double cx = 0, cy = 0, cz = 0;
+#ifndef SX_NS_NOPF
+        load(cur, cx, cy, cz);
+#endif
+        while (cur.cc < numCand)
+        {
+            Blk nxt = cur;
+            advance(nxt);
+            double nx = 0, ny = 0, nz = 0;
+#ifdef SX_NS_NOPF
+            load(cur, cx, cy, cz);
+#else
+            load(nxt, nx, ny, nz);
+#endif
+            const uint32_t j  = cur.s + lane;
+            const bool     in = j < cur.p1;
+            float          px = 0, py = 0, pz = 0;
+            bool           pass = in;
+            if (in && fastWave)
+            {
+                px = (float)foldPbc(cx - ox, a.box, 0);
+                py = (float)foldPbc(cy - oy, a.box, 1);
+                pz = (float)foldPbc(cz - oz, a.box, 2);
+                const float dx = fmaxf(fabsf(px - bcx) - bsx, 0.0f), dy = fmaxf(fabsf(py - bcy) - bsy, 0.0f),
+                            dz = fmaxf(fabsf(pz - bcz) - bsz, 0.0f);
+                pass = fmaf(dx, dx, fmaf(dy, dy, dz * dz)) <= cullR2;
+            }
+            const uint64_t bm = __ballot(pass);
+            const int      n  = __popcll(bm);
+            if (fill + n > kWave) testChunk();
+            if (pass)
+            {
+                const int slot = fill + __popcll(bm & ltMask);
+                float*    P    = srec + (slot >> 1) * 8 + (slot & 1);
+                P[0] = px, P[2] = py, P[4] = pz, P[6] = fmaf(px, px, fmaf(py, py, pz * pz));
+                sci[slot] = cur.base + j;
+            }
+            // this lane's own particle in the block (it always passes: it lies in the wave box)
+            if (valid && i >= cur.s && i < cur.p1)
+                selfSeq = seq + (uint32_t)(fill + __popcll(bm & ((1ull << (i - cur.s)) - 1ull)));
+            fill += n;
+            if (fill == kWave || (nxt.cc >= numCand && fill > 0)) testChunk();
+            cur = nxt, cx = nx, cy = ny, cz = nz;
         }
         if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
@@ -718,6 +758,8 @@ findNeighborsKernel(NsArgs a)
         atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 6), tested);
         if (wave == 0 && local) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 8), (unsigned long long)ucnt);
     }
+    __syncthreads(); // LDS is reused by the next cluster of a persistent launch
+    }
 }
 
 //! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]
@@ -754,51 +796,54 @@ __global__ void importKernel(uint32_t* nidx, uint32_t first, uint32_t last, uint
         nidx[((size_t)g * ngmax + k) * kWave + lane] = in[(size_t)ni * ngmax + k];
 }
 
-//! this build's search over [first, last); frames: also (re)compute the float prefilter records
-hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, bool frames)
+//! this build's search over [first, last); grid 0: one workgroup per cluster, else a persistent grid of that size
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, unsigned grid)
 {
     if (a.numGroups == 0) return hipSuccess;
-    unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    if (frames && a.qrel && a.numLeaves > 0)
-        leafFrameKernel<<<(a.numLeaves + 3) / 4, 256, 0, s>>>(a.layout, a.numLeaves, a.x, a.y, a.z, a.qrel);
-    findNeighborsKernel<<<clusters, kCluster, 0, s>>>(a);
+    const unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    findNeighborsKernel<<<grid ? std::min(grid, clusters) : clusters, kCluster, 0, s>>>(a);
     return hipGetLastError();
 }
 
 #ifndef SX_NS_SMALL
 namespace small
 {
-hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, bool frames);
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, unsigned grid);
+}
+
+//! after the compact build: if it overflowed (stats bits 2 / 4), restore the saved h of its range
+__global__ void fallbackRestoreKernel(float* h, const float* hSave, uint32_t n, const uint32_t* stats)
+{
+    if (!(stats[0] & 6u)) return;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+        h[k] = hSave[k];
+}
+
+//! ... and reset the statistics, raising the gate word [10] of the large-build launch; [11] = compact ran first
+__global__ void fallbackGateKernel(uint32_t* stats)
+{
+    const bool redo = (stats[0] & 6u) != 0u;
+    __syncthreads();
+    if (threadIdx.x < kStatsWords)
+        stats[threadIdx.x] = threadIdx.x == 10 ? (redo ? 1u : 0u) : threadIdx.x == 11 ? 1u : (redo ? 0u : stats[threadIdx.x]);
 }
 
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
-    if (!a.hSave || !a.flagHost) return findNeighborsOnce(a, s, true);
-    // after an overflow the next searches go straight to the large build (particle distributions change slowly),
-    // then the compact one is tried again
-    if (a.largeRuns && *a.largeRuns > 0)
-    {
-        --*a.largeRuns;
-        return findNeighborsOnce(a, s, true);
-    }
-    // the compact build spills registers in the hit-append loop: with many neighbors per target (the previous
-    // search's mean, still in flagHost[4..5]) the large build is faster (Noh, ~120: 19 vs 25 ms; Sedov, ~92:
-    // 6.7 vs 5.6 ms).  Both builds give identical results.
-    const uint64_t prevSum = *reinterpret_cast<const uint64_t*>(a.flagHost + 4);
-    if (prevSum > 105ull * (a.last - a.first)) return findNeighborsOnce(a, s, true);
-    const size_t bytes = (size_t)(a.last - a.first) * sizeof(float);
-    hipError_t   e;
-    if ((e = hipMemcpyAsync(a.hSave, a.h + a.first, bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-    if ((e = small::findNeighborsOnce(a, s, true)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(a.flagHost, a.stats, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    if (!(a.flagHost[0] & 6u)) return hipSuccess; // bits 2 / 4: candidate leaves or candidate space exceeded
-    if (a.largeRuns) *a.largeRuns = 64;
-    // redo the whole range with the large build from the saved h (the h-nc iteration mutates h in place)
-    if ((e = hipMemcpyAsync(a.h + a.first, a.hSave, bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.stats, 0, kStatsWords * 4, s)) != hipSuccess) return e;
-    return findNeighborsOnce(a, s, false);
+    if (!a.hSave || !a.policy || a.policy->useLarge()) return findNeighborsOnce(a, s, 0);
+    const uint32_t n = a.last - a.first;
+    hipError_t     e;
+    if (a.iterateH &&
+        (e = hipMemcpyAsync(a.hSave, a.h + a.first, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s)))
+        return e;
+    if ((e = small::findNeighborsOnce(a, s, 0))) return e;
+    if (a.iterateH)
+        fallbackRestoreKernel<<<std::min(2048u, (n + 255) / 256), 256, 0, s>>>(a.h + a.first, a.hSave, n, a.stats);
+    fallbackGateKernel<<<1, 64, 0, s>>>(a.stats);
+    NsArgs b = a;
+    b.gate   = a.stats + 10;
+    return findNeighborsOnce(b, s, 2048);
 }
 #endif
 

@@ -479,7 +479,7 @@ __global__ void unpackGPartKernel(const GPart* in, size_t n, double* x, double* 
 struct sx_sim
 {
     sx_ctx*        ctx;
-    int            nsLargeRuns{0}; // neighbor search: steps left on the large build after a compact-build overflow
+    NsPolicy       nsPolicy;       // neighbor search: compact or large build (sx_tree.hpp)
     sx::Transport* comm{nullptr};
     sx_params      p;
     sx_box         box;
@@ -631,6 +631,7 @@ void allocFields(sx_sim* s, size_t cap)
     s->nb.reserve(a, 0, (uint32_t)cap, s->p.ngmax, true);
     s->stats      = a.get<uint32_t>("stats", kStatsWords);
     s->statsHost  = a.pinned<uint32_t>("statsHost", kStatsWords);
+    if (s->statsHost) std::fill(s->statsHost, s->statsHost + kStatsWords, 0u);
     s->sc         = a.get<Scalars>("scalars", 1);
     s->scHost     = a.pinned<Scalars>("scalarsHost", 1);
 }
@@ -1422,12 +1423,10 @@ extern "C"
             na.margin         = quantMargin(s->dbox);
             na.stats          = s->stats;
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
-            na.numLeaves      = s->tree.numLeaves;
-            na.qrel           = s->mem.get<float>("ns.qrel", qrelFloats(s->n));
+            na.prefilter      = 1;
             na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(1, s->last - s->first));
-            na.flagHost       = s->statsHost;
-            na.largeRuns      = &s->nsLargeRuns;
-            if (!na.qrel || !na.hSave) return SX_ERR_NOMEM;
+            na.policy         = &s->nsPolicy;
+            if (!na.hSave) return SX_ERR_NOMEM;
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));
@@ -1636,6 +1635,8 @@ extern "C"
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
+        s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
+        s->lastStats.build         = s->nsPolicy.lastBuild;
 #ifdef SX_NS_PROFILE
         {
             const uint64_t* pr = reinterpret_cast<const uint64_t*>(s->statsHost + 12);

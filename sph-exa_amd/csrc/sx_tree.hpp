@@ -148,7 +148,39 @@ struct NbLists
 };
 
 constexpr int kStatsWords = 26; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
-                                //!< neighbors, [6] candidates tested, [8] union entries, [12..23] profile build
+                                //!< neighbors, [6] candidates tested, [8] union entries, [10] compact-build
+                                //!< overflow redone by the large build, [11] the compact build ran first,
+                                //!< [12..23] profile build
+
+//! which search build runs: the compact one (four workgroups per CU) with a device-side fallback to the large one,
+//! or the large one directly.  Host state of one caller (context or sim), fed with the stats of each finished
+//! search through observe() -- never with stale or foreign data (statsHost is zeroed when allocated).
+struct NsPolicy
+{
+    int      largeRuns{0};   //!< searches left that go straight to the large build (after a compact overflow)
+    uint64_t prevStored{0};  //!< stored neighbors of the previous search
+    uint32_t prevTargets{0}; //!< its target count
+    uint32_t lastBuild{0};   //!< 0 compact, 1 large, 2 compact overflowed and redone by the large build
+
+    void observe(const uint32_t* statsHost, uint32_t targets)
+    {
+        lastBuild = statsHost[10] ? 2u : (statsHost[11] ? 0u : 1u);
+        if (statsHost[10]) largeRuns = 64;
+        prevStored  = *reinterpret_cast<const uint64_t*>(statsHost + 4);
+        prevTargets = targets;
+    }
+    //! the compact build spills registers in the hit-append loop: with many neighbors per target (> 105 on
+    //! average in the previous search) the large build is faster
+    bool useLarge()
+    {
+        if (largeRuns > 0)
+        {
+            --largeRuns;
+            return true;
+        }
+        return prevTargets && prevStored > 105ull * prevTargets;
+    }
+};
 
 //! neighbor-search arguments (sx_neighbors.hip)
 struct NsArgs
@@ -176,17 +208,15 @@ struct NsArgs
     DevBox          box;
     double          margin; // node-box inflation covering key quantisation round-off
     const float*    powTab; // glibc powf(1 + 1023*ng0/nc, 0.1f) by nc (updateH)
-    // float prefilter records (leafFrameKernel, pair layout, qrelFloats(n) floats, written by findNeighbors); nullptr
-    // selects the exact double test for every candidate
-    int             numLeaves;
-    float*          qrel;
-    uint32_t*       stats;  // kStatsWords words, see above
-    // optional (both non-null): the search first runs the compact variant (four workgroups per CU) and, if one of its
-    // capacities was exceeded, restores h from hSave (last - first floats) and redoes the range with the large one;
-    // flagHost: one pinned word
+    int             prefilter; // 1: packed f32 distance test in the cluster frame, exact double test only for the
+                               // ambiguous chunks; 0: the exact double test for every candidate
+    uint32_t*       stats;     // kStatsWords words, see above
+    // optional (both non-null): the compact build runs first (policy permitting) with h saved to hSave
+    // (last - first floats); if one of its capacities was exceeded, kernels on the stream restore h and redo the
+    // range with the large build -- no host synchronisation
     float*          hSave;
-    uint32_t*       flagHost;
-    int*            largeRuns; // host counter owned by the caller: searches left that go straight to the large build
+    NsPolicy*       policy;
+    const uint32_t* gate; // set by findNeighbors for the fallback launch: the kernel runs only if *gate != 0
 
     void setLists(const NbLists& L)
     {
@@ -229,8 +259,6 @@ void       packC(size_t n, const float* c11, const float* c12, const float* c13,
 void       packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s);
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
-//! floats of the prefilter record buffer for n particles (pairs of 8 floats + one padded chunk)
-inline size_t qrelFloats(size_t n) { return ((n + 1) / 2 + 64) * 8; }
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
 //! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);
