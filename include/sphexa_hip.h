@@ -211,6 +211,11 @@ int sx_leaf_layout(sx_ctx* ctx, const uint32_t* counts, int32_t numLeaves, uint3
 int sx_compute_groups(sx_ctx* ctx, uint32_t first, uint32_t last, sx_groups* groups);
 /*! neighbor search for targets [first,last) into the context's list; iterate_h != 0 runs the h-nc iteration
  *  (mutates h). nc has length fields->n (written at [first,last)). stats may be NULL. */
+/*! which neighbor-search build sx_find_neighbors runs: 0 automatic (the compact build, four workgroups per CU,
+ *  with a device-side fallback to the large build on a capacity overflow; the large one after an overflow or at
+ *  > 105 neighbors per target), 1 large only, 2 compact first, 3 compact with a forced overflow of every cluster
+ *  (test hook for the fallback).  All give identical h, nc and neighbor lists. */
+int sx_set_search_mode(sx_ctx* ctx, int mode);
 int sx_find_neighbors(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, const sx_box* box,
                       const sx_params* p, uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats);
 /*! copy the cached list out / in, CPU layout neighbors[(i-first)*ngmax + k] (device pointers); export zero-fills

@@ -264,6 +264,7 @@ def _bind(lib):
         ("update_h", C.c_float, [C.c_uint, C.c_uint, C.c_float]),
         ("gravity", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint, C.c_uint,
                                  C.c_uint, P, P, C.c_int]),
+        ("set_scales", None, [P, P, P, P, P]),
     ]:
         for prefix in ("ref_", "ox_"):
             if hasattr(lib, prefix + name):
@@ -289,6 +290,19 @@ class Lib:
 
     def params(self, av_clean=False, g=0.0, theta=0.5, std=False):
         return default_params(self.K, av_clean, g, theta, std)
+
+    SCALES = ("du", "a", "dv", "gradh", "alpha")
+
+    def scales_on(self, n):
+        """make the oracle's J-loops export per-particle error scales (sums of |term|, ox_set_scales) into fresh
+        float64 arrays of length n, indexed like the state the kernels run on; returns the dict of arrays"""
+        self._scales = {k: np.zeros(n, np.float64) for k in self.SCALES}
+        self.lib.set_scales(*[self._scales[k].ctypes.data for k in self.SCALES])
+        return self._scales
+
+    def scales_off(self):
+        self.lib.set_scales(None, None, None, None, None)
+        self._scales = None
 
     def sfc_keys(self, st, box):
         self.lib.sfc_keys(st.x.ctypes.data, st.y.ctypes.data, st.z.ctypes.data, st.n, C.byref(box),

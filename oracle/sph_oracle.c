@@ -688,6 +688,17 @@ static inline unsigned nc_capped(const uint32_t* nc, size_t i, unsigned ngmax)
     return v < ngmax ? v : ngmax;
 }
 
+/* Error scales of the neighbor sums (tests only): when registered by ox_set_scales, the J-loops also accumulate,
+ * per particle, the magnitude of the terms their float sums are made of -- the scale of the rounding error of a
+ * float sum in any order (SURVEY.md 8(c) tier 1).  a: L1 over the three components; dv: divv, curlv and dV;
+ * gradh and alpha: the sums propagated through the closing formula. */
+static double *g_sc_du, *g_sc_a, *g_sc_dv, *g_sc_gradh, *g_sc_alpha;
+
+void ox_set_scales(double* du, double* a, double* dv, double* gradh, double* alpha)
+{
+    g_sc_du = du, g_sc_a = a, g_sc_dv = dv, g_sc_gradh = gradh, g_sc_alpha = alpha;
+}
+
 /* xmassJLoop (xmass_kern.hpp:50-79) */
 static float xmassJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, const ox_state* s)
 {
@@ -731,6 +742,7 @@ static void veDefGradhJLoop(uint32_t i, double K, const ox_box* b, const uint32_
     float  kxi      = xmassi;
     float  whomegai = -3.0f * xmassi;
     float  wrho0i   = -3.0f * mi;
+    double sOm = 3.0 * fabs((double)xmassi), sRh = 3.0 * fabs((double)mi);
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
         uint32_t j      = nb[pj];
@@ -743,6 +755,11 @@ static void veDefGradhJLoop(uint32_t i, double K, const ox_box* b, const uint32_
         kxi += w * xmassj;
         whomegai += dterh * xmassj;
         wrho0i += dterh * s->m[j];
+        if (g_sc_gradh)
+        {
+            sOm += fabs((double)dterh * xmassj);
+            sRh += fabs((double)dterh * s->m[j]);
+        }
     }
     kxi      = (float)((double)kxi * (K * (double)h3Inv));
     whomegai = (float)((double)whomegai * (K * (double)h3Inv * (double)hInv));
@@ -753,6 +770,13 @@ static void veDefGradhJLoop(uint32_t i, double K, const ox_box* b, const uint32_
     float dhdrho = -hi / (rhoi * 3.0f);
     *kxo         = kxi;
     *gradho      = 1.0f - dhdrho * whomegai;
+    if (g_sc_gradh)
+    {
+        const double k4 = K * (double)h3Inv * (double)hInv;
+        g_sc_gradh[i]   = 1.0 + fabs((double)dhdrho) * k4 *
+                                  (fabs((double)mi / xmassi) * sOm +
+                                   (fabs((double)kxi) + K * fabs((double)xmassi) * (double)h3Inv) * sRh);
+    }
 }
 
 void ox_ve_def_gradh(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
@@ -851,6 +875,7 @@ static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t
     float  dVx[3] = {0, 0, 0}, dVy[3] = {0, 0, 0}, dVz[3] = {0, 0, 0};
     float  c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i],
           c33i = s->c33[i];
+    double sdv = 0.0;
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
         uint32_t j  = nb[pj];
@@ -877,8 +902,12 @@ static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t
             dVy[k] = dVy[k] + tA[k] * fy;
             dVz[k] = dVz[k] + tA[k] * fz;
         }
+        if (g_sc_dv)
+            sdv += (fabs((double)tA[0]) + fabs((double)tA[1]) + fabs((double)tA[2])) *
+                   (fabs((double)fx) + fabs((double)fy) + fabs((double)fz));
     }
     float norm_kxi = (float)(K * (double)hiInv3 / (double)kxi);
+    if (g_sc_dv) g_sc_dv[i] = fabs((double)norm_kxi) * sdv;
     s->divv[i]     = norm_kxi * (dVx[0] + dVy[1] + dVz[2]);
     if (s->curlv)
     {
@@ -925,6 +954,7 @@ static float AVswitchesJLoop(uint32_t i, double K, const ox_box* b, const uint32
     float hiInv3      = hiInv * hiInv * hiInv;
     float divv_i      = s->divv[i];
     float gx = 0, gy = 0, gz = 0;
+    double sg = 0.0;
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
         uint32_t j  = nb[pj];
@@ -951,8 +981,14 @@ static float AVswitchesJLoop(uint32_t i, double K, const ox_box* b, const uint32
         gx += factor * termA1;
         gy += factor * termA2;
         gz += factor * termA3;
+        if (g_sc_alpha)
+            sg += fabs((double)factor) * (fabs((double)termA1) + fabs((double)termA2) + fabs((double)termA3));
     }
     float graddivv = sqrtf(gx * gx + gy * gy + gz * gz);
+    /* d alphaloc / d graddivv <= alphamax h^2 / (h^2 graddivv + h |divv| + 0.05 c) */
+    if (g_sc_alpha)
+        g_sc_alpha[i] = (double)alphamax * (double)hi * hi * sg /
+                        ((double)hi * hi * graddivv + (double)hi * fabs((double)divv_i) + 0.05 * ci);
     float alphaloc = 0.0f;
     if (divv_i < 0.0f)
     {
@@ -1038,6 +1074,7 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
     }
     /* T(32) * M_PI / T(3) / T(neighborsCount + 1) is formed in double, cbrt in double, stored as float */
     float eta_crit = (float)cbrt((double)32.0f * M_PI / (double)3.0f / (double)(float)(cnt + 1));
+    double sE = 0.0, sV = 0.0, sA = 0.0;
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
         uint32_t j   = nb[pj];
@@ -1118,6 +1155,20 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
         mx += momentum_i * tA1i + momentum_j * tA1j + a_visc_x;
         my += momentum_i * tA2i + momentum_j * tA2j + a_visc_y;
         mz += momentum_i * tA3i + momentum_j * tA3j + a_visc_z;
+        if (g_sc_du)
+        {
+            sE += fabs((double)mj * a_mom) *
+                  (fabs((double)vx_ij * tA1i) + fabs((double)vy_ij * tA2i) + fabs((double)vz_ij * tA3i));
+            sV += fabs((double)a_visc_x * vx_ij) + fabs((double)a_visc_y * vy_ij) + fabs((double)a_visc_z * vz_ij);
+            sA += fabs((double)momentum_i) * (fabs((double)tA1i) + fabs((double)tA2i) + fabs((double)tA3i)) +
+                  fabs((double)momentum_j) * (fabs((double)tA1j) + fabs((double)tA2j) + fabs((double)tA3j)) +
+                  fabs((double)a_visc_x) + fabs((double)a_visc_y) + fabs((double)a_visc_z);
+        }
+    }
+    if (g_sc_du)
+    {
+        g_sc_du[i] = K * (fabs((double)prhoi) * sE + 0.5 * sV);
+        if (g_sc_a) g_sc_a[i] = K * sA;
     }
     if (a_visc_energy < 0.0f) a_visc_energy = 0.0f; /* stl::max(T(0), x) */
     float eCoeff = prhoi;
@@ -1211,6 +1262,7 @@ static void momentumStdJLoop(uint32_t i, double K, const ox_box* b, const uint32
     float       hiInv3 = hiInv * hiInv * hiInv;
     float       maxvsignali = 0.0f;
     float       momentum_x = 0, momentum_y = 0, momentum_z = 0, energy = 0;
+    double      sA = 0.0, sE = 0.0;
     float c11i = s->c11[i], c12i = s->c12[i], c13i = s->c13[i], c22i = s->c22[i], c23i = s->c23[i], c33i = s->c33[i];
     for (unsigned pj = 0; pj < cnt; ++pj)
     {
@@ -1264,6 +1316,19 @@ static void momentumStdJLoop(uint32_t i, double K, const ox_box* b, const uint32
         float ae = Wi * (2.0f * mj_pro_i + viscosity_ij * mi_roi);
         float be = viscosity_ij * mj_roj_Wj;
         energy += vx_ij * (ae * tA1i + be * tA1j) + vy_ij * (ae * tA2i + be * tA2j) + vz_ij * (ae * tA3i + be * tA3j);
+        if (g_sc_du)
+        {
+            const double ta = fabs((double)tA1i) + fabs((double)tA2i) + fabs((double)tA3i),
+                         tb = fabs((double)tA1j) + fabs((double)tA2j) + fabs((double)tA3j),
+                         vv = fabs((double)vx_ij) + fabs((double)vy_ij) + fabs((double)vz_ij);
+            sA += fabs((double)am) * ta + fabs((double)bm) * tb;
+            sE += vv * (fabs((double)ae) * ta + fabs((double)be) * tb);
+        }
+    }
+    if (g_sc_du)
+    {
+        g_sc_du[i] = K * 0.5 * sE;
+        if (g_sc_a) g_sc_a[i] = K * sA;
     }
     s->du[i]    = -K * 0.5 * (double)energy;
     s->ax[i]    = (float)(K * (double)momentum_x);
@@ -1529,6 +1594,9 @@ static inline void grav_m2p(double* acc, double tx, double ty, double tz, const 
     acc[1] += r_minus5 * Qrx + rQrAndMonopole * r0;
     acc[2] += r_minus5 * Qry + rQrAndMonopole * r1;
     acc[3] += r_minus5 * Qrz + rQrAndMonopole * r2;
+    /* magnitude of the terms (error scale, ox_set_scales) */
+    acc[4] += fabs(r_minus5) * (fabs(Qrx) + fabs(Qry) + fabs(Qrz)) +
+              fabs(rQrAndMonopole) * (fabs(r0) + fabs(r1) + fabs(r2));
 }
 
 /* P2P<double, double, float, float> (kernel.hpp:514-535), softened by h_i + h_j */
@@ -1547,6 +1615,7 @@ static inline void grav_p2p(double* acc, double xi, double yi, double zi, double
     acc[1] += dx * invR3m;
     acc[2] += dy * invR3m;
     acc[3] += dz * invR3m;
+    acc[4] += fabs(invR3m) * (fabs(dx) + fabs(dy) + fabs(dz));
 }
 
 #define GRAV_GROUP 16
@@ -1563,11 +1632,11 @@ static double grav_traverse(ox_state* s, const ox_tree* t, const double* centers
     for (uint32_t i0 = first; i0 < last; i0 += GRAV_GROUP)
     {
         uint32_t nt = last - i0 < GRAV_GROUP ? last - i0 : GRAV_GROUP;
-        double   acc[GRAV_GROUP][4];
+        double   acc[GRAV_GROUP][5];
         double   lo[3], hi[3];
         for (uint32_t k = 0; k < nt; ++k)
         {
-            acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0;
+            acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = acc[k][4] = 0.0;
             double p[3] = {s->x[i0 + k], s->y[i0 + k], s->z[i0 + k]};
             for (int d = 0; d < 3; ++d)
             {
@@ -1643,6 +1712,7 @@ static double grav_traverse(ox_state* s, const ox_tree* t, const double* centers
             s->ax[i0 + k] = (float)((double)s->ax[i0 + k] + (double)G * acc[k][1]);
             s->ay[i0 + k] = (float)((double)s->ay[i0 + k] + (double)G * acc[k][2]);
             s->az[i0 + k] = (float)((double)s->az[i0 + k] + (double)G * acc[k][3]);
+            if (g_sc_a) g_sc_a[i0 + k] += fabs((double)G) * acc[k][4];
         }
     }
     return 0.5 * egrav;

@@ -361,6 +361,14 @@ extern "C"
         return SX_OK;
     }
 
+    int sx_set_search_mode(sx_ctx* c, int mode)
+    {
+        if (mode < 0 || mode > 3) return fail(c, SX_ERR_ARG, "sx_set_search_mode: mode must be 0..3");
+        c->nsPolicy.mode      = mode;
+        c->nsPolicy.largeRuns = 0;
+        return SX_OK;
+    }
+
     int sx_find_neighbors(sx_ctx* c, const sx_fields* f, const sx_tree* tree, const sx_box* box, const sx_params* p,
                           uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats)
     {

@@ -238,6 +238,16 @@ __device__ __forceinline__ void pbcRule(const Clu& cu, const DevBox& b, float r,
 }
 
 // ---- XMass: xmassJLoop (hydro_ve/xmass_kern.hpp:50-79) ----------------------------------------------------------
+/*! |(a, b, c)| scaled by the largest component: this file flushes denormals to zero, so the plain sum of squares
+ *  would lose components below ~1e-19 (tiny velocity gradients) that the reference keeps */
+__device__ __forceinline__ float norm3(float a, float b, float c)
+{
+    const float m = fmaxf(fabsf(a), fmaxf(fabsf(b), fabsf(c)));
+    if (m == 0.0f) return 0.0f;
+    const float r = 1.0f / m, x = a * r, y = b * r, z = c * r;
+    return m * sqrtf(x * x + (y * y + z * z));
+}
+
 template<int CH, int SPLIT>
 __global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)
 {
@@ -431,7 +441,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
-            a.curlv[i]      = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
+            a.curlv[i]      = norm_kxi * norm3(cv0, cv1, cv2);
         }
         if (a.dV11) // doGradV (divv_curlv_kern.hpp:113-121)
         {
@@ -533,7 +543,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
-            a.curlv[i]      = norm_kxi * sqrtf(cv0 * cv0 + (cv1 * cv1 + cv2 * cv2));
+            a.curlv[i]      = norm_kxi * norm3(cv0, cv1, cv2);
         }
         if (a.dV11)
         {
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         gx = v[0], gy = v[1], gz = v[2], vijsignal_i = v[3];
     }
     if (!cu.valid || cu.part != 0) return;
-    const float graddivv = sqrtf(gx * gx + gy * gy + gz * gz);
+    const float graddivv = norm3(gx, gy, gz);
     float       alphaloc = 0.0f;
     if (divv_i < 0.0f)
     {

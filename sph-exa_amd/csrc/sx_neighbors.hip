@@ -237,7 +237,10 @@ findNeighborsKernel(NsArgs a)
             {
                 s_cOff[nCand] = run;
                 // error bits: 2 = traversal queue / candidate-leaf list full, 4 = candidate space beyond u16
-                const unsigned f = (overflow ? 2u : 0u) | ((local && run > (uint32_t)kCandSpace) ? 4u : 0u);
+                unsigned f = (overflow ? 2u : 0u) | ((local && run > (uint32_t)kCandSpace) ? 4u : 0u);
+#ifdef SX_NS_SMALL
+                if (a.forceOverflow) f |= 4u; // test hook (sx_set_search_mode 3): exercise the device-side fallback
+#endif
                 if (f) atomicOr(&a.stats[0], 1u | f);
 #ifdef SX_NS_DEBUG
                 if (f && atomicAdd(&a.stats[3], 1u) < 8)
@@ -831,13 +834,16 @@ __global__ void fallbackGateKernel(uint32_t* stats)
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
-    if (!a.hSave || !a.policy || a.policy->useLarge()) return findNeighborsOnce(a, s, 0);
+    const int mode = a.policy ? a.policy->mode : 1;
+    if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge())) return findNeighborsOnce(a, s, 0);
     const uint32_t n = a.last - a.first;
     hipError_t     e;
     if (a.iterateH &&
         (e = hipMemcpyAsync(a.hSave, a.h + a.first, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s)))
         return e;
-    if ((e = small::findNeighborsOnce(a, s, 0))) return e;
+    NsArgs c = a;
+    c.forceOverflow = mode == 3;
+    if ((e = small::findNeighborsOnce(c, s, 0))) return e;
     if (a.iterateH)
         fallbackRestoreKernel<<<std::min(2048u, (n + 255) / 256), 256, 0, s>>>(a.h + a.first, a.hSave, n, a.stats);
     fallbackGateKernel<<<1, 64, 0, s>>>(a.stats);

@@ -157,6 +157,8 @@ constexpr int kStatsWords = 26; //!< [0] error flags, [1] failures, [2] max coun
 //! search through observe() -- never with stale or foreign data (statsHost is zeroed when allocated).
 struct NsPolicy
 {
+    int      mode{0};        //!< 0 auto, 1 large build only, 2 compact first (fallback on overflow), 3 = 2 with a
+                             //!< forced overflow of every cluster (test hook: the device-side fallback path)
     int      largeRuns{0};   //!< searches left that go straight to the large build (after a compact overflow)
     uint64_t prevStored{0};  //!< stored neighbors of the previous search
     uint32_t prevTargets{0}; //!< its target count
@@ -217,6 +219,7 @@ struct NsArgs
     float*          hSave;
     NsPolicy*       policy;
     const uint32_t* gate; // set by findNeighbors for the fallback launch: the kernel runs only if *gate != 0
+    int             forceOverflow; // compact build only: report a capacity overflow for every cluster (mode 3)
 
     void setLists(const NbLists& L)
     {

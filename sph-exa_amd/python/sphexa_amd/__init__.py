@@ -122,6 +122,7 @@ def lib():
         "sx_node_centers": (C.c_int, [vp, vp, i32, C.POINTER(SxBox), vp, vp]),
         "sx_leaf_layout": (C.c_int, [vp, vp, i32, vp]),
         "sx_compute_groups": (C.c_int, [vp, u32, u32, C.POINTER(SxGroups)]),
+        "sx_set_search_mode": (C.c_int, [vp, C.c_int]),
         "sx_find_neighbors": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.POINTER(SxBox),
                                         C.POINTER(SxParams), u32, u32, C.c_int, C.POINTER(SxNbStats)]),
         "sx_export_neighbors": (C.c_int, [vp, vp, u32, u32, u32, vp]),

@@ -14,7 +14,7 @@ import pytest
 import gpu_util as gutil
 import pyoracle as po
 import sphexa_amd as sx
-from test_gpu_parity import compare_state, fast_tolerance_scale, kernel_chain, FLOATS
+from test_gpu_parity import fast_tolerance_scale, kernel_chain, run_checked_steps, FLOATS
 
 pytestmark = pytest.mark.gpu
 
@@ -96,16 +96,6 @@ def test_avclean_changes_momentum(ctx, ora):
 
 @pytest.mark.parametrize("ic,side,steps", [("sedov", 16, 3), ("noh", 16, 2)])
 def test_avclean_full_steps(ctx, ora, ic, side, steps):
+    """per-particle checks (gpu_util.StepChecker) of whole avClean steps against the oracle"""
     st, obox = (po.sedov_state if ic == "sedov" else po.noh_state)(side)
-    box = gutil.box_to_sx(obox)
-    sim = sx.Sim(ctx, st.n, box, params=sx.default_params(av_clean=True))
-    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
-    ref = st.copy()
-    p = ora.params(av_clean=True)
-    for s in range(steps):
-        sim.step()
-        ora.step(ref, obox, params=p)
-        got = sim.get(["id", "nc", "h"] + FLOATS)
-        compare_state(got, ref, strict_discrete=(s == 0))
-        assert sim.scalars()["minDt"] == pytest.approx(ref.minDt, rel=1e-5)
-    sim.close()
+    run_checked_steps(ctx, ora, st, obox, steps, av_clean=True).close()
