@@ -10,7 +10,9 @@
  *   sx_compute_octree      cstone::computeOctreeGpu / updateOctreeGpu (converged)  tree/csarray_gpu.cu:100-264
  *   sx_build_octree        cstone::buildOctreeGpu               tree/octree_gpu.cu:153-170
  *   sx_node_centers        cstone::computeGeoCentersGpu         focus/source_center_gpu.cu:117-135
- *   sx_compute_groups      sph::computeSpatialGroups            sph/include/sph/groups.cu:30-47
+ *   sx_compute_groups      cstone::computeFixedGroups (64)      domain/include/cstone/traversal/groups.cuh:13-41
+ *   sx_spatial_groups      sph::computeSpatialGroups            sph/include/sph/groups.cu:30-47 (computeGroupSplits<64>,
+ *                                                               traversal/groups.cuh:195-310)
  *   sx_find_neighbors      cstone::findNeighbors (+ sph h-nc iteration) findneighbors.hpp:167-188,
  *                                                               sph/include/sph/find_neighbors.hpp:10-44
  *   sx_xmass               sph::cuda::computeXMass              sph/include/sph/sph_gpu.hpp:25, hydro_ve/xmass_gpu.cu:103
@@ -25,6 +27,11 @@
  *   sx_iad                 sph::computeIADGpu (std)             sph_gpu.hpp:19-20, hydro_std/iad_gpu.cu:111-124
  *   sx_momentum_energy_std sph::computeMomentumEnergyStdGpu     sph_gpu.hpp:22-23, hydro_std/momentum_energy_gpu.cu:109
  *   sx_positions           sph::computePositionsGpu             sph_gpu.hpp:64-72, positions_gpu.cu:167-179
+ *   sx_positions_rungs     sph::computePositionsGpu (rungs)     sph_gpu.hpp:64-72, positions_gpu.cu:110-179
+ *   sx_drift_positions     sph::driftPositionsGpu               sph_gpu.hpp:57-62, positions_gpu.cu:45-108
+ *   sx_group_divv_timestep sph::groupDivvTimestepGpu            sph_gpu.hpp:80, ts_groups.cu:17-46
+ *   sx_group_acc_timestep  sph::groupAccTimestepGpu             sph_gpu.hpp:83, ts_groups.cu:48-81
+ *   sx_store_rung          sph::storeRungGpu                    sph_gpu.hpp:86, ts_groups.cu:84-108
  *   sx_update_h            sph::updateSmoothingLengthGpu        sph_gpu.hpp:78, update_h_gpu.cu:49-60
  *   sx_max_divv            cstone::MinMaxGpu (rhoTimestep)      sph/ts_global.hpp:72-94
  *   sx_sim_*               one HydroVeProp step (sync + computeForces + integrate), main/src/propagator/ve_hydro.hpp:132-218
@@ -208,7 +215,15 @@ int sx_node_centers(sx_ctx* ctx, const uint64_t* prefixes, int32_t numNodes, con
 int sx_leaf_layout(sx_ctx* ctx, const uint32_t* counts, int32_t numLeaves, uint32_t* layout);
 
 /* ---- sph ------------------------------------------------------------------------------------------------- */
+/*! fixed groups of 64 SFC-consecutive targets (one wavefront each); groupStart/groupEnd = NULL (implicit) */
 int sx_compute_groups(sx_ctx* ctx, uint32_t first, uint32_t last, sx_groups* groups);
+/*! computeSpatialGroups: the fixed 64-groups split where consecutive particles are farther apart than
+ *  tolFactor * cbrt(smallest leaf volume of the group) in box-scaled coordinates (the reference passes
+ *  tolFactor = 2).  Writes groups[0..numGroups] (device array of capacity cap >= last - first + 1) and sets
+ *  out->groupStart = groups, out->groupEnd = groups + 1. */
+int sx_spatial_groups(sx_ctx* ctx, uint32_t first, uint32_t last, const double* x, const double* y, const double* z,
+                      const sx_tree* tree, const sx_box* box, float tolFactor, uint32_t* groups, uint32_t cap,
+                      sx_groups* out);
 /*! neighbor search for targets [first,last) into the context's list; iterate_h != 0 runs the h-nc iteration
  *  (mutates h). nc has length fields->n (written at [first,last)). stats may be NULL. */
 /*! which neighbor-search build sx_find_neighbors runs: 0 automatic (the compact build, four workgroups per CU,
@@ -265,6 +280,26 @@ int sx_momentum_energy_std(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, 
 int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
                  double gamma, float muiConst, const sx_box* box);
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
+
+/* ---- block time-steps (HydroVeBdtProp, main/src/propagator/ve_hydro_bdt.hpp) ------------------------------------
+ * Groups: explicit [groupStart[g], groupEnd[g]) (sx_spatial_groups, or a slice of a rung-sorted group list) or, with
+ * groupStart == NULL, fixed 64-particle blocks of [firstBody, lastBody).  dt_m1[SX_MAX_RUNGS] holds the previous
+ * time-step of each rung; rung (nullable) selects dt_m1[rung[i]], else dt_m1[0].  constCv < 0: cv from f->mui
+ * (idealGasCv per particle).  f->temp NULL: the update acts on f->u instead. */
+#define SX_MAX_RUNGS 4 /* sph::Timestep::maxNumRungs (sph/timestep.h:42) */
+/*! computePositionsGpu (sph_gpu.hpp:64-72, positions_gpu.cu:110-179): Press position update + AB2 energy */
+int sx_positions_rungs(sx_ctx* ctx, const sx_groups* g, float dt, const float* dt_m1, const uint8_t* rung,
+                       const sx_fields* f, double gamma, double constCv, const sx_box* box);
+/*! driftPositionsGpu (sph_gpu.hpp:57-62, positions_gpu.cu:45-108): back by dt_back, forward by dt, open box */
+int sx_drift_positions(sx_ctx* ctx, const sx_groups* g, float dt, float dt_back, const float* dt_m1,
+                       const uint8_t* rung, const sx_fields* f, double gamma, double constCv);
+/*! groupDivvTimestepGpu (ts_groups.cu:17-46): groupDt[g] = min(groupDt[g], Krho / |max divv over g|) */
+int sx_group_divv_timestep(sx_ctx* ctx, float Krho, const sx_groups* g, const float* divv, float* groupDt);
+/*! groupAccTimestepGpu (ts_groups.cu:48-81): groupDt[g] = min(groupDt[g], etaAcc / |a|max^(1/2)) */
+int sx_group_acc_timestep(sx_ctx* ctx, float etaAcc, const sx_groups* g, const float* ax, const float* ay,
+                          const float* az, float* groupDt);
+/*! storeRungGpu (ts_groups.cu:84-108) */
+int sx_store_rung(sx_ctx* ctx, const sx_groups* g, uint8_t rung, uint8_t* rungs);
 int sx_max_divv(sx_ctx* ctx, uint32_t first, uint32_t last, const float* divv, float* maxDivv);
 
 /* ---- observables ---------------------------------------------------------------------------------------- */

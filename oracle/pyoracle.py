@@ -265,6 +265,9 @@ def _bind(lib):
         ("gravity", C.c_double, [C.POINTER(OxState), C.POINTER(OxParams), C.POINTER(OxBox), C.c_uint, C.c_uint,
                                  C.c_uint, P, P, C.c_int]),
         ("set_scales", None, [P, P, P, P, P]),
+        ("make_splits", C.c_int, [C.c_uint64, P]),
+        ("group_splits", C.c_int, [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P, C.POINTER(OxBox), C.c_float,
+                                   P]),
     ]:
         for prefix in ("ref_", "ox_"):
             if hasattr(lib, prefix + name):
@@ -299,6 +302,24 @@ class Lib:
         self._scales = {k: np.zeros(n, np.float64) for k in self.SCALES}
         self.lib.set_scales(*[self._scales[k].ctypes.data for k in self.SCALES])
         return self._scales
+
+    def make_splits(self, mask):
+        out = np.zeros(65, np.uint32)
+        k = self.lib.make_splits(int(mask), out.ctypes.data)
+        return out[:k].tolist()
+
+    def group_splits(self, first, last, x, y, z, leaves, layout, box, tol_factor=2.0):
+        """computeGroupSplits<64> restated (sph_oracle.c ox_group_splits): group boundaries, length numGroups+1"""
+        x, y, z = (np.ascontiguousarray(a, np.float64) for a in (x, y, z))
+        leaves = np.ascontiguousarray(leaves, np.uint64)
+        layout = np.ascontiguousarray(layout, np.uint32)
+        nl = leaves.size - 1
+        ng = self.lib.group_splits(first, last, x.ctypes.data, y.ctypes.data, z.ctypes.data, leaves.ctypes.data, nl,
+                                   layout.ctypes.data, C.byref(box), tol_factor, None)
+        out = np.zeros(ng + 1, np.uint32)
+        self.lib.group_splits(first, last, x.ctypes.data, y.ctypes.data, z.ctypes.data, leaves.ctypes.data, nl,
+                              layout.ctypes.data, C.byref(box), tol_factor, out.ctypes.data)
+        return out
 
     def scales_off(self):
         self.lib.set_scales(None, None, None, None, None)

@@ -414,6 +414,106 @@ void ox_build_octree(const uint64_t* leaves, int numLeaves, uint64_t* prefixes, 
 
 /* nodeFpCenters (focus/source_center.hpp:146-157) with hilbertIBox (hilbert.hpp:274-290) and
  * centerAndSize (sfc/box.hpp:333-348) */
+/* ------------------------------------------------------------------------------------------------
+ * Target groups: computeGroupSplits<64> (cstone/traversal/groups.cuh:195-310; caller sph/groups.cu:30-47 with
+ * tolFactor 2).  Restated for the 64-wide wavefront of the AMD build (GpuConfig::warpSize = 64, so one fixed group
+ * of 64 particles = one warp and one 64-bit split mask, nwt = 1).
+ * ------------------------------------------------------------------------------------------------ */
+
+/* findSplits (groups.cuh:55-93) for one fixed group: bit l set when |X[l+1] - X[l]|^2 > distCritSq, X in
+ * box-scaled coordinates (x * ilx, no origin shift), lane 63 and clamped lanes compare with themselves */
+static uint64_t find_splits(const double* X, const double* Y, const double* Z, double distCritSq)
+{
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l)
+    {
+        int    n  = l < 63 ? l + 1 : l;
+        double dx = X[n] - X[l], dy = Y[n] - Y[l], dz = Z[n] - Z[l];
+        double d2 = dx * dx + (dy * dy + dz * dz); /* norm2 = right fold dot (util/array.hpp:253) */
+        if (d2 > distCritSq) m |= 1ull << l;
+    }
+    return m;
+}
+
+/* makeSplits (groups.cuh:116-150): lengths of the runs of the split mask, the last one extended to 64 */
+int ox_make_splits(uint64_t mask, uint32_t* lengths)
+{
+    int k = 0, remaining = 64;
+    while (mask)
+    {
+        int length = __builtin_ctzll(mask) + 1;
+        remaining -= length;
+        lengths[k++] = (uint32_t)length;
+        mask = length < 64 ? mask >> length : 0;
+    }
+    lengths[k++] = (uint32_t)remaining;
+    return k;
+}
+
+/* groupSplitsKernel (groups.cuh:180-250) per fixed group g; returns the split mask */
+uint64_t ox_group_split_mask(uint32_t first, uint32_t last, uint32_t g, const double* x, const double* y,
+                             const double* z, const uint64_t* leaves, int numLeaves, const uint32_t* layout,
+                             const ox_box* b, float tolFactor)
+{
+    double X[64], Y[64], Z[64];
+    float  nodeVolume = 1.0f;
+    for (int l = 0; l < 64; ++l)
+    {
+        uint32_t body = first + g * 64 + l;
+        if (body > last - 1) body = last - 1;
+        /* leafIdx = upper_bound(layout, layout + numLeaves, body) - layout - 1 */
+        int lo = 0, hi = numLeaves;
+        while (lo < hi)
+        {
+            int mid = (lo + hi) / 2;
+            if (layout[mid] <= body) lo = mid + 1;
+            else hi = mid;
+        }
+        int leaf = lo - 1;
+        /* centerAndSize<KeyType>(sfcIBox(leaf range), unit box) in float: half-size of a cube of
+         * (range)^(1/3) integer units, 2^-21 per unit; vol = 8 * sx * sy * sz (all powers of two) */
+        uint64_t range = leaves[leaf + 1] - leaves[leaf];
+        unsigned level = treeLevel(range);
+        float    uL    = 1.0f / (float)(1u << MAXLEVEL);
+        float    half  = 0.5f * uL * 1.0f;
+        float    side  = (float)(1u << (MAXLEVEL - level));
+        float    sz    = side * half;
+        float    vol   = 8.0f * sz * sz * sz;
+        nodeVolume     = vol < nodeVolume ? vol : nodeVolume;
+        X[l] = x[body] * box_il(b, 0);
+        Y[l] = y[body] * box_il(b, 1);
+        Z[l] = z[body] * box_il(b, 2);
+    }
+    double distCrit = (double)(cbrtf(nodeVolume) * tolFactor);
+    return find_splits(X, Y, Z, distCrit * distCrit);
+}
+
+/* computeGroupSplits<64> (groups.cuh:255-310): group boundaries groups[0..numGroups] (groups[numGroups] = last);
+ * returns numGroups; groups == NULL: size query */
+int ox_group_splits(uint32_t first, uint32_t last, const double* x, const double* y, const double* z,
+                    const uint64_t* leaves, int numLeaves, const uint32_t* layout, const ox_box* b, float tolFactor,
+                    uint32_t* groups)
+{
+    if (last <= first) return 0;
+    uint32_t numFixed = (last - first + 63) / 64;
+    uint32_t pos = first;
+    int      ng  = 0;
+    for (uint32_t g = 0; g < numFixed; ++g)
+    {
+        uint64_t m = ox_group_split_mask(first, last, g, x, y, z, leaves, numLeaves, layout, b, tolFactor);
+        uint32_t len[65];
+        int      k = ox_make_splits(m, len);
+        for (int q = 0; q < k; ++q)
+        {
+            if (groups) groups[ng] = pos;
+            pos += len[q];
+            ng++;
+        }
+    }
+    if (groups) groups[ng] = last;
+    return ng;
+}
+
 void ox_node_centers(const uint64_t* prefixes, int numNodes, const ox_box* b, double* centers, double* sizes)
 {
     const int    maxCoord = 1 << MAXLEVEL;
@@ -1421,6 +1521,123 @@ void ox_positions(ox_state* s, const ox_params* p, const ox_box* b, unsigned fir
         if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
         s->temp[i]  = u_new / (double)constCv;
         s->du_m1[i] = (float)s->du[i];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Block time-steps (HydroVeBdtProp seam): positions_gpu.cu:45-179, ts_groups.cu:17-108, restated per group
+ * [gs[g], ge[g]).  dt, dt_m1 per rung and cv as the GPU seam passes them (float), evaluated in double like
+ * positionUpdate / energyUpdate (positions.hpp:54-88).
+ * ------------------------------------------------------------------------------------------------ */
+static double energy_update(double u_old, double dt, double dt_m1, double du, double du_m1)
+{
+    double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;
+    if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
+    return u_new;
+}
+
+static void position_update(double dt, double dt_m1, const double* X, const double* A, const double* dX,
+                            const ox_box* b, double* Xn, double* V, double* dXn)
+{
+    double inv = 1.0 / dt_m1, hdm1 = 0.5 * dt_m1, adt = fabs(dt);
+    for (int k = 0; k < 3; ++k)
+    {
+        double Vnmhalf = dX[k] * inv;
+        double Vn      = Vnmhalf + A[k] * hdm1;
+        V[k]           = Vn + A[k] * dt;
+        dXn[k]         = (Vn + (A[k] * 0.5) * adt) * dt;
+        Xn[k]          = X[k] + dXn[k];
+    }
+    if (b)
+        for (int d = 0; d < 3; ++d)
+        {
+            int pbc = box_pbc(b, d);
+            if (pbc && Xn[d] > b->lim[2 * d + 1]) Xn[d] -= box_l(b, d);
+            else if (pbc && Xn[d] < b->lim[2 * d]) Xn[d] += box_l(b, d);
+        }
+}
+
+/* computePositionsKernel (positions_gpu.cu:110-160), temp form, cv = (float)constCv (Thydro cv) */
+void ox_positions_rungs(ox_state* s, const uint32_t* gs, const uint32_t* ge, unsigned ng, float dt, const float* dt_m1,
+                        const uint8_t* rung, double constCv, const ox_box* b)
+{
+    float cv = (float)constCv;
+    for (unsigned g = 0; g < ng; ++g)
+        for (uint32_t i = gs[g]; i < ge[g]; ++i)
+        {
+            int fbc = b->bnd[0] == 2 || b->bnd[1] == 2 || b->bnd[2] == 2, skip = 0;
+            if (fbc && s->vx[i] == 0.0f && s->vy[i] == 0.0f && s->vz[i] == 0.0f)
+            {
+                double X[3] = {s->x[i], s->y[i], s->z[i]};
+                for (int d = 0; d < 3; ++d)
+                {
+                    double top = b->lim[2 * d + 1], bot = b->lim[2 * d];
+                    if (b->bnd[d] == 2 && (fabs(top - X[d]) < 2.0f * s->h[i] || fabs(bot - X[d]) < 2.0f * s->h[i]))
+                        skip = 1;
+                }
+            }
+            if (skip) continue;
+            double dm1  = rung ? dt_m1[rung[i]] : dt_m1[0];
+            double A[3] = {s->ax[i], s->ay[i], s->az[i]}, X[3] = {s->x[i], s->y[i], s->z[i]},
+                   dX[3] = {s->x_m1[i], s->y_m1[i], s->z_m1[i]};
+            double Xn[3], V[3], dXn[3];
+            position_update(dt, dm1, X, A, dX, b, Xn, V, dXn);
+            s->x[i] = Xn[0], s->y[i] = Xn[1], s->z[i] = Xn[2];
+            s->x_m1[i] = (float)dXn[0], s->y_m1[i] = (float)dXn[1], s->z_m1[i] = (float)dXn[2];
+            s->vx[i] = (float)V[0], s->vy[i] = (float)V[1], s->vz[i] = (float)V[2];
+            s->temp[i]  = energy_update(s->temp[i] * cv, dt, dm1, s->du[i], (double)s->du_m1[i]) / cv;
+            s->du_m1[i] = (float)s->du[i];
+        }
+}
+
+/* driftKernel (positions_gpu.cu:45-86): open box, x_m1 and du_m1 kept */
+void ox_drift_positions(ox_state* s, const uint32_t* gs, const uint32_t* ge, unsigned ng, float dt, float dt_back,
+                        const float* dt_m1, const uint8_t* rung, double constCv)
+{
+    float cv = (float)constCv;
+    for (unsigned g = 0; g < ng; ++g)
+        for (uint32_t i = gs[g]; i < ge[g]; ++i)
+        {
+            double dm1  = rung ? dt_m1[rung[i]] : dt_m1[0];
+            double A[3] = {s->ax[i], s->ay[i], s->az[i]}, Xb[3] = {s->x[i], s->y[i], s->z[i]},
+                   dX[3] = {s->x_m1[i], s->y_m1[i], s->z_m1[i]};
+            double X0[3], V[3], dXn[3], X1[3];
+            position_update(-(double)dt_back, dm1, Xb, A, dX, NULL, X0, V, dXn);
+            position_update(dt, dm1, X0, A, dX, NULL, X1, V, dXn);
+            s->x[i] = X1[0], s->y[i] = X1[1], s->z[i] = X1[2];
+            s->vx[i] = (float)V[0], s->vy[i] = (float)V[1], s->vz[i] = (float)V[2];
+            double u_recov = energy_update(s->temp[i] * cv, -(double)dt_back, dm1, s->du[i], (double)s->du_m1[i]);
+            s->temp[i]     = energy_update(u_recov, dt, dm1, s->du[i], (double)s->du_m1[i]) / cv;
+        }
+}
+
+/* groupDivvKernel / groupAccKernel (ts_groups.cu:17-68) */
+void ox_group_divv_dt(float Krho, const uint32_t* gs, const uint32_t* ge, unsigned ng, const float* divv,
+                      float* groupDt)
+{
+    for (unsigned g = 0; g < ng; ++g)
+    {
+        float m = -INFINITY;
+        for (uint32_t i = gs[g]; i < ge[g]; ++i)
+            m = m > divv[i] ? m : divv[i];
+        float v    = Krho / fabsf(m);
+        groupDt[g] = groupDt[g] < v ? groupDt[g] : v;
+    }
+}
+
+void ox_group_acc_dt(float etaAcc, const uint32_t* gs, const uint32_t* ge, unsigned ng, const float* ax,
+                     const float* ay, const float* az, float* groupDt)
+{
+    for (unsigned g = 0; g < ng; ++g)
+    {
+        float m = 0.0f;
+        for (uint32_t i = gs[g]; i < ge[g]; ++i)
+        {
+            float a2 = ax[i] * ax[i] + (ay[i] * ay[i] + az[i] * az[i]);
+            m        = m > a2 ? m : a2;
+        }
+        float v    = etaAcc / sqrtf(sqrtf(m));
+        groupDt[g] = groupDt[g] < v ? groupDt[g] : v;
     }
 }
 

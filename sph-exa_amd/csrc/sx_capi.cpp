@@ -17,6 +17,7 @@
 #include "sx_kernel_poly.hpp"
 #include "sx_observables.hpp"
 #include "sx_tree.hpp"
+#include "sx_timestep.hpp"
 
 using namespace sx;
 
@@ -358,6 +359,25 @@ extern "C"
         g->groupStart = nullptr;
         g->groupEnd   = nullptr;
         (void)c;
+        return SX_OK;
+    }
+
+    int sx_spatial_groups(sx_ctx* c, uint32_t first, uint32_t last, const double* x, const double* y,
+                          const double* z, const sx_tree* tree, const sx_box* box, float tolFactor, uint32_t* groups,
+                          uint32_t cap, sx_groups* out)
+    {
+        if (!tree || !box || !groups || !out || last < first || (last > first && (!x || !y || !z)))
+            return fail(c, SX_ERR_ARG, "sx_spatial_groups: bad arguments");
+        uint32_t ng = 0;
+        hipError_t e = spatialGroups(c->arena, first, last, x, y, z, tree->leaves, tree->numLeafNodes, tree->layout,
+                                     toDev(box), tolFactor, groups, cap, &ng, c->stream);
+        if (e == hipErrorInvalidValue) return fail(c, SX_ERR_ARG, "sx_spatial_groups: group capacity too small");
+        SX_HIP(c, e);
+        out->firstBody  = first;
+        out->lastBody   = last;
+        out->numGroups  = ng;
+        out->groupStart = groups;
+        out->groupEnd   = groups + 1;
         return SX_OK;
     }
 
@@ -748,6 +768,80 @@ extern "C"
         a.constCv = idealGasCv(muiConst, gamma);
         c->hydro().positions(a, c->stream);
         SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    // ---- block time-steps (ve-bdt seam: ts_groups.cu, positions_gpu.cu) ---------------------------------------
+
+    static GroupArgs toGroups(const sx_groups* g)
+    {
+        return GroupArgs{g->firstBody, g->lastBody, g->numGroups, g->groupStart, g->groupEnd};
+    }
+
+    static RungPosArgs rungArgs(const sx_groups* g, float dt, const float* dt_m1, const uint8_t* rung,
+                                const sx_fields* f, double gamma, double constCv)
+    {
+        RungPosArgs a{};
+        a.grp  = toGroups(g);
+        a.dt   = dt;
+        for (int k = 0; k < kMaxNumRungs; ++k)
+            a.dt_m1[k] = dt_m1[k];
+        a.rung  = rung;
+        a.x = f->x, a.y = f->y, a.z = f->z;
+        a.x_m1 = f->x_m1, a.y_m1 = f->y_m1, a.z_m1 = f->z_m1;
+        a.vx = f->vx, a.vy = f->vy, a.vz = f->vz;
+        a.ax = f->ax, a.ay = f->ay, a.az = f->az;
+        a.temp = f->temp, a.u = f->temp ? nullptr : f->u;
+        a.du = f->du, a.du_m1 = f->du_m1, a.h = f->h, a.mui = f->mui;
+        a.gamma = gamma, a.constCv = constCv;
+        return a;
+    }
+
+    static bool groupsOk(const sx_groups* g) { return g && (g->numGroups == 0 || !g->groupStart == !g->groupEnd); }
+
+    int sx_positions_rungs(sx_ctx* c, const sx_groups* g, float dt, const float* dt_m1, const uint8_t* rung,
+                           const sx_fields* f, double gamma, double constCv, const sx_box* box)
+    {
+        if (!groupsOk(g) || !dt_m1 || !f || !box || (constCv < 0 && !f->mui))
+            return fail(c, SX_ERR_ARG, "sx_positions_rungs: bad arguments");
+        RungPosArgs a = rungArgs(g, dt, dt_m1, rung, f, gamma, constCv);
+        a.box         = toDev(box);
+        SX_HIP(c, rungPositions(a, c->stream));
+        return SX_OK;
+    }
+
+    int sx_drift_positions(sx_ctx* c, const sx_groups* g, float dt, float dt_back, const float* dt_m1,
+                           const uint8_t* rung, const sx_fields* f, double gamma, double constCv)
+    {
+        if (!groupsOk(g) || !dt_m1 || !f || (constCv < 0 && !f->mui))
+            return fail(c, SX_ERR_ARG, "sx_drift_positions: bad arguments");
+        RungPosArgs a = rungArgs(g, dt, dt_m1, rung, f, gamma, constCv);
+        a.dtBack      = dt_back;
+        SX_HIP(c, driftPositions(a, c->stream));
+        return SX_OK;
+    }
+
+    int sx_group_divv_timestep(sx_ctx* c, float Krho, const sx_groups* g, const float* divv, float* groupDt)
+    {
+        if (!groupsOk(g) || (g->numGroups && (!divv || !groupDt)))
+            return fail(c, SX_ERR_ARG, "sx_group_divv_timestep: bad arguments");
+        SX_HIP(c, groupDivvTimestep(Krho, toGroups(g), divv, groupDt, c->stream));
+        return SX_OK;
+    }
+
+    int sx_group_acc_timestep(sx_ctx* c, float etaAcc, const sx_groups* g, const float* ax, const float* ay,
+                              const float* az, float* groupDt)
+    {
+        if (!groupsOk(g) || (g->numGroups && (!ax || !ay || !az || !groupDt)))
+            return fail(c, SX_ERR_ARG, "sx_group_acc_timestep: bad arguments");
+        SX_HIP(c, groupAccTimestep(etaAcc, toGroups(g), ax, ay, az, groupDt, c->stream));
+        return SX_OK;
+    }
+
+    int sx_store_rung(sx_ctx* c, const sx_groups* g, uint8_t rung, uint8_t* rungs)
+    {
+        if (!groupsOk(g) || (g->numGroups && !rungs)) return fail(c, SX_ERR_ARG, "sx_store_rung: bad arguments");
+        SX_HIP(c, storeRung(toGroups(g), rung, rungs, c->stream));
         return SX_OK;
     }
 

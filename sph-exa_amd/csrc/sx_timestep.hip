@@ -1,0 +1,213 @@
+/*! @file sx_timestep.hip
+ * @brief Block time-step (ve-bdt) seam on gfx950: group time-steps, rung bookkeeping, the rung-aware position
+ *        update and the drift of inactive rungs.  Compiled -ffp-contract=off: the formulas round exactly like the
+ *        reference's (positions.hpp:54-88 energyUpdate / positionUpdate, eos.hpp:13-18 idealGasCv).
+ *
+ * Replaces sph/include/sph/ts_groups.cu:17-108 (groupDivvTimestepGpu, groupAccTimestepGpu, storeRungGpu) and
+ * sph/include/sph/positions_gpu.cu:45-179 (driftPositionsGpu, computePositionsGpu with dt_m1 per rung).
+ *
+ * Target groups: one wavefront per group (the reference's warp on AMD, 64 lanes), groups given as
+ * [groupStart[g], groupEnd[g]) (computeSpatialGroups / sliced rung views) or, with groupStart == nullptr, the
+ * fixed 64-particle blocks of [first, last).
+ */
+#include "sx_timestep.hpp"
+
+namespace sx
+{
+
+__device__ __forceinline__ bool groupBounds(const GroupArgs& g, uint32_t w, uint32_t& s, uint32_t& e)
+{
+    if (w >= g.numGroups) return false;
+    if (g.start)
+    {
+        s = g.start[w];
+        e = g.end[w];
+    }
+    else
+    {
+        s = g.first + w * 64u;
+        e = min(s + 64u, g.last);
+    }
+    return true;
+}
+
+//! idealGasCv<float, double> (eos.hpp:13-18): R / mui in float, divided by (gamma - 1) in double, stored as float
+__device__ __forceinline__ float idealGasCvF(float mui, double gamma)
+{
+    const float R = 8.317e7f;
+    return (float)((double)(R / mui) / (gamma - 1.0f));
+}
+
+//! energyUpdate<double, double> (positions.hpp:54-61)
+__device__ __forceinline__ double energyUpdate(double u_old, double dt, double dt_m1, double du, double du_m1)
+{
+    double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;
+    if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
+    return u_new;
+}
+
+//! positionUpdate<double> (positions.hpp:77-88); pbc: putInBox on the periodic axes (box.hpp:209-230)
+__device__ __forceinline__ void positionUpdate(double dt, double dt_m1, const double X[3], const double A[3],
+                                               const double dX[3], const DevBox* pbc, double Xn[3], double Vn1[3],
+                                               double dXn1[3])
+{
+    const double inv = 1.0 / dt_m1, hdm1 = 0.5 * dt_m1, adt = fabs(dt);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const double Vnmhalf = dX[k] * inv;
+        const double Vn      = Vnmhalf + A[k] * hdm1;
+        Vn1[k]               = Vn + A[k] * dt;
+        dXn1[k]              = (Vn + (A[k] * 0.5) * adt) * dt;
+        Xn[k]                = X[k] + dXn1[k];
+    }
+    if (pbc)
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+        {
+            if (pbc->pbc[d] && Xn[d] > pbc->lim[2 * d + 1]) Xn[d] -= pbc->l[d];
+            else if (pbc->pbc[d] && Xn[d] < pbc->lim[2 * d]) Xn[d] += pbc->l[d];
+        }
+}
+
+__device__ __forceinline__ float rungDtM1(const RungPosArgs& a, uint32_t i)
+{
+    return a.rung ? a.dt_m1[a.rung[i]] : a.dt_m1[0];
+}
+
+//! computePositionsKernel (positions_gpu.cu:110-160)
+__global__ void rungPositionsKernel(RungPosArgs a)
+{
+    const uint32_t w    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t       s, e;
+    if (!groupBounds(a.grp, w, s, e)) return;
+    const uint32_t i = s + lane;
+    if (i >= e) return;
+    const DevBox& b = a.box;
+    if ((b.fbc[0] || b.fbc[1] || b.fbc[2]) && a.vx[i] == 0.0f && a.vy[i] == 0.0f && a.vz[i] == 0.0f)
+    {
+        const double X[3] = {a.x[i], a.y[i], a.z[i]};
+        for (int d = 0; d < 3; ++d)
+        {
+            const double top = b.lim[2 * d + 1], bot = b.lim[2 * d];
+            if (b.fbc[d] && (fabs(top - X[d]) < 2.0f * a.h[i] || fabs(bot - X[d]) < 2.0f * a.h[i])) return;
+        }
+    }
+    const double dt_m1 = rungDtM1(a, i);
+    const double A[3] = {a.ax[i], a.ay[i], a.az[i]}, X[3] = {a.x[i], a.y[i], a.z[i]},
+                 dX[3] = {a.x_m1[i], a.y_m1[i], a.z_m1[i]};
+    double Xn[3], V[3], dXn[3];
+    positionUpdate(a.dt, dt_m1, X, A, dX, &b, Xn, V, dXn);
+    a.x[i] = Xn[0], a.y[i] = Xn[1], a.z[i] = Xn[2];
+    a.x_m1[i] = (float)dXn[0], a.y_m1[i] = (float)dXn[1], a.z_m1[i] = (float)dXn[2];
+    a.vx[i] = (float)V[0], a.vy[i] = (float)V[1], a.vz[i] = (float)V[2];
+    if (a.temp)
+    {
+        const float cv = a.constCv < 0 ? idealGasCvF(a.mui[i], a.gamma) : (float)a.constCv;
+        a.temp[i]      = energyUpdate(a.temp[i] * cv, a.dt, dt_m1, a.du[i], (double)a.du_m1[i]) / cv;
+    }
+    else if (a.u) { a.u[i] = energyUpdate(a.u[i], a.dt, dt_m1, a.du[i], (double)a.du_m1[i]); }
+    a.du_m1[i] = (float)a.du[i];
+}
+
+//! driftKernel (positions_gpu.cu:45-86): back to the start of the hierarchy by dt_back, then forward by dt, on an
+//! open box (no PBC: drifting must not invalidate the octree); x_m1 and du_m1 are kept
+__global__ void driftKernel(RungPosArgs a)
+{
+    const uint32_t w    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t       s, e;
+    if (!groupBounds(a.grp, w, s, e)) return;
+    const uint32_t i = s + lane;
+    if (i >= e) return;
+    const double dt_m1 = rungDtM1(a, i);
+    const double A[3] = {a.ax[i], a.ay[i], a.az[i]}, Xb[3] = {a.x[i], a.y[i], a.z[i]},
+                 dX[3] = {a.x_m1[i], a.y_m1[i], a.z_m1[i]};
+    double X0[3], V[3], dXn[3], X1[3];
+    positionUpdate(-a.dtBack, dt_m1, Xb, A, dX, nullptr, X0, V, dXn);
+    positionUpdate(a.dt, dt_m1, X0, A, dX, nullptr, X1, V, dXn);
+    a.x[i] = X1[0], a.y[i] = X1[1], a.z[i] = X1[2];
+    a.vx[i] = (float)V[0], a.vy[i] = (float)V[1], a.vz[i] = (float)V[2];
+    if (a.temp)
+    {
+        const float  cv      = a.constCv < 0 ? idealGasCvF(a.mui[i], a.gamma) : (float)a.constCv;
+        const double u_recov = energyUpdate(a.temp[i] * cv, -a.dtBack, dt_m1, a.du[i], (double)a.du_m1[i]);
+        a.temp[i]            = energyUpdate(u_recov, a.dt, dt_m1, a.du[i], (double)a.du_m1[i]) / cv;
+    }
+    else if (a.u)
+    {
+        const double u_recov = energyUpdate(a.u[i], -a.dtBack, dt_m1, a.du[i], (double)a.du_m1[i]);
+        a.u[i]               = energyUpdate(u_recov, a.dt, dt_m1, a.du[i], (double)a.du_m1[i]);
+    }
+}
+
+//! groupDivvKernel (ts_groups.cu:17-36): groupDt = min(groupDt, Krho / |max divv|), one thread per group
+__global__ void groupDivvKernel(float Krho, GroupArgs g, const float* divv, float* groupDt)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t       s, e;
+    if (!groupBounds(g, t, s, e)) return;
+    float localMax = -INFINITY;
+    for (uint32_t i = s; i < e; ++i)
+        localMax = fmaxf(localMax, divv[i]);
+    groupDt[t] = fminf(groupDt[t], Krho / fabsf(localMax));
+}
+
+//! groupAccKernel (ts_groups.cu:49-68): groupDt = min(groupDt, etaAcc / |a|max^(1/2)^(1/2))
+__global__ void groupAccKernel(float etaAcc, GroupArgs g, const float* ax, const float* ay, const float* az,
+                               float* groupDt)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t       s, e;
+    if (!groupBounds(g, t, s, e)) return;
+    float maxAcc = 0;
+    for (uint32_t i = s; i < e; ++i)
+        maxAcc = fmaxf(maxAcc, ax[i] * ax[i] + (ay[i] * ay[i] + az[i] * az[i])); // norm2, right-fold dot
+    groupDt[t] = fminf(groupDt[t], etaAcc / sqrtf(sqrtf(maxAcc)));
+}
+
+//! storeRungKernel (ts_groups.cu:84-96)
+__global__ void storeRungKernel(GroupArgs g, uint8_t rung, uint8_t* rungs)
+{
+    const uint32_t w    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t       s, e;
+    if (!groupBounds(g, w, s, e)) return;
+    if (s + lane < e) rungs[s + lane] = rung;
+}
+
+static unsigned waveGrid(uint32_t numGroups) { return (numGroups + 3) / 4; }
+
+hipError_t rungPositions(const RungPosArgs& a, hipStream_t s)
+{
+    if (a.grp.numGroups) rungPositionsKernel<<<waveGrid(a.grp.numGroups), 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t driftPositions(const RungPosArgs& a, hipStream_t s)
+{
+    if (a.grp.numGroups) driftKernel<<<waveGrid(a.grp.numGroups), 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t groupDivvTimestep(float Krho, const GroupArgs& g, const float* divv, float* groupDt, hipStream_t s)
+{
+    if (g.numGroups) groupDivvKernel<<<(g.numGroups + 255) / 256, 256, 0, s>>>(Krho, g, divv, groupDt);
+    return hipGetLastError();
+}
+
+hipError_t groupAccTimestep(float etaAcc, const GroupArgs& g, const float* ax, const float* ay, const float* az,
+                            float* groupDt, hipStream_t s)
+{
+    if (g.numGroups) groupAccKernel<<<(g.numGroups + 255) / 256, 256, 0, s>>>(etaAcc, g, ax, ay, az, groupDt);
+    return hipGetLastError();
+}
+
+hipError_t storeRung(const GroupArgs& g, uint8_t rung, uint8_t* rungs, hipStream_t s)
+{
+    if (g.numGroups) storeRungKernel<<<waveGrid(g.numGroups), 256, 0, s>>>(g, rung, rungs);
+    return hipGetLastError();
+}
+
+} // namespace sx

@@ -1,0 +1,49 @@
+/*! @file sx_timestep.hpp
+ * @brief host launchers of the block time-step seam (sx_timestep.hip): group time-steps, rungs, rung-aware
+ *        positions and drift.
+ */
+#pragma once
+
+#include "sx_device.hpp"
+
+namespace sx
+{
+
+//! a GroupView (traversal/groups.hpp:19-55): explicit [start[g], end[g]) or, with start == nullptr, fixed
+//! 64-particle blocks of [first, last)
+struct GroupArgs
+{
+    uint32_t        first, last, numGroups;
+    const uint32_t* start;
+    const uint32_t* end;
+};
+
+constexpr int kMaxNumRungs = 4; //!< sph::Timestep::maxNumRungs (timestep.h:42)
+
+struct RungPosArgs
+{
+    GroupArgs      grp;
+    double         dt, dtBack; // dtBack: drift only
+    float          dt_m1[kMaxNumRungs];
+    const uint8_t* rung; // nullable: dt_m1[0] for everyone
+    DevBox         box;
+    double *       x, *y, *z;
+    float *        x_m1, *y_m1, *z_m1, *vx, *vy, *vz;
+    const float *  ax, *ay, *az;
+    double*        temp; // temp or u (the other nullptr)
+    double*        u;
+    const double*  du;
+    float*         du_m1;
+    const float*   h;
+    const float*   mui;   // per-particle mean molecular weight when constCv < 0
+    double         gamma, constCv;
+};
+
+hipError_t rungPositions(const RungPosArgs& a, hipStream_t s);
+hipError_t driftPositions(const RungPosArgs& a, hipStream_t s);
+hipError_t groupDivvTimestep(float Krho, const GroupArgs& g, const float* divv, float* groupDt, hipStream_t s);
+hipError_t groupAccTimestep(float etaAcc, const GroupArgs& g, const float* ax, const float* ay, const float* az,
+                            float* groupDt, hipStream_t s);
+hipError_t storeRung(const GroupArgs& g, uint8_t rung, uint8_t* rungs, hipStream_t s);
+
+} // namespace sx

@@ -576,6 +576,102 @@ void packC(size_t n, const float* c11, const float* c12, const float* c13, const
 }
 void tablePairs(const float* t, float2* out, hipStream_t s) { tablePairKernel<<<grid(kTableSize), 256, 0, s>>>(t, out); }
 
+// ---- target groups: computeGroupSplits<64> (traversal/groups.cuh:55-310, caller sph/groups.cu:30-47) -----------
+// One wavefront per fixed group of 64 SFC-consecutive targets: the reference's warp on AMD (GpuConfig::warpSize 64),
+// so one 64-bit split mask per group.  A split follows lane l when the distance to particle l+1, in box-scaled
+// coordinates (x * 1/lx, no origin shift), exceeds tolFactor * cbrt(smallest leaf volume of the group).
+
+__global__ void groupSplitsKernel(uint32_t first, uint32_t last, const double* __restrict__ x,
+                                  const double* __restrict__ y, const double* __restrict__ z,
+                                  const uint64_t* __restrict__ leaves, int numLeaves,
+                                  const uint32_t* __restrict__ layout, DevBox b, float tolFactor, uint32_t numFixed,
+                                  uint64_t* __restrict__ masks, uint32_t* __restrict__ numSub)
+{
+    const uint32_t g    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int      lane = threadIdx.x & 63;
+    if (g >= numFixed) return;
+    const uint32_t body = min(first + g * 64u + (uint32_t)lane, last - 1);
+    // leafIdx = upper_bound(layout, layout + numLeaves, body) - layout - 1
+    int lo = 0, hi = numLeaves;
+    while (lo < hi)
+    {
+        const int mid = (lo + hi) >> 1;
+        if (layout[mid] <= body) lo = mid + 1;
+        else hi = mid;
+    }
+    const int      leaf  = lo - 1;
+    const uint64_t range = leaves[leaf + 1] - leaves[leaf];
+    const unsigned level = (unsigned)(clz64(range - 1) - 1) / 3u; // treeLevel (64-bit keys: one unused bit)
+    // centerAndSize in the unit box (float): half-size 2^-(level+1), vol = 8 s^3, all powers of two
+    const float half = 0.5f * (1.0f / (float)(1u << kMaxLevel));
+    const float sz   = (float)(1u << (kMaxLevel - level)) * half;
+    float       vol  = 8.0f * sz * sz * sz;
+    vol              = fminf(vol, 1.0f);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+        vol = fminf(vol, __shfl_xor(vol, o, 64));
+    const double distCrit   = (double)(cbrtf(vol) * tolFactor);
+    const double distCritSq = distCrit * distCrit;
+    const double X = x[body] * b.il[0], Y = y[body] * b.il[1], Z = z[body] * b.il[2];
+    // shflDown by one; lane 63 keeps its own value (HIP: out-of-range source lane)
+    const double Xn = __shfl_down(X, 1, 64), Yn = __shfl_down(Y, 1, 64), Zn = __shfl_down(Z, 1, 64);
+    const double dx = Xn - X, dy = Yn - Y, dz = Zn - Z;
+    const double d2 = dx * dx + (dy * dy + dz * dz);
+    const uint64_t m = __ballot(d2 > distCritSq);
+    if (lane == 0)
+    {
+        masks[g]  = m;
+        numSub[g] = 1u + (uint32_t)__popcll(m);
+    }
+}
+
+//! makeSplits (groups.cuh:116-150) + the boundary scan: group boundaries of fixed group g from its split mask
+__global__ void groupBoundsKernel(uint32_t first, uint32_t numFixed, const uint64_t* __restrict__ masks,
+                                  const uint32_t* __restrict__ off, uint32_t* __restrict__ groups)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= numFixed) return;
+    uint64_t m   = masks[g];
+    uint32_t pos = first + 64u * g, k = off[g];
+    groups[k++]  = pos;
+    while (m)
+    {
+        const int length = __builtin_ctzll(m) + 1;
+        pos += (uint32_t)length;
+        groups[k++] = pos;
+        m           = length < 64 ? m >> length : 0ull;
+    }
+}
+
+hipError_t spatialGroups(Arena& arena, uint32_t first, uint32_t last, const double* x, const double* y,
+                         const double* z, const uint64_t* leaves, int numLeaves, const uint32_t* layout,
+                         const DevBox& b, float tolFactor, uint32_t* groups, uint32_t cap, uint32_t* numGroups,
+                         hipStream_t s)
+{
+    *numGroups = 0;
+    if (last <= first) return hipSuccess;
+    const uint32_t numFixed = (last - first + 63) / 64;
+    uint64_t*      masks    = arena.get<uint64_t>("grp.masks", numFixed);
+    uint32_t*      nsub     = arena.get<uint32_t>("grp.nsub", numFixed + 1);
+    uint32_t*      off      = arena.get<uint32_t>("grp.off", numFixed + 1);
+    uint32_t*      hostN    = arena.pinned<uint32_t>("grp.n", 1);
+    if (!masks || !nsub || !off || !hostN) return hipErrorOutOfMemory;
+    hipError_t e;
+    if ((e = hipMemsetAsync(nsub + numFixed, 0, 4, s))) return e;
+    groupSplitsKernel<<<(numFixed + 3) / 4, 256, 0, s>>>(first, last, x, y, z, leaves, numLeaves, layout, b,
+                                                          tolFactor, numFixed, masks, nsub);
+    if ((e = exclusiveScan(arena, "grp.scan", nsub, off, (int)numFixed + 1, s))) return e;
+    if ((e = hipMemcpyAsync(hostN, off + numFixed, 4, hipMemcpyDeviceToHost, s))) return e;
+    if ((e = hipStreamSynchronize(s))) return e;
+    const uint32_t ng = *hostN;
+    if (ng + 1 > cap) return hipErrorInvalidValue;
+    groupBoundsKernel<<<(numFixed + 255) / 256, 256, 0, s>>>(first, numFixed, masks, off, groups);
+    if ((e = hipMemcpyAsync(groups + ng, &last, 4, hipMemcpyHostToDevice, s))) return e;
+    if ((e = hipStreamSynchronize(s))) return e; // `last` lives on this stack frame
+    *numGroups = ng;
+    return hipGetLastError();
+}
+
 hipError_t maxFloat(const float* v, uint32_t first, uint32_t last, unsigned* out, hipStream_t s)
 {
     hipMemsetAsync(out, 0, 4, s);

@@ -262,6 +262,11 @@ void       packC(size_t n, const float* c11, const float* c12, const float* c13,
 void       packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s);
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
+//! computeGroupSplits<64> with tolFactor: group boundaries groups[0..numGroups] (device, capacity cap)
+hipError_t spatialGroups(Arena& arena, uint32_t first, uint32_t last, const double* x, const double* y,
+                         const double* z, const uint64_t* leaves, int numLeaves, const uint32_t* layout,
+                         const DevBox& b, float tolFactor, uint32_t* groups, uint32_t cap, uint32_t* numGroups,
+                         hipStream_t s);
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
 //! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);

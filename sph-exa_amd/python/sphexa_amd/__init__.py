@@ -123,6 +123,15 @@ def lib():
         "sx_leaf_layout": (C.c_int, [vp, vp, i32, vp]),
         "sx_compute_groups": (C.c_int, [vp, u32, u32, C.POINTER(SxGroups)]),
         "sx_set_search_mode": (C.c_int, [vp, C.c_int]),
+        "sx_positions_rungs": (C.c_int, [vp, C.POINTER(SxGroups), C.c_float, vp, vp, C.POINTER(SxFields), C.c_double,
+                                         C.c_double, C.POINTER(SxBox)]),
+        "sx_drift_positions": (C.c_int, [vp, C.POINTER(SxGroups), C.c_float, C.c_float, vp, vp, C.POINTER(SxFields),
+                                         C.c_double, C.c_double]),
+        "sx_group_divv_timestep": (C.c_int, [vp, C.c_float, C.POINTER(SxGroups), vp, vp]),
+        "sx_group_acc_timestep": (C.c_int, [vp, C.c_float, C.POINTER(SxGroups), vp, vp, vp, vp]),
+        "sx_store_rung": (C.c_int, [vp, C.POINTER(SxGroups), C.c_uint8, vp]),
+        "sx_spatial_groups": (C.c_int, [vp, u32, u32, vp, vp, vp, C.POINTER(SxTree), C.POINTER(SxBox), C.c_float,
+                                        vp, u32, C.POINTER(SxGroups)]),
         "sx_find_neighbors": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.POINTER(SxBox),
                                         C.POINTER(SxParams), u32, u32, C.c_int, C.POINTER(SxNbStats)]),
         "sx_export_neighbors": (C.c_int, [vp, vp, u32, u32, u32, vp]),
