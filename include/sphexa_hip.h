@@ -27,6 +27,7 @@
  *   sx_iad                 sph::computeIADGpu (std)             sph_gpu.hpp:19-20, hydro_std/iad_gpu.cu:111-124
  *   sx_momentum_energy_std sph::computeMomentumEnergyStdGpu     sph_gpu.hpp:22-23, hydro_std/momentum_energy_gpu.cu:109
  *   sx_positions           sph::computePositionsGpu             sph_gpu.hpp:64-72, positions_gpu.cu:167-179
+ *   sx_mark_ramp           sph::cuda::computeMarkRamp           sph_gpu.hpp:54, hydro_ve/additional_fields.cu:86-98
  *   sx_positions_rungs     sph::computePositionsGpu (rungs)     sph_gpu.hpp:64-72, positions_gpu.cu:110-179
  *   sx_drift_positions     sph::driftPositionsGpu               sph_gpu.hpp:57-62, positions_gpu.cu:45-108
  *   sx_group_divv_timestep sph::groupDivvTimestepGpu            sph_gpu.hpp:80, ts_groups.cu:17-46
@@ -280,6 +281,11 @@ int sx_momentum_energy_std(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, 
 int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
                  double gamma, float muiConst, const sx_box* box);
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
+
+/*! computeMarkRamp (sph_gpu.hpp:54, hydro_ve/additional_fields.cu:47-98): per target the mean over its neighbors of
+ *  1 (Atwood > Atmax) or ramp*(Atwood - Atmin) (Atmin <= Atwood <= Atmax), rho = kx m / xm; uses the cached list */
+int sx_mark_ramp(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                 float* markRamp);
 
 /* ---- block time-steps (HydroVeBdtProp, main/src/propagator/ve_hydro_bdt.hpp) ------------------------------------
  * Groups: explicit [groupStart[g], groupEnd[g]) (sx_spatial_groups, or a slice of a rung-sorted group list) or, with

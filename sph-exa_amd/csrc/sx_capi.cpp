@@ -554,6 +554,23 @@ PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_pa
     return a;
 }
 
+int markRamp(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+             float* markRampOut)
+{
+    if (!markRampOut || !f->kx || !f->xm || !f->m) return fail(c, SX_ERR_ARG, "sx_mark_ramp: bad arguments");
+    if (int e = checkList(c, g, p)) return e;
+    if (g->firstBody >= g->lastBody) return SX_OK;
+    const size_t n = f->n;
+    Records      r = records(c, n);
+    if (!r.rx) return fail(c, SX_ERR_NOMEM, "record allocation failed");
+    packX(n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
+    PairArgs a = pairArgs(c, g, f, p, box, r);
+    a.markRamp = markRampOut;
+    c->hydro().markRamp(a, c->stream);
+    SX_HIP(c, hipGetLastError());
+    return SX_OK;
+}
+
 int momentumEnergy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
                    const sx_box* box, float* minDtCourant, bool avClean)
 {
@@ -583,6 +600,12 @@ int momentumEnergy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_field
 
 extern "C"
 {
+
+    int sx_mark_ramp(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
+                     float* markRampOut)
+    {
+        return markRamp(c, g, f, p, box, markRampOut);
+    }
 
     int sx_xmass(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
                  const sx_tree* tree)

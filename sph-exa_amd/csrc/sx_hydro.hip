@@ -430,6 +430,25 @@ __global__ void eosKernel(EosArgs a)
 
 // ---- std propagator (HydroProp, std_hydro.hpp:124-184) ----------------------------------------------------------
 
+//! markRampJLoop (hydro_ve/additional_fields_kern.hpp:38-58) on the step's neighbor lists; rho = kx m / xm from
+//! the field arrays (m from the packed RecX records)
+__global__ __launch_bounds__(kBlock) void markRampKernel(PairArgs a)
+{
+    SX_PAIR_PROLOGUE
+    if (!valid) return;
+    const float rhoi = a.kx[i] * a.rx[i].m / a.xm[i];
+    float       mark = 0.0f;
+    for (unsigned k = 0; k < cnt; ++k)
+    {
+        const uint32_t j      = nbj(k);
+        const float    rhoj   = a.kx[j] * a.rx[j].m / a.xm[j];
+        const float    Atwood = fabsf(rhoi - rhoj) / (rhoi + rhoj);
+        if (Atwood > a.Atmax) { mark += 1.0f; }
+        else if (Atwood >= a.Atmin) { mark += a.ramp * (Atwood - a.Atmin); }
+    }
+    a.markRamp[i] = mark / (float)cnt;
+}
+
 //! convertXmassToRho (hydro_ve/xmass_gpu.cu:134-148): the xmass kernel wrote m / rho0 into rho
 __global__ void xmassToRhoKernel(uint32_t first, uint32_t last, const float* m, float* rho)
 {
@@ -698,6 +717,10 @@ static void launchIadStd(const PairArgs& a, hipStream_t s)
     if (kFastClusters && a.localLists) return cluster::iadStd(a, s);
     if (a.numGroups) iadStdKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
 }
+static void launchMarkRamp(const PairArgs& a, hipStream_t s)
+{
+    if (a.numGroups) markRampKernel<<<pairGrid(a), kBlock, 0, s>>>(a);
+}
 static void launchMomentumStd(const PairArgs& a, hipStream_t s)
 {
     if (kFastClusters && a.localLists) return cluster::momentumStd(a, s);
@@ -715,7 +738,8 @@ const HydroLaunch& SX_CAT(hydro_, SX_VARIANT)()
                                SX_VARIANT::launchAv,        SX_VARIANT::launchMomentum,   SX_VARIANT::launchEos,
                                SX_VARIANT::launchPositions, SX_VARIANT::launchUpdateH,
                                SX_VARIANT::launchXmassToRho, SX_VARIANT::launchEosStd,
-                               SX_VARIANT::launchIadStd,    SX_VARIANT::launchMomentumStd};
+                               SX_VARIANT::launchIadStd,    SX_VARIANT::launchMomentumStd,
+                               SX_VARIANT::launchMarkRamp};
     return t;
 }
 

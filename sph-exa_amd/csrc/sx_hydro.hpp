@@ -51,6 +51,8 @@ struct PairArgs
     int    avClean;
     // std propagator (HydroProp, std_hydro.hpp:124-184): rho and p of every particle (IAD, momentumEnergySTD)
     const RecS* rs;
+    // markRampJLoop (hydro_ve/additional_fields_kern.hpp:38-58): fraction of the Atwood ramp over the neighbors
+    float* markRamp;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent
@@ -147,6 +149,8 @@ struct HydroLaunch
     void (*eosStd)(const EosArgs&, hipStream_t);
     void (*iadStd)(const PairArgs&, hipStream_t);
     void (*momentumStd)(const PairArgs&, hipStream_t);
+    // diagnostic field of the KH ramp (hydro_ve/additional_fields.cu:47-98): a.markRamp from xm, kx and m
+    void (*markRamp)(const PairArgs&, hipStream_t);
 };
 
 const HydroLaunch& hydro_exact();

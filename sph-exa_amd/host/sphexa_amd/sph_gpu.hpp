@@ -288,6 +288,20 @@ void computeEOS_HydroStd(size_t firstParticle, size_t lastParticle, Trho mui, Tu
               "computeEOS_HydroStd");
 }
 
+//! sph_gpu.hpp:53-54 (hydro_ve/additional_fields.cu:86-98): the markRamp diagnostic field over [first, last) on the
+//! step's cached neighbor list
+template<class Dataset, class Box>
+void computeMarkRamp(size_t first, size_t last, Dataset& d, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    sx_groups g{(uint32_t)first, (uint32_t)last, (uint32_t)((last - first + 63) / 64), nullptr, nullptr};
+    auto      f = sa::toFields(d);
+    auto      p = sa::toParams(d);
+    auto      b = sa::toBox(box);
+    sa::check(sx_mark_ramp(sa::context(), &g, &f, &p, &b, sa::detail::rawPtr(d.devData.markRamp)), "computeMarkRamp");
+    sa::check(sx_synchronize(sa::context()), "computeMarkRamp");
+}
+
 } // namespace sph::cuda
 
 namespace sph
@@ -317,6 +331,117 @@ void computeMomentumEnergyStdGpu(const GroupView& grp, Dataset& d, const Box& bo
     float minDt;
     sa::check(sx_momentum_energy_std(sa::context(), &g, &f, &p, &b, &minDt), "computeMomentumEnergyStdGpu");
     d.minDtCourant = minDt;
+}
+
+//! sph_gpu.hpp:15-17 (sph/groups.cu:30-47): computeGroupSplits<64> with tolFactor 2 into groups.data
+template<class Dataset, class Box, class GroupData>
+void computeSpatialGroups(size_t first, size_t last, Dataset& d, const Box& box, GroupData& groups)
+{
+    namespace sa = sphexa_amd;
+    groups.data.resize(last - first + 2);
+    auto      b = sa::toBox(box);
+    auto      t = sa::toTree(d.treeView);
+    auto&     dv = d.devData;
+    sx_groups out{};
+    sa::check(sx_spatial_groups(sa::context(), (uint32_t)first, (uint32_t)last, sa::detail::rawPtr(dv.x),
+                                sa::detail::rawPtr(dv.y), sa::detail::rawPtr(dv.z), &t, &b, 2.0f,
+                                sa::detail::rawPtr(groups.data), (uint32_t)(last - first + 2), &out),
+              "computeSpatialGroups");
+    groups.data.resize(out.numGroups + 1);
+    groups.firstBody  = first;
+    groups.lastBody   = last;
+    groups.numGroups  = out.numGroups;
+    groups.groupStart = sa::detail::rawPtr(groups.data);
+    groups.groupEnd   = sa::detail::rawPtr(groups.data) + 1;
+}
+
+namespace detail_bdt
+{
+template<class A>
+void dtArray(const A& dt_m1, float (&out)[SX_MAX_RUNGS])
+{
+    for (int k = 0; k < SX_MAX_RUNGS; ++k)
+        out[k] = dt_m1[k];
+}
+template<class T>
+constexpr bool isF32 = std::is_same_v<std::remove_cv_t<T>, float>;
+template<class T>
+constexpr bool isF64 = std::is_same_v<std::remove_cv_t<T>, double>;
+} // namespace detail_bdt
+
+/*! sph_gpu.hpp:64-72 (positions_gpu.cu:110-179): rung-aware Press position update + AB2 energy update.
+ *  The MI355X library stores the reference's SphTypes: coordinates, temp/u and du in double, the rest in float */
+template<class GroupView, class Tc, class Tv, class Ta, class Tdu, class Tm1, class Tu, class Thydro, class DtM1,
+         class Box>
+void computePositionsGpu(const GroupView& grp, float dt, DtM1 dt_m1, Tc* x, Tc* y, Tc* z, Tv* vx, Tv* vy, Tv* vz,
+                         Tm1* x_m1, Tm1* y_m1, Tm1* z_m1, Ta* ax, Ta* ay, Ta* az, const uint8_t* rung, Tu* temp, Tu* u,
+                         Tdu* du, Tm1* du_m1, Thydro* h, Thydro* mui, Tc gamma, Tc constCv, const Box& box)
+{
+    namespace sa = sphexa_amd;
+    using namespace detail_bdt;
+    static_assert(isF64<Tc> && isF32<Tv> && isF32<Ta> && isF64<Tdu> && isF32<Tm1> && isF64<Tu> && isF32<Thydro>,
+                  "computePositionsGpu: the MI355X library implements the SphTypes precision (sph/types.hpp:39-46)");
+    sx_fields f{};
+    f.x = x, f.y = y, f.z = z, f.vx = vx, f.vy = vy, f.vz = vz, f.x_m1 = x_m1, f.y_m1 = y_m1, f.z_m1 = z_m1;
+    f.ax = ax, f.ay = ay, f.az = az, f.temp = temp, f.u = u, f.du = du, f.du_m1 = du_m1, f.h = h, f.mui = mui;
+    float d[SX_MAX_RUNGS];
+    dtArray(dt_m1, d);
+    auto g = sa::toGroups(grp);
+    auto b = sa::toBox(box);
+    sa::check(sx_positions_rungs(sa::context(), &g, dt, d, rung, &f, (double)gamma, (double)constCv, &b),
+              "computePositionsGpu");
+}
+
+//! sph_gpu.hpp:57-62 (positions_gpu.cu:45-108): drift back by dt_back, forward by dt (open box)
+template<class GroupView, class Tc, class Thydro, class Tm1, class Tdu, class DtM1>
+void driftPositionsGpu(const GroupView& grp, float dt, float dt_back, DtM1 dt_m1, Tc* x, Tc* y, Tc* z, Thydro* vx,
+                       Thydro* vy, Thydro* vz, const Tm1* x_m1, const Tm1* y_m1, const Tm1* z_m1, const Thydro* ax,
+                       const Thydro* ay, const Thydro* az, const uint8_t* rung, Tc* temp, Tc* u, Tdu* du, Tm1* du_m1,
+                       Thydro* mui, Tc gamma, Tc constCv)
+{
+    namespace sa = sphexa_amd;
+    using namespace detail_bdt;
+    static_assert(isF64<Tc> && isF32<Thydro> && isF32<Tm1> && isF64<Tdu>,
+                  "driftPositionsGpu: the MI355X library implements the SphTypes precision (sph/types.hpp:39-46)");
+    sx_fields f{};
+    f.x = x, f.y = y, f.z = z, f.vx = vx, f.vy = vy, f.vz = vz;
+    f.x_m1 = const_cast<Tm1*>(x_m1), f.y_m1 = const_cast<Tm1*>(y_m1), f.z_m1 = const_cast<Tm1*>(z_m1);
+    f.ax = const_cast<Thydro*>(ax), f.ay = const_cast<Thydro*>(ay), f.az = const_cast<Thydro*>(az);
+    f.temp = temp, f.u = u, f.du = du, f.du_m1 = du_m1, f.mui = mui;
+    float d[SX_MAX_RUNGS];
+    dtArray(dt_m1, d);
+    auto g = sa::toGroups(grp);
+    sa::check(sx_drift_positions(sa::context(), &g, dt, dt_back, d, rung, &f, (double)gamma, (double)constCv),
+              "driftPositionsGpu");
+}
+
+//! sph_gpu.hpp:80-81 (ts_groups.cu:17-46)
+template<class GroupView, class T>
+void groupDivvTimestepGpu(float Krho, const GroupView& grp, const T* divv, float* groupDt)
+{
+    static_assert(detail_bdt::isF32<T>, "groupDivvTimestepGpu: float hydro fields (SphTypes)");
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    sa::check(sx_group_divv_timestep(sa::context(), Krho, &g, divv, groupDt), "groupDivvTimestepGpu");
+}
+
+//! sph_gpu.hpp:83-84 (ts_groups.cu:48-81)
+template<class GroupView, class T>
+void groupAccTimestepGpu(float etaAcc, const GroupView& grp, const T* ax, const T* ay, const T* az, float* groupDt)
+{
+    static_assert(detail_bdt::isF32<T>, "groupAccTimestepGpu: float hydro fields (SphTypes)");
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    sa::check(sx_group_acc_timestep(sa::context(), etaAcc, &g, ax, ay, az, groupDt), "groupAccTimestepGpu");
+}
+
+//! sph_gpu.hpp:86 (ts_groups.cu:84-108)
+template<class GroupView>
+void storeRungGpu(const GroupView& grp, uint8_t rung, uint8_t* particleRungs)
+{
+    namespace sa = sphexa_amd;
+    auto g = sa::toGroups(grp);
+    sa::check(sx_store_rung(sa::context(), &g, rung, particleRungs), "storeRungGpu");
 }
 
 //! sph_gpu.hpp:71-72 (update_h_gpu.cu:49-60)

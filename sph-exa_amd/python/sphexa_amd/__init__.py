@@ -123,6 +123,8 @@ def lib():
         "sx_leaf_layout": (C.c_int, [vp, vp, i32, vp]),
         "sx_compute_groups": (C.c_int, [vp, u32, u32, C.POINTER(SxGroups)]),
         "sx_set_search_mode": (C.c_int, [vp, C.c_int]),
+        "sx_mark_ramp": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxParams),
+                                   C.POINTER(SxBox), vp]),
         "sx_positions_rungs": (C.c_int, [vp, C.POINTER(SxGroups), C.c_float, vp, vp, C.POINTER(SxFields), C.c_double,
                                          C.c_double, C.POINTER(SxBox)]),
         "sx_drift_positions": (C.c_int, [vp, C.POINTER(SxGroups), C.c_float, C.c_float, vp, vp, C.POINTER(SxFields),

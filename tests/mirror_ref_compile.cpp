@@ -1,0 +1,89 @@
+/*! Compile (and link) check of the C++ mirror (sph-exa_amd/host/sphexa_amd/sph_gpu.hpp) against the REFERENCE's own
+ *  types: cstone::Box<double> (sfc/box.hpp), cstone::GroupView / GroupData (traversal/groups.hpp),
+ *  cstone::OctreeNsView<double, uint64_t> (tree/octree.hpp), util::array<float, Timestep::maxNumRungs>
+ *  (sph/timestep.h), and a dataset whose devData has the members and element types of DeviceParticlesData
+ *  (sph/particles_data_gpu.cuh:78-105, std::vector standing in for thrust::device_vector).
+ *  Every function the reference's sph/include/sph/sph_gpu.hpp:15-89 declares is instantiated with the argument types
+ *  the reference's propagators pass (ve_hydro.hpp, ve_hydro_bdt.hpp, std_hydro.hpp).  Built by
+ *  tests/test_mirror_compile.py with g++ -I<reference include dirs>; never run (no GPU is touched). */
+#include <cstdint>
+#include <vector>
+
+#include "cstone/sfc/box.hpp"
+#include "cstone/traversal/groups.hpp"
+#include "cstone/tree/octree.hpp"
+#include "sph/timestep.h"
+
+#include "sphexa_amd/sph_gpu.hpp"
+
+struct DevData
+{
+    template<class T>
+    using V = std::vector<T>;
+    V<double>   x, y, z, temp, u, du;
+    V<float>    x_m1, y_m1, z_m1, du_m1;
+    V<float>    vx, vy, vz, rho, p, prho, tdpdTrho, h, m, c, cv, mue, mui, divv, curlv, ax, ay, az;
+    V<float>    c11, c12, c13, c22, c23, c33, alpha, xm, kx, gradh, dV11, dV12, dV13, dV22, dV23, dV33, markRamp;
+    V<uint64_t> keys;
+    V<unsigned> nc;
+    V<uint8_t>  rung;
+};
+
+struct Dataset
+{
+    using RealType = double;
+    using KeyType  = uint64_t;
+    DevData                                 devData;
+    cstone::OctreeNsView<double, uint64_t> treeView{};
+    double K{1}, Kcour{0.2}, Krho{0.06}, gamma{5.0 / 3.0}, minDt{1e-6}, minDtCourant{0};
+    unsigned ng0{100}, ngmax{150};
+    float    muiConst{10}, alphamin{0.05}, alphamax{1}, decay_constant{0.2}, Atmin{0.1}, Atmax{0.2}, ramp{10};
+};
+
+void instantiate(Dataset& d, const cstone::Box<double>& box, const cstone::GroupView& grp,
+                 cstone::GroupData<cstone::CpuTag>& groups, float* groupDt)
+{
+    auto& dv = d.devData;
+    sph::computeSpatialGroups(0, 100, d, box, groups);
+    sph::cuda::computeXMass(grp, d, box);
+    sph::cuda::computeDensity(grp, d, box);
+    sph::cuda::computeVeDefGradh(grp, d, box);
+    sph::cuda::computeEOS(0, 100, d.muiConst, d.gamma, dv.temp.data(), dv.m.data(), dv.kx.data(), dv.xm.data(),
+                          dv.gradh.data(), dv.prho.data(), dv.c.data(), dv.rho.data(), dv.p.data());
+    sph::cuda::computeIadDivvCurlv(grp, d, box);
+    sph::cuda::computeAVswitches(grp, d, box);
+    sph::cuda::computeMomentumEnergy<false>(grp, groupDt, d, box);
+    sph::cuda::computeMomentumEnergy<true>(grp, groupDt, d, box);
+    sph::cuda::computeEOS_HydroStd(0, 100, d.muiConst, d.gamma, dv.temp.data(), dv.m.data(), dv.rho.data(),
+                                   dv.p.data(), dv.c.data());
+    sph::cuda::computeMarkRamp(0, 100, d, box);
+    sph::computeIADGpu(grp, d, box);
+    sph::computeMomentumEnergyStdGpu(grp, d, box);
+    util::array<float, sph::Timestep::maxNumRungs> dt_m1{1e-6f, 2e-6f, 4e-6f, 8e-6f};
+    sph::computePositionsGpu(grp, 1e-6f, dt_m1, dv.x.data(), dv.y.data(), dv.z.data(), dv.vx.data(), dv.vy.data(),
+                             dv.vz.data(), dv.x_m1.data(), dv.y_m1.data(), dv.z_m1.data(), dv.ax.data(), dv.ay.data(),
+                             dv.az.data(), dv.rung.data(), dv.temp.data(), dv.u.data(), dv.du.data(), dv.du_m1.data(),
+                             dv.h.data(), dv.mui.data(), d.gamma, -1.0, box);
+    sph::driftPositionsGpu(grp, 1e-6f, 5e-7f, dt_m1, dv.x.data(), dv.y.data(), dv.z.data(), dv.vx.data(), dv.vy.data(),
+                           dv.vz.data(), dv.x_m1.data(), dv.y_m1.data(), dv.z_m1.data(), dv.ax.data(), dv.ay.data(),
+                           dv.az.data(), dv.rung.data(), dv.temp.data(), dv.u.data(), dv.du.data(), dv.du_m1.data(),
+                           dv.mui.data(), d.gamma, -1.0);
+    sph::updateSmoothingLengthGpu(grp, d.ng0, dv.nc.data(), dv.h.data());
+    sph::groupDivvTimestepGpu(float(d.Krho), grp, dv.divv.data(), groupDt);
+    sph::groupAccTimestepGpu(0.2f, grp, dv.ax.data(), dv.ay.data(), dv.az.data(), groupDt);
+    sph::storeRungGpu(grp, uint8_t(1), dv.rung.data());
+}
+
+int main(int argc, char**)
+{
+    if (argc > 100) // never executed: the check is that this links against libsphexa_hip.so
+    {
+        Dataset                           d;
+        cstone::Box<double>               box(0, 1, cstone::BoundaryType::periodic);
+        cstone::GroupView                 grp{0, 100, 2, nullptr, nullptr};
+        cstone::GroupData<cstone::CpuTag> groups;
+        float                             groupDt[2];
+        instantiate(d, box, grp, groups, groupDt);
+    }
+    return 0;
+}
