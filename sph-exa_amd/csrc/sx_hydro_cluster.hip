@@ -237,7 +237,6 @@ __device__ __forceinline__ void pbcRule(const Clu& cu, const DevBox& b, float r,
     if (cu.pbc) applyPBC(b, r, x, y, z);
 }
 
-// ---- XMass: xmassJLoop (hydro_ve/xmass_kern.hpp:50-79) ----------------------------------------------------------
 /*! |(a, b, c)| scaled by the largest component: this file flushes denormals to zero, so the plain sum of squares
  *  would lose components below ~1e-19 (tiny velocity gradients) that the reference keeps */
 __device__ __forceinline__ float norm3(float a, float b, float c)
@@ -247,6 +246,8 @@ __device__ __forceinline__ float norm3(float a, float b, float c)
     const float r = 1.0f / m, x = a * r, y = b * r, z = c * r;
     return m * sqrtf(x * x + (y * y + z * z));
 }
+
+// ---- XMass: xmassJLoop (hydro_ve/xmass_kern.hpp:50-79) ----------------------------------------------------------
 
 template<int CH, int SPLIT>
 __global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)

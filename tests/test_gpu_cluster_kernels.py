@@ -265,3 +265,37 @@ def test_cluster_kernels_std_vs_oracle(ctx, ora, ic, side, steps):
         close(k, sc["a"])
     assert mdt.value == pytest.approx(dt, rel=1e-5)
     ctx.free_all()
+
+
+def test_mark_ramp_on_cluster_lists(ctx, ora):
+    """computeMarkRamp (hydro_ve/additional_fields.cu:47-98, markRampJLoop additional_fields_kern.hpp:38-58) on the
+    search's own cluster lists vs numpy over the reference neighbor list of the fixture (same sets, float sums in
+    another order: 1e-5 relative); a Noh state has Atwood numbers across the whole ramp"""
+    params = ora.params()
+    st, box, nbr = advanced_state(ora, "noh", 20, 3, params)
+    chk = st.copy()
+    ref, _ = reference_chain(ora, chk, box, nbr, params, st.minDt)
+    n = st.n
+    rho = (ref["kx"].astype(np.float32) * st.m / ref["xm"]).astype(np.float32)
+    cnt = np.minimum(st.nc.astype(np.int64) - 1, 150)
+    nb = nbr.reshape(n, 150)
+    want = np.zeros(n, np.float64)
+    p = sx.default_params()
+    for i in range(n):
+        js = nb[i, :cnt[i]]
+        at = np.abs(rho[i] - rho[js]) / (rho[i] + rho[js])
+        want[i] = np.sum(np.where(at > p.Atmax, 1.0, np.where(at >= p.Atmin, p.ramp * (at - p.Atmin), 0.0))) / cnt[i]
+    host = gutil.host_dict(st)
+    host["xm"], host["kx"] = ref["xm"], ref["kx"]
+    ds = sx.DeviceState(ctx, host)
+    box_sx = gutil.box_to_sx(box)
+    tree, _ = gutil.device_tree(ctx, ds.dev["keys"], n, 64, box_sx)
+    ctx.check(ctx.L.sx_find_neighbors(ctx.h, C.byref(ds.fields), C.byref(tree), C.byref(box_sx), C.byref(p), 0, n, 0,
+                                      None), "search")
+    out = ctx.alloc(n, np.float32)
+    g = sx.SxGroups(firstBody=0, lastBody=n, numGroups=(n + 63) // 64)
+    ctx.check(ctx.L.sx_mark_ramp(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(p), C.byref(box_sx), out.ptr), "ramp")
+    got = out.get().astype(np.float64)
+    assert np.max(want) > 0.5  # the ramp is exercised
+    assert np.all(np.abs(got - want) <= 1e-5 * np.abs(want) + 1e-7), float(np.max(np.abs(got - want)))
+    ctx.free_all()
