@@ -367,6 +367,12 @@ int    sx_sim_set_comm(sx_sim* sim, sx_comm* comm);
 /*! this rank's share of a Sedov lattice of side^3 particles (contiguous lattice-index slab; the first step's
  *  sync moves particles to their SFC owner) */
 int    sx_sim_init_sedov_rank(sx_sim* sim, uint32_t side, int rank, int size);
+/*! overlap of the halo exchanges with the pair kernels (default on; several ranks, fast kernels): each exchange of
+ *  ve_hydro.hpp:150-186 runs on a communication stream while the clusters whose neighbor union holds no halo are
+ *  computed, the rest after it lands.  Results are bitwise identical with it off. */
+int    sx_sim_set_overlap(sx_sim* sim, int on);
+/*! interior and boundary cluster counts of the last distributed step (0, 0 without overlap) */
+int    sx_sim_overlap_stats(sx_sim* sim, uint32_t out[2]);
 /*! local particle range [first,last) and total (with halos) of the last step */
 int    sx_sim_layout(sx_sim* sim, uint64_t out[4]);
 /*! upload a host state (conserved fields, length n) */

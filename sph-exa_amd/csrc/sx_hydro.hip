@@ -681,7 +681,6 @@ static void launchMomentum(const PairArgs& a, hipStream_t s)
 {
     if (kFastClusters && a.localLists) return cluster::momentumEnergy(a, s);
     if (!a.numGroups) return;
-    if (!a.numGroups) return;
     if (a.avClean) momentumEnergyKernel<true><<<pairGrid(a), kBlock, 0, s>>>(a);
     else momentumEnergyKernel<false><<<pairGrid(a), kBlock, 0, s>>>(a);
 }
@@ -739,7 +738,8 @@ const HydroLaunch& SX_CAT(hydro_, SX_VARIANT)()
                                SX_VARIANT::launchPositions, SX_VARIANT::launchUpdateH,
                                SX_VARIANT::launchXmassToRho, SX_VARIANT::launchEosStd,
                                SX_VARIANT::launchIadStd,    SX_VARIANT::launchMomentumStd,
-                               SX_VARIANT::launchMarkRamp};
+                               SX_VARIANT::launchMarkRamp,
+                               SX_VARIANT::kFastClusters};
     return t;
 }
 

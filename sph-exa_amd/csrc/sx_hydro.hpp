@@ -53,6 +53,10 @@ struct PairArgs
     const RecS* rs;
     // markRampJLoop (hydro_ve/additional_fields_kern.hpp:38-58): fraction of the Atwood ramp over the neighbors
     float* markRamp;
+    // cluster kernels only: process the listCount clusters clusterList[0..listCount) instead of all of them (the
+    // interior / boundary split that overlaps a halo exchange with the interior clusters, sx_sim.cpp)
+    const uint32_t* clusterList;
+    uint32_t        listCount;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent
@@ -151,6 +155,8 @@ struct HydroLaunch
     void (*momentumStd)(const PairArgs&, hipStream_t);
     // diagnostic field of the KH ramp (hydro_ve/additional_fields.cu:47-98): a.markRamp from xm, kx and m
     void (*markRamp)(const PairArgs&, hipStream_t);
+    // the pair launchers honour PairArgs::clusterList (cluster kernels on local lists); false for the exact variant
+    bool clusterLists;
 };
 
 const HydroLaunch& hydro_exact();

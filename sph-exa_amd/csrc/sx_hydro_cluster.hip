@@ -75,7 +75,8 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     const int      sub  = wave & (kClusterWaves - 1);
     cu.part             = wave / kClusterWaves;
     cu.tid              = sub * kWave + lane;
-    cu.c                = xcdBlock(blockIdx.x, gridDim.x);
+    const uint32_t blk  = xcdBlock(blockIdx.x, gridDim.x);
+    cu.c                = a.clusterList ? a.clusterList[blk] : blk;
     cu.gw               = cu.c * kClusterWaves + sub;
     const uint32_t c0   = a.first + cu.c * kCluster;
     cu.i                = c0 + cu.tid;
@@ -957,31 +958,34 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 // kChVd = 2000: 40 KB of records, four VeDefGradh workgroups per CU (eight waves per SIMD)
 constexpr int kChXm = 2048, kChVd = 2000, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME, kChMeAvc = 1536;
 
-static inline unsigned clusters(const PairArgs& a) { return (a.numGroups + kClusterWaves - 1) / kClusterWaves; }
+static inline unsigned clusters(const PairArgs& a)
+{
+    return a.clusterList ? a.listCount : (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+}
 
 void xmass(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) xmassKernel<kChXm, SX_SPLIT_XM><<<clusters(a), kB * SX_SPLIT_XM, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) xmassKernel<kChXm, SX_SPLIT_XM><<<clusters(a), kB * SX_SPLIT_XM, 0, s>>>(a);
 }
 void veDefGradh(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) veDefGradhKernel<kChVd, SX_SPLIT_VD><<<clusters(a), kB * SX_SPLIT_VD, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) veDefGradhKernel<kChVd, SX_SPLIT_VD><<<clusters(a), kB * SX_SPLIT_VD, 0, s>>>(a);
 }
 void iadDivvCurlv(const PairArgs& a, hipStream_t s)
 {
 #ifdef SX_IAD_TWO_PASS
-    if (a.numGroups) iadDivvCurlvKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) iadDivvCurlvKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
 #else
-    if (a.numGroups) iadDivvCurlvFusedKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) iadDivvCurlvFusedKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
 #endif
 }
 void avSwitches(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) avSwitchesKernel<kChAv, SX_SPLIT_AV><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) avSwitchesKernel<kChAv, SX_SPLIT_AV><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
 }
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
-    if (!a.numGroups) return;
+    if (!a.numGroups || !clusters(a)) return;
     if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME_AVC, true><<<clusters(a), kB * SX_SPLIT_ME_AVC, 0, s>>>(a);
     else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
@@ -989,11 +993,11 @@ void momentumEnergy(const PairArgs& a, hipStream_t s)
 constexpr int kChIadStd = 2048, kChMeStd = 2048;
 void iadStd(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) iadDivvCurlvKernel<kChIadStd, SX_SPLIT_IAD, true><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) iadDivvCurlvKernel<kChIadStd, SX_SPLIT_IAD, true><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
 }
 void momentumStd(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups) momentumStdKernel<kChMeStd, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    if (a.numGroups && clusters(a)) momentumStdKernel<kChMeStd, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
 }
 
 } // namespace cluster

@@ -532,6 +532,16 @@ struct sx_sim
     uint64_t              numHalos{0};
     uint64_t*             cntBuf{nullptr};
 
+    // overlap of the halo exchanges with the pair kernels of the interior clusters (no halo in their union):
+    // exchanges run on commStream, joined by events; cluster index lists built after each search
+    bool        overlap{true};
+    hipStream_t commStream{nullptr};
+    hipEvent_t  evProd{nullptr}, evComm{nullptr};
+    uint32_t*   clsList{nullptr}; // [interior | boundary] cluster indices (2 x numClusters)
+    uint32_t*   clsCount{nullptr};
+    uint32_t*   clsHost{nullptr}; // pinned copy of clsCount
+    uint32_t    nInterior{0}, nBoundary{0};
+
     std::vector<hipEvent_t>  ev;
     std::vector<std::string> stageNames;
     std::vector<hipEvent_t>  kev; // begin/end pairs around the hot kernels alone
@@ -631,6 +641,7 @@ void allocFields(sx_sim* s, size_t cap)
     s->nb.reserve(a, 0, (uint32_t)cap, s->p.ngmax, true);
     s->stats      = a.get<uint32_t>("stats", kStatsWords);
     s->statsHost  = a.pinned<uint32_t>("statsHost", kStatsWords);
+    s->clsHost    = a.pinned<uint32_t>("ovl.countHost", 2);
     if (s->statsHost) std::fill(s->statsHost, s->statsHost + kStatsWords, 0u);
     s->sc         = a.get<Scalars>("scalars", 1);
     s->scHost     = a.pinned<Scalars>("scalarsHost", 1);
@@ -723,6 +734,31 @@ int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
     return SX_OK;
 }
 
+//! interior / boundary clusters: a cluster is interior when no entry of its neighbor union is a halo (outside
+//! [first, last)).  One wave per cluster; the lists are compacted with one atomic per cluster (order is free: every
+//! cluster is computed independently)
+__global__ void classifyClustersKernel(const uint32_t* uni, const uint32_t* ucount, uint32_t ucap, uint32_t first,
+                                       uint32_t last, uint32_t numClusters, uint32_t* lists, uint32_t* counts)
+{
+    const uint32_t c    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= numClusters) return;
+    const uint32_t  U = ucount[c];
+    const uint32_t* u = uni + (size_t)c * ucap;
+    bool            halo = false;
+    for (uint32_t k = lane; k < U; k += 64)
+    {
+        const uint32_t j = u[k];
+        halo |= j < first || j >= last;
+    }
+    const bool any = __ballot(halo) != 0ull;
+    if (lane == 0)
+    {
+        const uint32_t pos = atomicAdd(&counts[any ? 1 : 0], 1u);
+        lists[(any ? numClusters : 0u) + pos] = c;
+    }
+}
+
 //! exchange one set of fields for the halos of this step (send lists built by discoverHalos)
 int haloExchange(sx_sim* s, std::initializer_list<std::pair<void*, int>> fields, hipStream_t st)
 {
@@ -743,6 +779,46 @@ int haloExchange(sx_sim* s, std::initializer_list<std::pair<void*, int>> fields,
         }
         SIM_COMM(s->comm->alltoallv(buf, sb.data(), so.data(), f, rb.data(), ro.data(), st));
     }
+    return SX_OK;
+}
+
+//! whether this step's exchanges overlap with interior clusters (several ranks, cluster lists, not disabled)
+bool overlapping(const sx_sim* s, const HydroLaunch& H)
+{
+    return s->comm && s->comm->size() > 1 && s->overlap && s->nb.local && s->commStream && H.clusterLists;
+}
+
+/*! halo exchange of `fields` followed by the pair kernel `launch`, which needs the exchanged halo values.  Without
+ *  overlap: exchange, pack(0, n), launch over all clusters.  With overlap: the exchange runs on commStream after the
+ *  producer's kernels (event); meanwhile the compute stream packs the locals' records and runs the interior
+ *  clusters; then it waits for the exchange, packs the halos' records and runs the boundary clusters.  Every cluster
+ *  is computed exactly as in the serial order, so results are bitwise identical. */
+template<class Pack, class Launch>
+int exchangeThen(sx_sim* s, const HydroLaunch& H, std::initializer_list<std::pair<void*, int>> fields, Pack&& pack,
+                 Launch&& launch, PairArgs pa, hipStream_t st)
+{
+    if (!overlapping(s, H))
+    {
+        if (int e = haloExchange(s, fields, st)) return e;
+        pack(size_t(0), s->n);
+        launch(pa);
+        return SX_OK;
+    }
+    SIM_HIP(hipEventRecord(s->evProd, st));
+    SIM_HIP(hipStreamWaitEvent(s->commStream, s->evProd, 0));
+    if (int e = haloExchange(s, fields, s->commStream)) return e;
+    SIM_HIP(hipEventRecord(s->evComm, s->commStream));
+    pack(s->first, s->last);
+    const uint32_t nc = (uint32_t)((s->last - s->first + kCluster - 1) / kCluster);
+    pa.clusterList    = s->clsList;
+    pa.listCount      = s->nInterior;
+    launch(pa);
+    SIM_HIP(hipStreamWaitEvent(st, s->evComm, 0));
+    pack(size_t(0), s->first);
+    pack(s->last, s->n);
+    pa.clusterList = s->clsList + nc;
+    pa.listCount   = s->nBoundary;
+    launch(pa);
     return SX_OK;
 }
 
@@ -1198,6 +1274,9 @@ extern "C"
         for (auto& e : s->kev)
             (void)hipEventCreate(&e);
         s->kernelMs.assign(s->kernelNames.size(), 0.f);
+        if (hipStreamCreateWithFlags(&s->commStream, hipStreamNonBlocking) != hipSuccess) s->commStream = nullptr;
+        (void)hipEventCreateWithFlags(&s->evProd, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&s->evComm, hipEventDisableTiming);
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
@@ -1212,12 +1291,28 @@ extern "C"
             (void)hipEventDestroy(e);
         for (auto& e : s->kev)
             (void)hipEventDestroy(e);
+        if (s->evProd) (void)hipEventDestroy(s->evProd);
+        if (s->evComm) (void)hipEventDestroy(s->evComm);
+        if (s->commStream) (void)hipStreamDestroy(s->commStream);
         delete s;
     }
 
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
         s->comm = sx_comm_transport_internal(c);
+        return SX_OK;
+    }
+
+    int sx_sim_set_overlap(sx_sim* s, int on)
+    {
+        s->overlap = on != 0;
+        return SX_OK;
+    }
+
+    int sx_sim_overlap_stats(sx_sim* s, uint32_t out[2])
+    {
+        out[0] = s->nInterior;
+        out[1] = s->nBoundary;
         return SX_OK;
     }
 
@@ -1445,7 +1540,20 @@ extern "C"
             // the retry decision must be global: a rank redoing the sync alone would deadlock the collectives
             SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
             SIM_HIP(hipMemcpyAsync(s->statsHost + 3, flg, 4, hipMemcpyDeviceToHost, st));
+            if (overlapping(s, H))
+            {
+                const uint32_t ncl = (uint32_t)((nl + kCluster - 1) / kCluster);
+                s->clsList         = s->work.get<uint32_t>("ovl.list", 2 * (size_t)std::max(1u, ncl));
+                s->clsCount        = s->work.get<uint32_t>("ovl.count", 2);
+                SIM_HIP(hipMemsetAsync(s->clsCount, 0, 8, st));
+                if (ncl)
+                    classifyClustersKernel<<<(ncl + 3) / 4, 256, 0, st>>>(s->nb.uni, s->nb.ucount, s->nb.ucap,
+                                                                         (uint32_t)s->first, (uint32_t)s->last, ncl,
+                                                                         s->clsList, s->clsCount);
+                SIM_HIP(hipMemcpyAsync(s->clsHost, s->clsCount, 8, hipMemcpyDeviceToHost, st));
+            }
             SIM_HIP(hipStreamSynchronize(st));
+            if (overlapping(s, H)) s->nInterior = s->clsHost[0], s->nBoundary = s->clsHost[1];
             hf = s->statsHost[3];
             if (!hf) break;
             if (attempt >= 3) return SX_ERR_NOT_CONVERGED;
@@ -1475,25 +1583,32 @@ extern "C"
                        nullptr, nullptr, s->c, s->rho, s->pres};
             H.eosStd(ea, st);
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->rho, 4}, {s->pres, 4}, {s->c, 4}},
-                                     st))
-                return e;
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
-            packS(n, s->rho, s->pres, s->rs, st);
             SIM_HIP(hipEventRecord(s->kev[6], st));
-            H.iadStd(pa, st);
-            SIM_HIP(hipEventRecord(s->kev[7], st));
-            if (int e = haloExchange(s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}},
-                                     st))
+            if (int e = exchangeThen(
+                    s, H, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->rho, 4}, {s->pres, 4}, {s->c, 4}},
+                    [&](size_t a, size_t b)
+                    {
+                        packV(b - a, s->vx + a, s->vy + a, s->vz + a, s->c + a, s->rv + a, st);
+                        packS(b - a, s->rho + a, s->pres + a, s->rs + a, st);
+                    },
+                    [&](const PairArgs& p) { H.iadStd(p, st); }, pa, st))
                 return e;
+            SIM_HIP(hipEventRecord(s->kev[7], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, nullptr, s->rc, st);
             SIM_HIP(hipEventRecord(s->kev[8], st));
             SIM_HIP(hipEventRecord(s->kev[9], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             SIM_HIP(hipEventRecord(s->kev[10], st));
-            H.momentumStd(pa, st);
+            if (int e = exchangeThen(
+                    s, H, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}},
+                    [&](size_t a, size_t b)
+                    {
+                        packC(b - a, s->c11 + a, s->c12 + a, s->c13 + a, s->c22 + a, s->c23 + a, s->c33 + a, nullptr,
+                              s->rc + a, st);
+                    },
+                    [&](const PairArgs& p) { H.momentumStd(p, st); }, pa, st))
+                return e;
             SIM_HIP(hipEventRecord(s->kev[11], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
         }
@@ -1504,52 +1619,63 @@ extern "C"
             SIM_HIP(hipEventRecord(s->kev[2], st));
             H.xmass(pa, st);
             SIM_HIP(hipEventRecord(s->kev[3], st));
-            if (int e = haloExchange(s, {{s->xm, 4}}, st)) return e;
+            // ---- [xm] halos, VeDefGradh (overlapped: interior clusters while the halos are in flight)
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            // ---- VeDefGradh
-            packT(n, s->xm, nullptr, nullptr, nullptr, s->rt, st);
             SIM_HIP(hipEventRecord(s->kev[4], st));
-            H.veDefGradh(pa, st);
+            if (int e = exchangeThen(
+                    s, H, {{s->xm, 4}},
+                    [&](size_t a, size_t b) { packT(b - a, s->xm + a, nullptr, nullptr, nullptr, s->rt + a, st); },
+                    [&](const PairArgs& p) { H.veDefGradh(p, st); }, pa, st))
+                return e;
             SIM_HIP(hipEventRecord(s->kev[5], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             // ---- EOS, then the v/prho/c/kx halo exchange
             EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
                        s->gradh, s->prho, s->c, nullptr, nullptr};
             H.eos(ea, st);
-            if (int e = haloExchange(s, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}}, st))
-                return e;
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            // ---- IAD + divv/curlv, rho time-step, then the c_ij/divv exchange
-            packV(n, s->vx, s->vy, s->vz, s->c, s->rv, st);
-            packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
+            // ---- [v, prho, c, kx] halos, IAD + divv/curlv, rho time-step
+            auto packVT = [&](size_t a, size_t b)
+            {
+                packV(b - a, s->vx + a, s->vy + a, s->vz + a, s->c + a, s->rv + a, st);
+                packT(b - a, s->xm + a, s->kx + a, s->prho + a, s->alpha + a, s->rt + a, st);
+            };
             SIM_HIP(hipEventRecord(s->kev[6], st));
-            H.iadDivvCurlv(pa, st);
+            if (int e = exchangeThen(s, H, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}},
+                                     packVT, [&](const PairArgs& p) { H.iadDivvCurlv(p, st); }, pa, st))
+                return e;
             SIM_HIP(hipEventRecord(s->kev[7], st));
             SIM_HIP(maxFloat(s->divv, (uint32_t)s->first, (uint32_t)s->last, &s->sc->maxDivvU, st));
-            if (int e = haloExchange(
-                    s, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}}, st))
-                return e;
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            // ---- AV switches, then the alpha exchange
-            packC(n, s->c11, s->c12, s->c13, s->c22, s->c23, s->c33, s->divv, s->rc, st);
+            // ---- [c_ij, divv] halos, AV switches
             SIM_HIP(hipEventRecord(s->kev[8], st));
-            H.avSwitches(pa, st);
+            if (int e = exchangeThen(
+                    s, H, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}},
+                    [&](size_t a, size_t b)
+                    {
+                        packC(b - a, s->c11 + a, s->c12 + a, s->c13 + a, s->c22 + a, s->c23 + a, s->c33 + a,
+                              s->divv + a, s->rc + a, st);
+                    },
+                    [&](const PairArgs& p) { H.avSwitches(p, st); }, pa, st))
+                return e;
             SIM_HIP(hipEventRecord(s->kev[9], st));
+            SIM_HIP(hipEventRecord(s->ev[ev++], st));
+            // ---- [alpha (+ dV)] halos, momentum + energy.  With avClean the reference exchanges dV11,dV12,dV22,
+            //      dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo dV13 undefined; all six are exchanged
+            //      here so the result does not depend on the decomposition
+            auto packTa = [&](size_t a, size_t b)
+            { packT(b - a, s->xm + a, s->kx + a, s->prho + a, s->alpha + a, s->rt + a, st); };
+            auto launchMe = [&](const PairArgs& p) { H.momentumEnergy(p, st); };
+            SIM_HIP(hipEventRecord(s->kev[10], st));
             if (s->p.avClean)
             {
-                // the reference exchanges dV11,dV12,dV22,dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo
-                // dV13 undefined; all six are exchanged here so the result does not depend on the decomposition
-                if (int e = haloExchange(s, {{s->dV[0], 4}, {s->dV[1], 4}, {s->dV[2], 4}, {s->dV[3], 4}, {s->dV[4], 4},
-                                             {s->dV[5], 4}, {s->alpha, 4}},
-                                         st))
+                if (int e = exchangeThen(s, H,
+                                         {{s->dV[0], 4}, {s->dV[1], 4}, {s->dV[2], 4}, {s->dV[3], 4}, {s->dV[4], 4},
+                                          {s->dV[5], 4}, {s->alpha, 4}},
+                                         packTa, launchMe, pa, st))
                     return e;
             }
-            else if (int e = haloExchange(s, {{s->alpha, 4}}, st)) return e;
-            SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            // ---- momentum + energy
-            packT(n, s->xm, s->kx, s->prho, s->alpha, s->rt, st);
-            SIM_HIP(hipEventRecord(s->kev[10], st));
-            H.momentumEnergy(pa, st);
+            else if (int e = exchangeThen(s, H, {{s->alpha, 4}}, packTa, launchMe, pa, st)) return e;
             SIM_HIP(hipEventRecord(s->kev[11], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
         }

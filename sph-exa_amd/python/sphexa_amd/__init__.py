@@ -183,6 +183,8 @@ def lib():
                                               C.POINTER(C.c_double)]),
         "sx_sim_init_sedov_rank": (C.c_int, [vp, u32, C.c_int, C.c_int]),
         "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_sim_set_overlap": (C.c_int, [vp, C.c_int]),
+        "sx_sim_overlap_stats": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
         "sx_comm_unique_id": (C.c_int, [vp]),
         "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
@@ -429,6 +431,14 @@ class Sim:
     def set_comm(self, comm):
         self.comm = comm
         self.ctx.check(self.L.sx_sim_set_comm(self.h, comm.h), "set_comm")
+
+    def set_overlap(self, on):
+        self.ctx.check(self.L.sx_sim_set_overlap(self.h, int(bool(on))), "set_overlap")
+
+    def overlap_stats(self):
+        out = (C.c_uint32 * 2)()
+        self.L.sx_sim_overlap_stats(self.h, out)
+        return dict(interior=out[0], boundary=out[1])
 
     def layout(self):
         out = (C.c_uint64 * 4)()

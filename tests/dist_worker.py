@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--ic", default="sedov", help="sedov | sedov_dev | noh | evrard (self-gravity, G = 1)")
     ap.add_argument("--std", action="store_true", help="std propagator (HydroProp)")
+    ap.add_argument("--no-overlap", action="store_true", help="serial halo exchanges (no interior/boundary split)")
+    ap.add_argument("--av-clean", action="store_true", help="avClean momentum (dV halos)")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -45,9 +47,10 @@ def main():
     if args.ic == "evrard":
         po.converge_h(po.load_oracle(), st, obox)  # the lattice-contracted IC's h iterate in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
-    params = sx.default_params(g=1.0 if args.ic == "evrard" else 0.0, std=args.std)
+    params = sx.default_params(g=1.0 if args.ic == "evrard" else 0.0, std=args.std, av_clean=args.av_clean)
     sim = sx.Sim(ctx, 2 * st.n // size + 4096, box, params=params)
     sim.set_comm(comm)
+    sim.set_overlap(not args.no_overlap)
     if args.ic == "sedov_dev":
         sim.init_sedov(args.side, rank, size)
     else:
@@ -67,6 +70,8 @@ def main():
         out[f"s{s}_gravity"] = np.array([gs["halos"], gs["far_cells"], gs["remote_cells"]])
         lay = sim.layout()
         out[f"s{s}_layout"] = np.array([lay["first"], lay["last"], lay["n"], lay["haloRetries"]])
+        ov = sim.overlap_stats()
+        out[f"s{s}_overlap"] = np.array([ov["interior"], ov["boundary"]])
     np.savez(os.path.join(args.out, f"rank{rank}.npz"), **out)
     sim.close()
     comm.close()

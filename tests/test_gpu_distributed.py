@@ -184,3 +184,26 @@ def test_distributed_std_steps_match_oracle(tmp_path, nproc, port):
             b = ref.arrays[k][o].astype(np.float64)
             tol = 1e-4 * np.abs(b) + 1e-5 * np.max(np.abs(b))
             assert np.all(np.abs(a - b) <= tol), (s, k, np.max(np.abs(a - b) / (np.abs(b) + 1e-300)))
+
+
+@pytest.mark.parametrize("opts,port", [((), 29661), (("--std",), 29662), (("--av-clean",), 29663)])
+def test_overlapped_exchanges_bitwise_equal_serial(tmp_path, opts, port):
+    """halo exchanges overlapped with the interior clusters (communication stream, interior/boundary cluster lists,
+    ve_hydro.hpp:150-186 exchange points) give bitwise the same state as the serial exchanges, for the VE, avClean
+    and std propagators; the split is real (both lists non-empty) and covers every cluster"""
+    side, steps, nproc = 32, 2, 2
+    a_dir, b_dir = tmp_path / "ovl", tmp_path / "ser"
+    a_dir.mkdir()
+    b_dir.mkdir()
+    ovl = run_ranks_opts(a_dir, nproc, side, steps, port, "sedov", opts)
+    ser = run_ranks_opts(b_dir, nproc, side, steps, port + 100, "sedov", opts + ("--no-overlap",))
+    keys = [k for k in ovl[0] if not k.endswith("_overlap")]
+    for q in range(nproc):
+        for k in keys:
+            assert np.array_equal(ovl[q][k], ser[q][k], equal_nan=True), (q, k)
+        for s in range(steps):
+            first, last, _, _ = ovl[q][f"s{s}_layout"]
+            ncl = (last - first + 255) // 256
+            inner, bound = ovl[q][f"s{s}_overlap"]
+            assert inner + bound == ncl and inner > 0 and bound > 0, (q, s, inner, bound, ncl)
+            assert tuple(ser[q][f"s{s}_overlap"]) == (0, 0)
