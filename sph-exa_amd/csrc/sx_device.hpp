@@ -95,17 +95,19 @@ constexpr uint32_t kPowTable = 1u << 16; //!< nc values covered by the host-comp
  *  run, so the factor is tabulated on the host with glibc powf itself (powTab[nc], nc < 2^16) and the device
  *  result is bit-identical; beyond the table a double pow is used (never reached: nc <= N and the h iteration
  *  keeps nc near ng0). */
+//! the beyond-the-table factor, out of line: inlined, the double pow's polynomial constants stay live across the
+//! caller's loops (the neighbor search kept 16 of them in scratch)
+__device__ __noinline__ float updateHFactorFar(unsigned ng0, unsigned nc)
+{
+    const float c0   = 1023.0f;
+    const float ex   = (float)(1.0 / 10.0);
+    float       base = 1.0f + c0 * ng0 / (float)nc;
+    return (float)pow((double)base, (double)ex);
+}
+
 __device__ __forceinline__ float updateH(unsigned ng0, unsigned nc, float h, const float* __restrict__ powTab)
 {
-    float f;
-    if (nc < kPowTable) { f = powTab[nc]; }
-    else
-    {
-        const float c0   = 1023.0f;
-        const float ex   = (float)(1.0 / 10.0);
-        float       base = 1.0f + c0 * ng0 / (float)nc;
-        f                = (float)pow((double)base, (double)ex);
-    }
+    const float f = nc < kPowTable ? powTab[nc] : updateHFactorFar(ng0, nc);
     return h * 0.5f * f;
 }
 
