@@ -20,7 +20,7 @@ SOURCES = {
     "sx_hydro_cluster": ("csrc/sx_hydro_cluster.hip", ["-ffp-contract=fast", "-fno-slp-vectorize",
                                                        "-fgpu-flush-denormals-to-zero"]),
     "sx_hydro (fast)": ("csrc/sx_hydro.hip", ["-ffp-contract=fast", "-DSX_VARIANT=fast"]),
-    "sx_gravity": ("csrc/sx_gravity.hip", ["-ffp-contract=off"]),
+    "sx_gravity": ("csrc/sx_gravity.hip", ["-ffp-contract=off", "-fno-slp-vectorize"]),
     "sx_tree": ("csrc/sx_tree.hip", ["-ffp-contract=off"]),
     "sx_timestep": ("csrc/sx_timestep.hip", ["-ffp-contract=off"]),
 }

@@ -12,7 +12,7 @@ acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         if r["Counter_Name"] in ("FETCH_SIZE",):
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)

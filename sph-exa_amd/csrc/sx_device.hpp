@@ -198,6 +198,14 @@ __device__ __forceinline__ double readlaneD(double v, int k)
     return *reinterpret_cast<double*>(&p);
 }
 
+//! a wave-uniform double moved to scalar registers
+__device__ __forceinline__ double readfirstlaneD(double v)
+{
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 //! float atomic min for non-negative values via the ordered int representation
 __device__ __forceinline__ void atomicMinPos(float* addr, float v)
 {

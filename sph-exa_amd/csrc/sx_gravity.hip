@@ -198,48 +198,26 @@ __device__ __forceinline__ void p2p(double (&acc)[4], double xi, double yi, doub
     acc[3] += dz * invR3m;
 }
 
-//! fast M2P: the displacement is formed in double and rounded once, the expansion evaluated in float (rsqrt)
-template<class A>
-__device__ __forceinline__ void m2pFastV(A (&acc)[4], double tx, double ty, double tz, double c0, double c1,
-                                         double c2, const float (&M)[8])
+//! fast M2P on a staged record: r = t - c from float coordinates relative to the wave origin (for an accepted node
+//! |c - o| is of the order of |r|, so the relative rounding stays ~2^-23), expansion in float with the raw v_rsq_f32
+//! (rr > mac^2 > 0, never denormal).  A = {cx, cy, cz, M0}, B = {M1, M2, M3, M4}, C = {M5, M6}.
+__device__ __forceinline__ void m2pRec(float (&acc)[4], float tx, float ty, float tz, const float4& A, const float4& B,
+                                       const float2& C)
 {
-    const float r0 = (float)(tx - c0), r1 = (float)(ty - c1), r2 = (float)(tz - c2);
+    const float r0 = tx - A.x, r1 = ty - A.y, r2 = tz - A.z;
     const float rr       = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-    const float r_minus1 = __builtin_amdgcn_rsqf(rr); // raw v_rsq_f32: rr > mac^2 > 0, never denormal
+    const float r_minus1 = __builtin_amdgcn_rsqf(rr);
     const float r_minus2 = r_minus1 * r_minus1;
     const float r_minus5 = r_minus2 * r_minus2 * r_minus1;
-    const float Qrx      = fmaf(r0, M[1], fmaf(r1, M[2], r2 * M[3]));
-    const float Qry      = fmaf(r0, M[2], fmaf(r1, M[4], r2 * M[5]));
-    const float Qrz      = fmaf(r0, M[3], fmaf(r1, M[5], r2 * M[6]));
+    const float Qrx      = fmaf(r0, B.x, fmaf(r1, B.y, r2 * B.z));
+    const float Qry      = fmaf(r0, B.y, fmaf(r1, B.w, r2 * C.x));
+    const float Qrz      = fmaf(r0, B.z, fmaf(r1, C.x, r2 * C.y));
     const float rQr      = fmaf(r0, Qrx, fmaf(r1, Qry, r2 * Qrz));
-    const float rQrAndMonopole = (-2.5f * rQr * r_minus5 - M[0] * r_minus1) * r_minus2;
-    acc[0] += (A)(-fmaf(M[0], r_minus1, 0.5f * r_minus5 * rQr));
-    acc[1] += (A)fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
-    acc[2] += (A)fmaf(r_minus5, Qry, rQrAndMonopole * r1);
-    acc[3] += (A)fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
-}
-template<class A>
-__device__ __forceinline__ void m2pFast(A (&acc)[4], double tx, double ty, double tz, const double* com,
-                                        const float* M)
-{
-    const float Mv[8] = {M[0], M[1], M[2], M[3], M[4], M[5], M[6], M[7]};
-    m2pFastV(acc, tx, ty, tz, com[0], com[1], com[2], Mv);
-}
-
-//! fast P2P: displacement in double rounded to float, softened inverse distance by rsqrt
-__device__ __forceinline__ void p2pFast(double (&acc)[4], double xi, double yi, double zi, double xj, double yj,
-                                        double zj, float mj, float hi, float hj)
-{
-    const float dx = (float)(xj - xi), dy = (float)(yj - yi), dz = (float)(zj - zi);
-    const float R2     = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-    const float h_ij   = hi + hj;
-    const float R2eff  = fmaxf(R2, h_ij * h_ij);
-    const float invR   = rsqrtf(R2eff);
-    const float invR3m = mj * invR * invR * invR;
-    acc[0] -= (double)(invR3m * R2);
-    acc[1] += (double)(dx * invR3m);
-    acc[2] += (double)(dy * invR3m);
-    acc[3] += (double)(dz * invR3m);
+    const float rQrAndMonopole = (-2.5f * rQr * r_minus5 - A.w * r_minus1) * r_minus2;
+    acc[0] -= fmaf(A.w, r_minus1, 0.5f * r_minus5 * rQr);
+    acc[1] += fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
+    acc[2] += fmaf(r_minus5, Qry, rQrAndMonopole * r1);
+    acc[3] += fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
 }
 
 struct __attribute__((aligned(16))) GSrc
@@ -248,8 +226,11 @@ struct __attribute__((aligned(16))) GSrc
     float  m, h;
 };
 
+#ifndef SX_GRAV_WPE
+#define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
+#endif
 template<bool FAST>
-__global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE))) void gravityTraverseKernel(GravArgs a)
 {
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
@@ -257,6 +238,7 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     __shared__ GSrc   s_src[FAST ? 1 : 4][kWave];
     __shared__ float4 s_srcF[FAST ? 4 : 1][2][kWave]; // fast P2P: source x, y, z relative to the wave origin, m
     __shared__ float  s_hF[FAST ? 4 : 1][2][kWave];
+    __shared__ uint8_t s_idx[FAST ? 4 : 1][kWave]; // fast M2P: one quarter's accepted entries of the window
 
     const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4;
     const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * 4 + wave;
@@ -269,7 +251,7 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     const float    hi = a.h[iS];
     const uint64_t ltMask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // fast variant: coordinates relative to the wave's first target, formed in double and rounded once
-    const double ox = __shfl(xi, 0), oy = __shfl(yi, 0), oz = __shfl(zi, 0);
+    const double ox = readfirstlaneD(xi), oy = readfirstlaneD(yi), oz = readfirstlaneD(zi); // lane 0's target
     const float  txr = (float)(xi - ox), tyr = (float)(yi - oy), tzr = (float)(zi - oz);
 
     // target box of each 16-lane quarter (computeCenterAndSize, traversal_cpu.hpp:43-59), over its valid targets
@@ -288,8 +270,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
         for (int d = 0; d < 3; ++d)
         {
             const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
-            tc[qq][d]      = (h + l) * 0.5;
-            ts[qq][d]      = (h - l) * 0.5;
+            // wave-uniform: kept in scalar registers (48 VGPRs otherwise)
+            tc[qq][d]      = readfirstlaneD((h + l) * 0.5);
+            ts[qq][d]      = readfirstlaneD((h - l) * 0.5);
         }
     const uint64_t bv     = __ballot(valid); // quarters with at least one valid target (lanes fill in order)
     const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
@@ -324,22 +307,84 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     int    nM = 0, nP = 0, sp = 0;
     bool   overflow = false;
 
+    // fast evaluation layout: lane 16 * sub + t evaluates target t of EVERY quarter qq against the sub-th of each
+    // group of four interaction entries that quarter needs, so no lane idles on an entry its quarter did not accept.
+    // Per quarter the lanes fetch that quarter's targets (qx..qh), sum into fq, and the four partial sums of a target
+    // are added across subs into the target's own lane (sub == qq), which accumulates fo and, per flush, acc.
+    const int sub = lane >> 4, tq = lane & 15;
+    float qx = 0, qy = 0, qz = 0, qh = 0;
+    bool  qok = false;
+    float fq[4] = {0, 0, 0, 0}, fo[4] = {0, 0, 0, 0};
+#define SX_LOAD_QUARTER(qq)                                                                                            \
+    {                                                                                                                  \
+        const int src_ = 16 * (qq) + tq;                                                                               \
+        qx = __shfl(txr, src_), qy = __shfl(tyr, src_), qz = __shfl(tzr, src_), qh = __shfl(hi, src_);                 \
+        qok = __shfl((int)valid, src_) != 0;                                                                           \
+    }
+#define SX_FOLD_QUARTER(qq)                                                                                            \
+    _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_)                                                                  \
+    {                                                                                                                  \
+        float v_ = fq[c_];                                                                                             \
+        v_ += __shfl_xor(v_, 16);                                                                                      \
+        v_ += __shfl_xor(v_, 32);                                                                                      \
+        if (sub == (qq)) fo[c_] += v_;                                                                                 \
+        fq[c_] = 0.0f;                                                                                                 \
+    }
+#define SX_FLUSH_FO()                                                                                                  \
+    _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_) acc[c_] += (double)fo[c_], fo[c_] = 0.0f;
     auto flushM2P = [&]() {
         if constexpr (FAST)
         {
-            float fa[4] = {0, 0, 0, 0};
-            for (int k = 0; k < nM; ++k)
+            // windows of 64 entries: each lane stages one node (center relative to the wave origin, multipole) into
+            // LDS -- one load round trip per window instead of one per node -- then every quarter walks the entries
+            // it accepted four at a time
+            float4* sA = &s_srcF[wave][0][0];
+            float4* sB = &s_srcF[wave][1][0];
+            float2* sC = reinterpret_cast<float2*>(&s_hF[wave][0][0]);
+            for (int b0 = 0; b0 < nM; b0 += kWave)
             {
-                const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
-                const int node = e >> 4;
-                if (valid && (((e & 15) >> q) & 1))
-                    m2pFast(fa, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
-                if ((k & 31) == 31)
-                    for (int c = 0; c < 4; ++c)
-                        acc[c] += (double)fa[c], fa[c] = 0.0f;
+                const int nw = min(kWave, nM - b0);
+                unsigned  em = 0;
+                __builtin_amdgcn_wave_barrier(); // the previous window's records have been read
+                if (lane < nw)
+                {
+                    const int     e    = s_m2p[wave][b0 + lane];
+                    const int     node = e >> 4;
+                    const double* c    = a.centers4 + 4 * (size_t)node;
+                    const float*  M    = a.multipoles + 8 * (size_t)node;
+                    em                 = (unsigned)(e & 15);
+                    sA[lane] = make_float4((float)(c[0] - ox), (float)(c[1] - oy), (float)(c[2] - oz), M[0]);
+                    sB[lane] = make_float4(M[1], M[2], M[3], M[4]);
+                    sC[lane] = make_float2(M[5], M[6]);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+                {
+                    // the window's entries this quarter accepted, compacted in LDS; lanes take them four at a time
+                    const bool     mine = (em >> qq) & 1u;
+                    const uint64_t W    = __ballot(mine);
+                    const int      cnt  = __popcll(W);
+#ifdef SX_GRAV_NOM2P
+                    continue;
+#endif
+                    if (cnt == 0) continue;
+                    SX_LOAD_QUARTER(qq)
+                    __builtin_amdgcn_wave_barrier(); // the previous quarter's reads of s_idx are done
+                    if (mine) s_idx[wave][__popcll(W & ltMask)] = (uint8_t)lane;
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    __builtin_amdgcn_wave_barrier();
+                    if (qok)
+                        for (int k = sub; k < cnt; k += 4)
+                        {
+                            const int e = s_idx[wave][k];
+                            m2pRec(fq, qx, qy, qz, sA[e], sB[e], sC[e]);
+                        }
+                    SX_FOLD_QUARTER(qq)
+                }
             }
-            for (int c = 0; c < 4; ++c)
-                acc[c] += (double)fa[c];
+            SX_FLUSH_FO()
         }
         else
             for (int k = 0; k < nM; ++k)
@@ -399,26 +444,33 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
             if (have) loadRegs();
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
             __builtin_amdgcn_wave_barrier();
-            if (valid && ((cm >> q) & 1u))
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
             {
-                float fa0 = 0, fa1 = 0, fa2 = 0, fa3 = 0;
-                for (uint32_t s = 0; s < cn; ++s)
-                {
-                    const float4 src = s_srcF[wave][buf][s];
-                    const float  dx = src.x - txr, dy = src.y - tyr, dz = src.z - tzr;
-                    const float  R2    = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                    const float  h_ij  = hi + s_hF[wave][buf][s];
-                    const float  invR  = __builtin_amdgcn_rsqf(fmaxf(R2, h_ij * h_ij)); // >= h^2: no denormals
-                    const float  invR3m = src.w * invR * invR * invR;
-                    fa0 = fmaf(-invR3m, R2, fa0);
-                    fa1 = fmaf(dx, invR3m, fa1);
-                    fa2 = fmaf(dy, invR3m, fa2);
-                    fa3 = fmaf(dz, invR3m, fa3);
-                }
-                acc[0] += (double)fa0, acc[1] += (double)fa1, acc[2] += (double)fa2, acc[3] += (double)fa3;
+                if (!((cm >> qq) & 1u)) continue;
+#ifdef SX_GRAV_NOP2P
+                continue;
+#endif
+                SX_LOAD_QUARTER(qq)
+                if (qok)
+                    for (uint32_t s = sub; s < cn; s += 4)
+                    {
+                        const float4 src = s_srcF[wave][buf][s];
+                        const float  dx = src.x - qx, dy = src.y - qy, dz = src.z - qz;
+                        const float  R2   = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                        const float  h_ij = qh + s_hF[wave][buf][s];
+                        const float  invR = __builtin_amdgcn_rsqf(fmaxf(R2, h_ij * h_ij)); // >= h^2: no denormals
+                        const float  invR3m = src.w * invR * invR * invR;
+                        fq[0] = fmaf(-invR3m, R2, fq[0]);
+                        fq[1] = fmaf(dx, invR3m, fq[1]);
+                        fq[2] = fmaf(dy, invR3m, fq[2]);
+                        fq[3] = fmaf(dz, invR3m, fq[3]);
+                    }
+                SX_FOLD_QUARTER(qq)
             }
             buf ^= 1;
         }
+        SX_FLUSH_FO()
         nP = 0;
     };
     auto flushP2P = [&]() {
@@ -445,8 +497,7 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
                     for (uint32_t s = 0; s < cnt; ++s)
                     {
                         const GSrc src = s_src[wave][s];
-                        if constexpr (FAST) p2pFast(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
-                        else p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
+                        p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
                     }
             }
         }
@@ -519,6 +570,9 @@ __global__ __launch_bounds__(256) void gravityTraverseKernel(GravArgs a)
     }
     u = waveSum(u);
     if (lane == 0 && a.egrav) atomicAdd(a.egrav, 0.5 * u);
+#undef SX_LOAD_QUARTER
+#undef SX_FOLD_QUARTER
+#undef SX_FLUSH_FO
 }
 
 inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
