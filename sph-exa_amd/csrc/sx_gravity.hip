@@ -230,8 +230,24 @@ struct __attribute__((aligned(16))) GSrc
 #define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
 #endif
 template<bool FAST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE))) void gravityTraverseKernel(GravArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE))) void gravityTraverseKernel(GravArgs args)
 {
+    // the fields the traversal reads, as scalars: with the many closures below capturing the kernel argument by
+    // reference, the compiler copied the whole struct to scratch and addressed it through flat pointers
+    struct
+    {
+        const double *x, *y, *z, *centers4;
+        const float * m, *h, *multipoles;
+        const int32_t *childOffsets, *internalToLeaf;
+        const uint32_t* layout;
+        float *         ax, *ay, *az;
+        double*         egrav;
+        uint32_t*       err;
+        uint32_t        first, last;
+        float           G;
+    } const a{args.x, args.y, args.z, args.centers4, args.m, args.h, args.multipoles, args.childOffsets,
+              args.internalToLeaf, args.layout, args.ax, args.ay, args.az, args.egrav, args.err, args.first, args.last,
+              args.G};
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
     __shared__ int  s_p2p[4][kGList];
@@ -239,6 +255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     __shared__ float4 s_srcF[FAST ? 4 : 1][2][kWave]; // fast P2P: source x, y, z relative to the wave origin, m
     __shared__ float  s_hF[FAST ? 4 : 1][2][kWave];
     __shared__ uint8_t s_idx[FAST ? 4 : 1][kWave]; // fast M2P: one quarter's accepted entries of the window
+    __shared__ uint2   s_rng[FAST ? 4 : 1][FAST ? kGList : 1]; // fast P2P: particle range of each listed leaf
 
     const int      wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4;
     const uint32_t g    = xcdBlock(blockIdx.x, gridDim.x) * 4 + wave;
@@ -399,15 +416,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     // fast P2P: leaf sources converted to float relative coordinates while staged; the next leaf chunk (<= 64
     // sources, one per lane) is loaded into registers while the current one is evaluated from LDS
     auto flushP2PFast = [&]() {
+        // the particle ranges of all listed leaves are resolved first, one leaf per lane (two dependent loads per
+        // 64 leaves instead of per leaf), into s_rng
+        for (int b0 = 0; b0 < nP; b0 += kWave)
+            if (b0 + lane < nP)
+            {
+                const int lidx              = a.internalToLeaf[s_p2p[wave][b0 + lane] >> 4];
+                s_rng[wave][b0 + lane] = make_uint2(a.layout[lidx], a.layout[lidx + 1]);
+            }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
         int      ek = 0;
         uint32_t ec0 = 0, js = 0, jn = 0;
         unsigned jm = 0;
         auto     nextChunk = [&]() -> bool {
             while (ek < nP)
             {
-                const int      e    = __builtin_amdgcn_readfirstlane(s_p2p[wave][ek]);
-                const int      lidx = a.internalToLeaf[e >> 4];
-                const uint32_t s0 = a.layout[lidx], s1 = a.layout[lidx + 1];
+                const int      e  = __builtin_amdgcn_readfirstlane(s_p2p[wave][ek]);
+                const uint32_t s0 = __builtin_amdgcn_readfirstlane(s_rng[wave][ek].x);
+                const uint32_t s1 = __builtin_amdgcn_readfirstlane(s_rng[wave][ek].y);
                 if (s0 + ec0 < s1)
                 {
                     js = s0 + ec0;
@@ -522,8 +549,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         }
         __builtin_amdgcn_wave_barrier();
     }
-    while (sp > 0)
+    // one call site per flush (the closures are then inlined and their captures stay in registers)
+    while (true)
     {
+        const bool done = sp == 0 || overflow;
+        if (done || nM > kGList - kWave) flushM2P();
+        if (done || nP > kGList - kWave) flushP2P();
+        if (done) break;
         const int take = min(8, sp);
         sp -= take;
         const int  slot = lane >> 3, oct = lane & 7;
@@ -550,12 +582,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (overflow) break;
-        if (nM > kGList - kWave) flushM2P();
-        if (nP > kGList - kWave) flushP2P();
     }
-    flushM2P();
-    flushP2P();
     if (overflow && lane == 0) atomicOr(a.err, 1u);
 
     // output: ax += G * acc (computeGravity, traversal_cpu.hpp:218-228), egrav = 0.5 sum G m_i phi_i
