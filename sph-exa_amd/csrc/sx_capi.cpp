@@ -418,7 +418,8 @@ extern "C"
         a.prefilter      = 1;
         a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(1u, last - first));
         a.policy         = &c->nsPolicy;
-        if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab)
+        a.clStats        = c->arena.get<uint4>("ns.clstats", (a.numGroups + kClusterWaves - 1) / kClusterWaves);
+        if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab || !a.clStats)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);
         SX_HIP(c, hipMemsetAsync(c->stats, 0, kStatsWords * 4, c->stream));

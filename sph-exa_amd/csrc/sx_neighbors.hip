@@ -85,6 +85,7 @@ findNeighborsKernel(NsArgs a)
     // per wave: [0] 64 staged candidate records (pair layout), [1] the candidate index of each staged slot
     __shared__ float4   s_chunk[kClusterWaves][2][kWave];
     __shared__ int      s_numCand;
+    __shared__ uint4    s_cst[kClusterWaves]; // per-wave statistics
     // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}; s_chunk is only used inside the stream
     double4* const s_reg = reinterpret_cast<double4*>(&s_chunk[0][0][0]);
     static_assert(sizeof(s_chunk) >= 2 * kMaxRegions * sizeof(double4), "search regions alias s_chunk");
@@ -207,9 +208,11 @@ findNeighborsKernel(NsArgs a)
         };
         if (wave == 0)
         {
-            bool      overflow;
-            const int nCand = waveCollectLeaves(
-                a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, lane, overflow);
+            bool      overflow = false;
+            const int nCand    = (a.experiment & 16) ? 0
+                                                     : waveCollectLeaves(
+                                                        a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; },
+                                                        s_queue, s_cand, lane, overflow);
             if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short
             // exclusive scan of the candidate leaf sizes
             uint32_t run = 0;
@@ -250,7 +253,7 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads();
-        numCand = s_numCand;
+        numCand = (a.experiment & 8) ? 0 : s_numCand;
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
@@ -376,9 +379,10 @@ findNeighborsKernel(NsArgs a)
             }
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): staged and padded slots have landed
             __builtin_amdgcn_wave_barrier();
-            uint64_t hm;
+            uint64_t hm    = 0;
             bool     exact = !fastWave;
-            if (!exact)
+            if (a.experiment & 4) exact = false;
+            else if (!exact)
             {
                 // t = |p - r|^2 - 4h^2 = pw + (|r|^2 - 4h^2) - 2 p.r per candidate pair (packed f32, p from LDS);
                 // hit = sign bit of t, gathered by v_alignbit; |t| < tol defers the chunk to the exact double test
@@ -442,7 +446,8 @@ findNeighborsKernel(NsArgs a)
             }
             count += nh;
             uint64_t lm = hm;
-            if (local)
+            if (a.experiment & 1) {}
+            else if (local)
             {
                 // union bitmap: slot k hit by some lane -> its candidate bit
                 const uint64_t wm = waveOr64(lm);
@@ -713,7 +718,7 @@ findNeighborsKernel(NsArgs a)
         // candidate indices -> union positions (ascending either way)
         // batches of 8 list words: the 8 loads are issued together (one L2 round trip per batch instead of one per
         // word), then ranked in LDS and stored
-        const uint32_t nwl = (stored + 1) >> 1;
+        const uint32_t nwl = (a.experiment & 2) ? 0u : (stored + 1) >> 1;
         constexpr int  kRB = 8;
         for (uint32_t k0 = 0; k0 < nwl; k0 += kRB)
         {
@@ -747,7 +752,7 @@ findNeighborsKernel(NsArgs a)
         a.nc[i] = count + 1;
         if (a.iterateH) a.h[i] = hi;
     }
-    // statistics (NcStats-like)
+    // statistics (NcStats-like): per wave, then per cluster into clStats (reduced after the launch)
     const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
     const unsigned           nfail  = waveSum(failed);
     const unsigned           maxCnt = waveMax(valid ? count : 0u);
@@ -755,11 +760,20 @@ findNeighborsKernel(NsArgs a)
     const unsigned long long tested = waveSum(valid ? candTested : 0ull);
     if (lane == 0)
     {
-        if (nfail) atomicAdd(&a.stats[1], nfail);
-        atomicMax(&a.stats[2], maxCnt);
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 4), nstore);
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 6), tested);
-        if (wave == 0 && local) atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 8), (unsigned long long)ucnt);
+        if (nfail) atomicAdd(&a.stats[1], nfail); // failures only: rare
+        s_cst[wave] = make_uint4(maxCnt, (uint32_t)nstore, (uint32_t)tested, 0u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint4 t = s_cst[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+        {
+            const uint4 u = s_cst[w];
+            t.x = max(t.x, u.x), t.y += u.y, t.z += u.z;
+        }
+        t.w          = local ? ucnt : 0u;
+        a.clStats[c] = t;
     }
     __syncthreads(); // LDS is reused by the next cluster of a persistent launch
     }
@@ -831,11 +845,49 @@ __global__ void fallbackGateKernel(uint32_t* stats)
         stats[threadIdx.x] = threadIdx.x == 10 ? (redo ? 1u : 0u) : threadIdx.x == 11 ? 1u : (redo ? 0u : stats[threadIdx.x]);
 }
 
+//! per-cluster statistics -> stats[2] (max count), u64 stats[4] (stored), [6] (tested), [8] (union entries)
+__global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
+{
+    __shared__ uint32_t           s_max[16];
+    __shared__ unsigned long long s_sum[3][16];
+    uint32_t                      mx = 0;
+    unsigned long long            st = 0, te = 0, un = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    {
+        const uint4 v = cl[i];
+        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w;
+    }
+    mx = waveMax(mx), st = waveSum(st), te = waveSum(te), un = waveSum(un);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_max[w] = mx, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+            mx = max(mx, s_max[k]), st += s_sum[0][k], te += s_sum[1][k], un += s_sum[2][k];
+        stats[2]                                            = mx;
+        *reinterpret_cast<unsigned long long*>(stats + 4) = st;
+        *reinterpret_cast<unsigned long long*>(stats + 6) = te;
+        *reinterpret_cast<unsigned long long*>(stats + 8) = un;
+    }
+}
+
+static hipError_t reduceClusterStats(const NsArgs& a, hipStream_t s)
+{
+    const uint32_t clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    reduceClusterStatsKernel<<<1, 1024, 0, s>>>(a.clStats, clusters, a.stats);
+    return hipGetLastError();
+}
+
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
     const int mode = a.policy ? a.policy->mode : 1;
-    if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge())) return findNeighborsOnce(a, s, 0);
+    if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge()))
+    {
+        if (hipError_t e = findNeighborsOnce(a, s, 0)) return e;
+        return reduceClusterStats(a, s);
+    }
     const uint32_t n = a.last - a.first;
     hipError_t     e;
     if (a.iterateH &&
@@ -849,7 +901,8 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
     fallbackGateKernel<<<1, 64, 0, s>>>(a.stats);
     NsArgs b = a;
     b.gate   = a.stats + 10;
-    return findNeighborsOnce(b, s, 2048);
+    if ((e = findNeighborsOnce(b, s, 2048))) return e;
+    return reduceClusterStats(a, s);
 }
 #endif
 

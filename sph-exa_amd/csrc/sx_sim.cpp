@@ -1521,7 +1521,31 @@ extern "C"
             na.prefilter      = 1;
             na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(1, s->last - s->first));
             na.policy         = &s->nsPolicy;
-            if (!na.hSave) return SX_ERR_NOMEM;
+            na.clStats        = s->mem.get<uint4>("ns.clstats", (na.numGroups + kClusterWaves - 1) / kClusterWaves);
+            if (!na.hSave || !na.clStats) return SX_ERR_NOMEM;
+            if (const char* reps = getenv("SX_SEARCH_REPS"); reps && attempt == 0)
+            {
+                // timing hook for search experiments (scripts/ab_search.sh): the search without the h iteration,
+                // repeated on this step's state before the real search; experiment bits from SX_SEARCH_EXP
+                NsArgs x     = na;
+                x.iterateH   = 0;
+                x.experiment = getenv("SX_SEARCH_EXP") ? atoi(getenv("SX_SEARCH_EXP")) : 0;
+                NsPolicy pol;
+                pol.mode = getenv("SX_SEARCH_LARGE") ? 1 : 2; // compact build first (as in the real search)
+                x.policy = &pol;
+                const int R  = std::max(1, atoi(reps));
+                SIM_HIP(hipEventRecord(s->kev[0], st));
+                for (int r = 0; r < R; ++r)
+                {
+                    SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
+                    SIM_HIP(findNeighbors(x, st));
+                }
+                SIM_HIP(hipEventRecord(s->kev[1], st));
+                SIM_HIP(hipEventSynchronize(s->kev[1]));
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, s->kev[0], s->kev[1]);
+                fprintf(stderr, "search-reps exp %d: %.3f ms per search (%d reps)\n", x.experiment, ms / R, R);
+            }
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));

@@ -213,6 +213,9 @@ struct NsArgs
     int             prefilter; // 1: packed f32 distance test in the cluster frame, exact double test only for the
                                // ambiguous chunks; 0: the exact double test for every candidate
     uint32_t*       stats;     // kStatsWords words, see above
+    uint4*          clStats;   // per cluster {max count, stored, tested, union}: reduced into stats by one small
+                               // kernel after the search (per-wave atomics on the stats words serialised: 10 ms of a
+                               // 64M-particle search)
     // optional (both non-null): the compact build runs first (policy permitting) with h saved to hSave
     // (last - first floats); if one of its capacities was exceeded, kernels on the stream restore h and redo the
     // range with the large build -- no host synchronisation
@@ -220,6 +223,9 @@ struct NsArgs
     NsPolicy*       policy;
     const uint32_t* gate; // set by findNeighbors for the fallback launch: the kernel runs only if *gate != 0
     int             forceOverflow; // compact build only: report a capacity overflow for every cluster (mode 3)
+    int             experiment;    // search-cost experiments of the SX_SEARCH_REPS timing hook (sx_sim.cpp), 0 in
+                                   // every real search: 1 no list append, 2 no union rewrite, 4 no distance test,
+                                   // 8 no candidate stream, 16 no tree walk
 
     void setLists(const NbLists& L)
     {
