@@ -538,6 +538,7 @@ PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_pa
     a.az             = f->az;
     a.du             = f->du;
     a.minDt          = c->minDt;
+    a.blockDt        = c->arena.get<float>("pair.blockdt", std::max<size_t>(1, (size_t(g->lastBody - g->firstBody) + kCluster - 1) / kCluster));
     a.alphamin       = p->alphamin;
     a.alphamax       = p->alphamax;
     a.decay_constant = p->decay_constant;
@@ -971,6 +972,7 @@ extern "C"
         a.fast       = c->exact ? 0 : 1; // exact: the reference's double M2P/P2P; fast: float expansions
         SX_HIP(c, hipMemsetAsync(acc, 0, sizeof(double), c->stream));
         SX_HIP(c, hipMemsetAsync(er, 0, sizeof(uint32_t), c->stream));
+        a.waveE      = c->arena.get<double>("grav.waveE", (a.last - a.first + kWave - 1) / kWave + 1);
         SX_HIP(c, gravityTraverse(a, c->stream));
         double   eh = 0;
         uint32_t eb = 0;

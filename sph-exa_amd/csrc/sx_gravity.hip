@@ -241,12 +241,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         const int32_t *childOffsets, *internalToLeaf;
         const uint32_t* layout;
         float *         ax, *ay, *az;
-        double*         egrav;
+        double *        egrav, *waveE;
         uint32_t*       err;
         uint32_t        first, last;
         float           G;
     } const a{args.x, args.y, args.z, args.centers4, args.m, args.h, args.multipoles, args.childOffsets,
-              args.internalToLeaf, args.layout, args.ax, args.ay, args.az, args.egrav, args.err, args.first, args.last,
+              args.internalToLeaf, args.layout, args.ax, args.ay, args.az, args.egrav, args.waveE, args.err, args.first,
+              args.last,
               args.G};
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
@@ -596,7 +597,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         a.az[i]        = (float)((double)a.az[i] + G * acc[3]);
     }
     u = waveSum(u);
-    if (lane == 0 && a.egrav) atomicAdd(a.egrav, 0.5 * u);
+    if (lane == 0 && a.waveE) a.waveE[g] = 0.5 * u;
+    else if (lane == 0 && a.egrav) atomicAdd(a.egrav, 0.5 * u);
 #undef SX_LOAD_QUARTER
 #undef SX_FOLD_QUARTER
 #undef SX_FLUSH_FO
@@ -765,12 +767,31 @@ hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipS
     return hipGetLastError();
 }
 
+//! sum of the per-wave energies of one traversal -> *egrav (one atomic)
+__global__ __launch_bounds__(1024) void reduceWaveEnergyKernel(const double* v, uint32_t n, double* egrav)
+{
+    __shared__ double s_e[16];
+    double            e = 0.0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        e += v[i];
+    e = waveSum(e);
+    if ((threadIdx.x & 63) == 0) s_e[threadIdx.x >> 6] = e;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+            e += s_e[w];
+        atomicAdd(egrav, e);
+    }
+}
+
 hipError_t gravityTraverse(const GravArgs& a, hipStream_t s)
 {
     if (a.last <= a.first) return hipSuccess;
     const uint32_t waves = (a.last - a.first + kWave - 1) / kWave;
     if (a.fast) gravityTraverseKernel<true><<<(waves + 3) / 4, 256, 0, s>>>(a);
     else gravityTraverseKernel<false><<<(waves + 3) / 4, 256, 0, s>>>(a);
+    if (a.waveE && a.egrav) reduceWaveEnergyKernel<<<1, 1024, 0, s>>>(a.waveE, waves, a.egrav);
     return hipGetLastError();
 }
 

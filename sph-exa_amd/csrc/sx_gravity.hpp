@@ -28,6 +28,8 @@ struct GravArgs
     float   G, invTheta;
     float * ax, *ay, *az; // gravity is added
     double*   egrav;      // device accumulator (atomic), nullable
+    double*   waveE;      // nullable: per-wavefront potential-energy sums of the traversal ((last-first+63)/64), reduced
+                          // into *egrav by one small kernel (one atomic per launch instead of one per wave)
     uint32_t* err;        // bit 0: traversal stack exhausted
     int       fast;       // 1: M2P/P2P in float with rsqrt (displacements formed in double, sums in double)
 };

@@ -39,6 +39,8 @@ struct PairArgs
     float *  ax, *ay, *az;
     double*  du;
     float*   minDt;   // device scalar, atomic min (Courant)
+    float*   blockDt; // cluster kernels, nullable: per-workgroup Courant minima (one per launched workgroup),
+                      // reduced into *minDt by one small kernel after the launch instead of one atomic per workgroup
     float*   groupDt; // nullable, per 64-block min
     // params
     float  alphamin, alphamax, decay_constant;

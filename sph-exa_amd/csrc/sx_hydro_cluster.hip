@@ -819,7 +819,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
         float m = s_red[0];
         for (int w = 1; w < kClusterWaves * SPLIT; ++w)
             m = s_red[w] < m ? s_red[w] : m;
-        atomicMinPos(a.minDt, m);
+        if (a.blockDt) a.blockDt[blockIdx.x] = m;
+        else atomicMinPos(a.minDt, m);
     }
 }
 
@@ -927,7 +928,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
         float m = s_red[0];
         for (int w = 1; w < kClusterWaves * SPLIT; ++w)
             m = s_red[w] < m ? s_red[w] : m;
-        atomicMinPos(a.minDt, m);
+        if (a.blockDt) a.blockDt[blockIdx.x] = m;
+        else atomicMinPos(a.minDt, m);
     }
 }
 
@@ -983,11 +985,34 @@ void avSwitches(const PairArgs& a, hipStream_t s)
 {
     if (a.numGroups && clusters(a)) avSwitchesKernel<kChAv, SX_SPLIT_AV><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
 }
+//! min over the per-workgroup Courant time-steps of one launch -> *minDt (one atomic)
+__global__ __launch_bounds__(1024) void reduceBlockDtKernel(const float* v, uint32_t n, float* minDt)
+{
+    __shared__ float s_m[16];
+    float            m = INFINITY;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        m = fminf(m, v[i]);
+    m = waveMin(m);
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+            m = fminf(m, s_m[w]);
+        atomicMinPos(minDt, m);
+    }
+}
+static void reduceBlockDt(const PairArgs& a, hipStream_t s)
+{
+    if (a.blockDt) reduceBlockDtKernel<<<1, 1024, 0, s>>>(a.blockDt, clusters(a), a.minDt);
+}
+
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
     if (!a.numGroups || !clusters(a)) return;
     if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME_AVC, true><<<clusters(a), kB * SX_SPLIT_ME_AVC, 0, s>>>(a);
     else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    reduceBlockDt(a, s);
 }
 // std propagator: the IAD kernel without velocity derivatives (16 B records), momentum with 68 B records
 constexpr int kChIadStd = 2048, kChMeStd = 2048;
@@ -997,7 +1022,9 @@ void iadStd(const PairArgs& a, hipStream_t s)
 }
 void momentumStd(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups && clusters(a)) momentumStdKernel<kChMeStd, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    if (!a.numGroups || !clusters(a)) return;
+    momentumStdKernel<kChMeStd, SX_SPLIT_ME><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
+    reduceBlockDt(a, s);
 }
 
 } // namespace cluster

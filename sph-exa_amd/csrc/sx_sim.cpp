@@ -686,6 +686,7 @@ PairArgs simPairArgs(sx_sim* s)
     a.az             = s->az;
     a.du             = s->du;
     a.minDt          = &s->sc->courant;
+    a.blockDt        = s->mem.get<float>("pair.blockdt", std::max<size_t>(1, (s->last - s->first + kCluster - 1) / kCluster));
     a.alphamin       = s->p.alphamin;
     a.alphamax       = s->p.alphamax;
     a.decay_constant = s->p.decay_constant;
@@ -1197,6 +1198,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     ga.err   = &s->sc->gravErr;
     ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
+    ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(ga, st));
 
     // --- 6. far field: far cells as leaves of the level-6 tree, traversed by the locals
@@ -1221,6 +1223,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     fa.err   = &s->sc->gravErr;
     fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
+    fa.waveE = s->work.get<double>("grav.waveE", (fa.last - fa.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(fa, st));
     s->gravHalos       = nLow + nHigh;
     s->gravRemoteCells = nAll;
@@ -1734,6 +1737,7 @@ extern "C"
             ga.err   = &s->sc->gravErr;
             ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
+            ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
             SIM_HIP(gravityTraverse(ga, st));
             }
             const size_t nl = s->last - s->first;
