@@ -247,6 +247,31 @@ def make_box(lim, bnd):
     return b
 
 
+# the step attributes of a restart file, in the order ParticlesData::loadOrStoreAttributes writes them
+# (particles_data.hpp:170-190) followed by Box::loadOrStore (box.hpp:170-171)
+ATTRIBUTE_NAMES = ["iteration", "numParticlesGlobal", "ng0", "ngmax", "time", "minDt", "minDt_m1", "Kcour", "Krho",
+                   "gravConstant", "gamma", "eps", "etaAcc", "muiConst", "alphamin", "alphamax", "decay_constant",
+                   "sincIndex", "kernelChoice", "box", "boundaryType"]
+
+
+def reference_attributes(params, box, scalars, iteration, num_particles_global):
+    """the reference's restart attributes with the reference's types (size_t/uint64 counters, double scalars, float
+    muiConst/alpha parameters, int kernel choice, 6 box limits, 3 boundary-type chars)"""
+    p = params
+    return {
+        "iteration": np.uint64(iteration), "numParticlesGlobal": np.uint64(num_particles_global),
+        "ng0": np.uint32(p.ng0), "ngmax": np.uint32(p.ngmax), "time": np.float64(scalars["ttot"]),
+        "minDt": np.float64(scalars["minDt"]), "minDt_m1": np.float64(scalars["minDt_m1"]),
+        "Kcour": np.float64(p.Kcour), "Krho": np.float64(p.Krho), "gravConstant": np.float64(p.g),
+        "gamma": np.float64(p.gamma), "eps": np.float64(p.eps), "etaAcc": np.float64(p.etaAcc),
+        "muiConst": np.float32(p.muiConst), "alphamin": np.float32(p.alphamin), "alphamax": np.float32(p.alphamax),
+        "decay_constant": np.float32(p.decay_constant), "sincIndex": np.float64(6.0),  # sinc_6, the kernel tabulated
+        "kernelChoice": np.int32(0),  # SphKernelType::sinc_n
+        "box": np.array([box.lim[k] for k in range(6)], dtype=np.float64),
+        "boundaryType": np.array([box.bnd[k] for k in range(3)], dtype=np.int8),
+    }
+
+
 class SxError(RuntimeError):
     pass
 
@@ -421,6 +446,7 @@ class Sim:
         self.L = ctx.L
         self.params = params or default_params()
         self.box = box
+        self.iteration = 0  # completed steps (the reference's "iteration" attribute)
         self.h = C.c_void_p()
         ctx.check(self.L.sx_sim_create(C.byref(self.h), ctx.h, int(capacity), C.byref(self.params), C.byref(box),
                                        bucket), "sx_sim_create")
@@ -457,26 +483,30 @@ class Sim:
 
     CONSERVED = ["x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "id"]
 
-    def save_checkpoint(self, path):
+    def save_checkpoint(self, path, num_particles_global=None):
         """restart file of this rank: the conserved fields under the reference's field names
         (ParticlesData::fieldNames, particles_data.hpp:247-251; the set HydroVeProp restarts from,
-        ve_hydro.hpp:74 + x,y,z,h,m) and the time-step scalars, as an .npz (HDF5/H5Part is not in this image)"""
+        ve_hydro.hpp:74 + x,y,z,h,m) and the step attributes under the reference's names
+        (reference_attributes: ParticlesData::loadOrStoreAttributes, particles_data.hpp:142-193, and
+        Box::loadOrStore, box.hpp:168-175), as an .npz (HDF5/H5Part is not in this image)"""
         st = self.get(self.CONSERVED)
-        sc = self.scalars()
-        np.savez(path, **st, minDt=np.float64(sc["minDt"]), minDt_m1=np.float64(sc["minDt_m1"]),
-                 ttot=np.float64(sc["ttot"]))
+        attrs = reference_attributes(self.params, self.box, self.scalars(), self.iteration,
+                                     self.size() if num_particles_global is None else num_particles_global)
+        np.savez(path, **st, **attrs)
 
     def load_checkpoint(self, path):
-        """continue from save_checkpoint's file: set_state with the saved fields and time-steps"""
+        """continue from save_checkpoint's file: set_state with the saved fields and time-steps; returns the time"""
         with np.load(path, allow_pickle=False) as d:
             st = {k: d[k] for k in self.CONSERVED}
             self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
-            return float(d["ttot"])
+            self.iteration = int(d["iteration"])
+            return float(d["time"])
 
     def step(self):
         rc = self.L.sx_sim_step(self.h)
         if rc != SX_OK:
             raise SxError(f"sx_sim_step failed with code {rc}")
+        self.iteration += 1
 
     def size(self):
         return self.L.sx_sim_size(self.h)

@@ -91,5 +91,9 @@ def test_checkpoint_restart_bitwise(ctx, tmp_path):
     for k in names:
         assert np.array_equal(ga[k][oa], gb[k][ob]), k
     assert a.scalars()["minDt"] == b.scalars()["minDt"]
+    with np.load(ck, allow_pickle=False) as d:  # the reference's restart attributes (particles_data.hpp:170-190)
+        assert all(n in d for n in sx.ATTRIBUTE_NAMES)
+        assert int(d["iteration"]) == 2 and int(d["numParticlesGlobal"]) == st.n
+    assert b.iteration == 4
     a.close()
     b.close()
