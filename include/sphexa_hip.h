@@ -281,6 +281,9 @@ int sx_momentum_energy_std(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, 
 int sx_positions(sx_ctx* ctx, uint32_t first, uint32_t last, double dt, double dt_m1, const sx_fields* f,
                  double gamma, float muiConst, const sx_box* box);
 int sx_update_h(sx_ctx* ctx, uint32_t first, uint32_t last, uint32_t ng0, const uint32_t* nc, float* h);
+/*! updateSmoothingLengthGpu over the targets of a group view (update_h_gpu.cu:49-60; ve_hydro_bdt.hpp:369 passes the
+ *  active rungs): explicit groups, or fixed 64-blocks of [firstBody, lastBody) when groupStart is NULL */
+int sx_update_h_groups(sx_ctx* ctx, const sx_groups* g, uint32_t ng0, const uint32_t* nc, float* h);
 
 /*! computeMarkRamp (sph_gpu.hpp:54, hydro_ve/additional_fields.cu:47-98): per target the mean over its neighbors of
  *  1 (Atwood > Atmax) or ramp*(Atwood - Atmin) (Atmin <= Atwood <= Atmax), rho = kx m / xm; uses the cached list */

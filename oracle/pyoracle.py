@@ -407,6 +407,12 @@ class Lib:
         s = st.struct()
         self.lib.eos(C.byref(s), C.byref(p), first, st.n if last is None else last)
 
+    def update_h_range(self, st, ng0, first=0, last=None):
+        """updateSmoothingLength over [first, last) (ox_update_h_range)"""
+        s = st.struct()
+        self.lib.update_h_range(C.byref(s), ng0, first, st.n if last is None else last)
+        st.pull(s)
+
     def positions(self, st, box, first=0, last=None, params=None):
         p = params or self.params()
         s = st.struct()

@@ -110,6 +110,7 @@ struct sx_ctx
 {
     int         device{0};
     NsPolicy    nsPolicy;       // neighbor search: compact or large build (sx_tree.hpp)
+    const uint8_t* viewActive{nullptr}; // active-target mask of the current call's group view (nullptr: all)
     hipStream_t own{nullptr};
     hipStream_t stream{nullptr};
     bool        exact{false};
@@ -389,8 +390,18 @@ extern "C"
         return SX_OK;
     }
 
+    static int findNeighborsView(sx_ctx* c, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                                 const sx_params* p, uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats);
+
     int sx_find_neighbors(sx_ctx* c, const sx_fields* f, const sx_tree* tree, const sx_box* box, const sx_params* p,
                           uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats)
+    {
+        c->viewActive = nullptr;
+        return findNeighborsView(c, f, tree, box, p, first, last, iterate_h, stats);
+    }
+
+    static int findNeighborsView(sx_ctx* c, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                                 const sx_params* p, uint32_t first, uint32_t last, int iterate_h, sx_nbstats* stats)
     {
         if (!f || !tree || !box || !p || last < first || last > f->n)
             return fail(c, SX_ERR_ARG, "sx_find_neighbors: bad arguments");
@@ -413,12 +424,14 @@ extern "C"
         a.sizes          = tree->sizes;
         a.box            = toDev(box);
         a.margin         = quantMargin(a.box);
+        a.extFactor      = tree->searchExtFactor;
         a.stats          = c->stats;
         a.powTab         = ensurePowTab(c, p->ng0);
         a.prefilter      = 1;
         a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(1u, last - first));
         a.policy         = &c->nsPolicy;
         a.clStats        = c->arena.get<uint4>("ns.clstats", (a.numGroups + kClusterWaves - 1) / kClusterWaves);
+        a.active         = c->viewActive;
         if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab || !a.clStats)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);
@@ -490,6 +503,39 @@ Records records(sx_ctx* c, size_t n)
             c->arena.get<RecC>("rec.c", n)};
 }
 
+/*! A group view with explicit groups (a GroupView slice, e.g. the active rungs of ve-bdt, whose extracted groups carry
+ *  firstBody = lastBody = 0, sph/groups.hpp:33-48) becomes the target range [min start, max end) plus an active-target
+ *  mask in c->viewActive: the pair kernels and the search skip every target outside the view's groups, like the
+ *  reference kernels that visit only the view's groups.  Without explicit groups: [firstBody, lastBody), all active. */
+int resolveView(sx_ctx* c, const sx_groups*& g, sx_groups& tmp, size_t n, bool cachedList = true)
+{
+    c->viewActive = nullptr;
+    if (!g) return fail(c, SX_ERR_ARG, "null group view");
+    if (!g->groupStart || g->numGroups == 0) return SX_OK;
+    uint8_t*  act = c->arena.get<uint8_t>("view.active", n);
+    uint32_t* mm  = c->arena.get<uint32_t>("view.range", 2);
+    if (!act || !mm) return fail(c, SX_ERR_NOMEM, "group view scratch");
+    const uint32_t init[2] = {0xffffffffu, 0u};
+    SX_HIP(c, hipMemsetAsync(act, 0, n, c->stream));
+    SX_HIP(c, hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+    SX_HIP(c, viewRange(GroupArgs{g->firstBody, g->lastBody, g->numGroups, g->groupStart, g->groupEnd}, act, mm,
+                        c->stream));
+    uint32_t r[2];
+    SX_HIP(c, hipMemcpyAsync(r, mm, sizeof(r), hipMemcpyDeviceToHost, c->stream));
+    SX_HIP(c, hipStreamSynchronize(c->stream));
+    tmp           = *g;
+    tmp.firstBody = r[0] < r[1] ? r[0] : 0u;
+    tmp.lastBody  = r[0] < r[1] ? r[1] : 0u;
+    // a cached neighbor list that covers the view (the step's list over all local targets) is used as it is: its
+    // blocks are laid out from its own first target, the mask restricts the targets to the view
+    if (cachedList && c->nbValid && c->nbLast <= n && tmp.firstBody < tmp.lastBody && c->nbFirst <= tmp.firstBody &&
+        tmp.lastBody <= c->nbLast)
+        tmp.firstBody = c->nbFirst, tmp.lastBody = c->nbLast;
+    g             = &tmp;
+    c->viewActive = act;
+    return SX_OK;
+}
+
 int checkList(sx_ctx* c, const sx_groups* g, const sx_params* p)
 {
     if (g->firstBody >= g->lastBody) return SX_OK; // empty range: zero groups, nothing is launched
@@ -553,12 +599,15 @@ PairArgs pairArgs(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_pa
     a.dV23           = f->dV23;
     a.dV33           = f->dV33;
     a.avClean        = 0;
+    a.active         = c->viewActive;
     return a;
 }
 
 int markRamp(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
              float* markRampOut)
 {
+    sx_groups tmpView;
+    if (int e = resolveView(c, g, tmpView, f->n)) return e;
     if (!markRampOut || !f->kx || !f->xm || !f->m) return fail(c, SX_ERR_ARG, "sx_mark_ramp: bad arguments");
     if (int e = checkList(c, g, p)) return e;
     if (g->firstBody >= g->lastBody) return SX_OK;
@@ -576,6 +625,9 @@ int markRamp(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params*
 int momentumEnergy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_fields* f, const sx_params* p,
                    const sx_box* box, float* minDtCourant, bool avClean)
 {
+    const sx_groups* view = g;
+    sx_groups        tmp;
+    if (int e = resolveView(c, g, tmp, f->n)) return e;
     if (int e = checkList(c, g, p)) return e;
     if (f->tdpdTrho) return fail(c, SX_ERR_ARG, "tdpdTrho != NULL is not supported by the VE momentum kernel");
     if (avClean && !(f->dV11 && f->dV12 && f->dV13 && f->dV22 && f->dV23 && f->dV33))
@@ -588,9 +640,17 @@ int momentumEnergy(sx_ctx* c, const sx_groups* g, float* groupDt, const sx_field
     float huge = 1e10f; // momentum_energy_gpu.cu:127
     SX_HIP(c, hipMemcpyAsync(c->minDt, &huge, 4, hipMemcpyHostToDevice, c->stream));
     PairArgs a = pairArgs(c, g, f, p, box, r);
-    a.groupDt  = groupDt;
-    a.avClean  = avClean ? 1 : 0;
+    // explicit groups: groupDt[k] of view group k = min over its targets (per-target Courant dt, then one minimum
+    // per group); fixed 64-blocks: per block inside the kernel
+    const bool viewGroups = groupDt && view->groupStart && view->numGroups;
+    a.groupDt             = viewGroups ? nullptr : groupDt;
+    a.dtOut               = viewGroups ? c->arena.get<float>("view.dt", f->n) : nullptr;
+    a.avClean             = avClean ? 1 : 0;
     c->hydro().momentumEnergy(a, c->stream);
+    if (viewGroups)
+        SX_HIP(c, groupMin(GroupArgs{view->firstBody, view->lastBody, view->numGroups, view->groupStart,
+                                     view->groupEnd},
+                           a.dtOut, groupDt, c->stream));
     SX_HIP(c, hipGetLastError());
     SX_HIP(c, hipMemcpyAsync(c->hostScalar, c->minDt, 4, hipMemcpyDeviceToHost, c->stream));
     SX_HIP(c, hipStreamSynchronize(c->stream));
@@ -612,7 +672,9 @@ extern "C"
     int sx_xmass(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
                  const sx_tree* tree)
     {
-        int rc = sx_find_neighbors(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n, false)) return e;
+        int rc = findNeighborsView(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
         if (rc != SX_OK) return rc;
         Records r = records(c, f->n);
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
@@ -623,6 +685,8 @@ extern "C"
 
     int sx_xmass_only(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         Records r = records(c, f->n);
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
@@ -633,6 +697,8 @@ extern "C"
 
     int sx_ve_def_gradh(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         Records r = records(c, f->n);
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
@@ -653,6 +719,8 @@ extern "C"
 
     int sx_iad_divv_curlv(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         Records r = records(c, f->n);
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
@@ -666,6 +734,8 @@ extern "C"
     int sx_av_switches(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
                        double minDt)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         Records r = records(c, f->n);
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
@@ -696,14 +766,18 @@ extern "C"
     int sx_density(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box,
                    const sx_tree* tree)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n, false)) return e;
         if (!f->rho) return fail(c, SX_ERR_ARG, "sx_density needs f->rho");
-        int rc = sx_find_neighbors(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
+        int rc = findNeighborsView(c, f, tree, box, p, g->firstBody, g->lastBody, 1, nullptr);
         if (rc != SX_OK) return rc;
         return sx_density_only(c, g, f, p, box);
     }
 
     int sx_density_only(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         if (!f->rho) return fail(c, SX_ERR_ARG, "sx_density needs f->rho");
         Records r = records(c, f->n);
@@ -728,6 +802,8 @@ extern "C"
 
     int sx_iad(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p, const sx_box* box)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         if (!f->rho) return fail(c, SX_ERR_ARG, "sx_iad needs f->rho");
         Records r = records(c, f->n);
@@ -744,6 +820,8 @@ extern "C"
     int sx_momentum_energy_std(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_params* p,
                                const sx_box* box, float* minDtCourant)
     {
+        sx_groups tmpView;
+        if (int e = resolveView(c, g, tmpView, f->n)) return e;
         if (int e = checkList(c, g, p)) return e;
         if (!(f->rho && f->p)) return fail(c, SX_ERR_ARG, "sx_momentum_energy_std needs f->rho and f->p");
         Records r = records(c, f->n);
@@ -876,6 +954,19 @@ extern "C"
         if (!tab) return fail(c, SX_ERR_NOMEM, "powTab");
         c->hydro().updateH(first, last, ng0, nc, h, tab, c->stream);
         SX_HIP(c, hipGetLastError());
+        return SX_OK;
+    }
+
+    int sx_update_h_groups(sx_ctx* c, const sx_groups* g, uint32_t ng0, const uint32_t* nc, float* h)
+    {
+        if (!g || !nc || !h || (g->numGroups && !g->groupStart != !g->groupEnd))
+            return fail(c, SX_ERR_ARG, "sx_update_h_groups: bad arguments");
+        const float* tab = ensurePowTab(c, ng0);
+        if (!tab) return fail(c, SX_ERR_NOMEM, "powTab");
+        const uint32_t ng = g->groupStart ? g->numGroups
+                                          : (g->lastBody > g->firstBody ? (g->lastBody - g->firstBody + 63) / 64 : 0);
+        SX_HIP(c, updateHGroups(GroupArgs{g->firstBody, g->lastBody, ng, g->groupStart, g->groupEnd}, ng0, nc, h, tab,
+                                c->stream));
         return SX_OK;
     }
 

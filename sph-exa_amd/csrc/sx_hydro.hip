@@ -33,7 +33,7 @@ constexpr bool kFastClusters = SX_STR(SX_VARIANT)[0] == 'f';
     const uint32_t gw   = (xcdBlock(blockIdx.x, gridDim.x) * kBlock + threadIdx.x) >> 6;                               \
     const uint32_t lane = threadIdx.x & 63;                                                                            \
     const uint32_t i     = a.first + gw * kGroupSize + lane;                                                           \
-    const bool     valid = gw < a.numGroups && i < a.last; /* no early return: momentum has a block barrier */     \
+    const bool     valid = gw < a.numGroups && i < a.last && (!a.active || a.active[i]); /* no early return: barrier */\
     unsigned       cnt   = 0;                                                                                          \
     if (valid)                                                                                                         \
     {                                                                                                                  \
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyKernel(PairArgs a)
         a.ay[i] = (float)(-a.K * (double)my);
         a.az[i] = (float)(-a.K * (double)mz);
         dt_lane = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+        if (a.dtOut) a.dtOut[i] = dt_lane;
     }
     // wave min -> block min -> one atomic per block (momentum_energy_gpu.cu:94-118)
     float wmin = waveMin(dt_lane);
@@ -575,6 +576,7 @@ __global__ __launch_bounds__(kBlock) void momentumStdKernel(PairArgs a)
         a.ay[i] = (float)(a.K * (double)my);
         a.az[i] = (float)(a.K * (double)mz);
         dt_lane = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+        if (a.dtOut) a.dtOut[i] = dt_lane;
     }
     float wmin = waveMin(dt_lane);
     __shared__ float smin[kBlock / kWave];

@@ -59,6 +59,11 @@ struct PairArgs
     // interior / boundary split that overlaps a halo exchange with the interior clusters, sx_sim.cpp)
     const uint32_t* clusterList;
     uint32_t        listCount;
+    // group views (ve-bdt active rungs): targets with active[i] == 0 are skipped -- not computed, not written, as the
+    // reference's kernels visit only the view's groups; nullable = every target of [first, last)
+    const uint8_t* active;
+    // nullable: each computed target's Courant time-step (momentum kernels), for the per-view-group minimum
+    float* dtOut;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent

@@ -80,7 +80,7 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     cu.gw               = cu.c * kClusterWaves + sub;
     const uint32_t c0   = a.first + cu.c * kCluster;
     cu.i                = c0 + cu.tid;
-    cu.valid            = cu.gw < a.numGroups && cu.i < a.last;
+    cu.valid            = cu.gw < a.numGroups && cu.i < a.last && (!a.active || a.active[cu.i]);
     cu.iSafe            = cu.valid ? cu.i : c0;
     cu.cnt              = 0;
     if (cu.valid)
@@ -802,6 +802,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
         a.ay[cu.i] = (float)(-a.K * (double)my);
         a.az[cu.i] = (float)(-a.K * (double)mz);
         dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+        if (a.dtOut) a.dtOut[cu.i] = dt_lane;
     }
     // wave min -> workgroup min -> one atomic per cluster (momentum_energy_gpu.cu:94-118)
     const float wmin = waveMin(dt_lane);
@@ -917,6 +918,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
         a.ay[cu.i] = (float)(a.K * (double)my);
         a.az[cu.i] = (float)(a.K * (double)mz);
         dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+        if (a.dtOut) a.dtOut[cu.i] = dt_lane;
     }
     const float wmin = waveMin(dt_lane);
     const int   wave = threadIdx.x >> 6;

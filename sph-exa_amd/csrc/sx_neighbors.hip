@@ -101,8 +101,8 @@ findNeighborsKernel(NsArgs a)
     const uint32_t g     = c * kClusterWaves + wave;
     const uint32_t c0    = a.first + c * kCluster;
     const uint32_t i     = c0 + threadIdx.x;
-    const bool     valid = g < a.numGroups && i < a.last;
-    const uint32_t iSafe = valid ? i : c0; // the cluster's first particle is always valid
+    const bool     valid = g < a.numGroups && i < a.last && (!a.active || a.active[i]);
+    const uint32_t iSafe = valid ? i : c0; // positions only: the cluster's first particle is always in range
     const double   xi = a.x[iSafe], yi = a.y[iSafe], zi = a.z[iSafe];
     const double   ox = a.x[c0], oy = a.y[c0], oz = a.z[c0]; // cluster origin of the float prefilter
     float          hi = a.h[iSafe];
@@ -168,8 +168,9 @@ findNeighborsKernel(NsArgs a)
                 const int k = atomicAdd(&s_nreg, 1);
                 if (k < kMaxRegions)
                 {
+                    const double ext = a.extFactor > 1.0 ? a.extFactor : 1.0;
                     s_reg[2 * k]     = make_double4(0.5 * (x0 + x1), 0.5 * (y0 + y1), 0.5 * (z0 + z1),
-                                                2.0 * (double)h * (1.0 + 1e-6) + a.margin);
+                                                2.0 * (double)h * ext * (1.0 + 1e-6) + a.margin);
                     s_reg[2 * k + 1] = make_double4(0.5 * (x1 - x0), 0.5 * (y1 - y0), 0.5 * (z1 - z0), (double)wave);
                 }
             };

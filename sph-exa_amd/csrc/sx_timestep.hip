@@ -177,7 +177,79 @@ __global__ void storeRungKernel(GroupArgs g, uint8_t rung, uint8_t* rungs)
     if (s + lane < e) rungs[s + lane] = rung;
 }
 
+// ---- group views of the pair kernels (ve-bdt active rungs: a slice of the rung-sorted groups) ---------------------
+
+//! marks the targets of the view's groups in active[] and reduces [min start, max end) into mm[0], mm[1]
+//! (mm preset to {UINT32_MAX, 0}); one atomic pair per workgroup
+__global__ void viewRangeKernel(GroupArgs g, uint8_t* active, uint32_t* mm)
+{
+    uint32_t lo = 0xffffffffu, hi = 0;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < g.numGroups; t += gridDim.x * blockDim.x)
+    {
+        uint32_t s, e;
+        groupBounds(g, t, s, e);
+        for (uint32_t i = s; i < e; ++i)
+            active[i] = 1;
+        if (s < e) lo = min(lo, s), hi = max(hi, e);
+    }
+    lo = waveMin(lo), hi = waveMax(hi);
+    __shared__ uint32_t s_lo[4], s_hi[4];
+    if ((threadIdx.x & 63) == 0) s_lo[threadIdx.x >> 6] = lo, s_hi[threadIdx.x >> 6] = hi;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int w = 1; w < 4; ++w)
+            lo = min(lo, s_lo[w]), hi = max(hi, s_hi[w]);
+        atomicMin(mm, lo);
+        atomicMax(mm + 1, hi);
+    }
+}
+
+//! groupDt[t] = min(groupDt[t], min over group t of v) -- the per-group Courant minimum of momentumEnergyGpu
+//! (momentum_energy_gpu.cu:98-104: warpMin of the group's targets into groupDt[targetIdx])
+__global__ void groupMinKernel(GroupArgs g, const float* v, float* groupDt)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t       s, e;
+    if (!groupBounds(g, t, s, e)) return;
+    float m = INFINITY;
+    for (uint32_t i = s; i < e; ++i)
+        m = fminf(m, v[i]);
+    groupDt[t] = fminf(groupDt[t], m);
+}
+
+//! updateSmoothingLengthGpu over the targets of a group view (update_h_gpu.cu:49-60)
+__global__ void updateHGroupsKernel(GroupArgs g, uint32_t ng0, const uint32_t* nc, float* h, const float* powTab)
+{
+    const uint32_t w    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t       s, e;
+    if (!groupBounds(g, w, s, e)) return;
+    for (uint32_t i = s + lane; i < e; i += 64)
+        h[i] = updateH(ng0, nc[i], h[i], powTab);
+}
+
 static unsigned waveGrid(uint32_t numGroups) { return (numGroups + 3) / 4; }
+
+hipError_t viewRange(const GroupArgs& g, uint8_t* active, uint32_t* mm, hipStream_t s)
+{
+    if (g.numGroups)
+        viewRangeKernel<<<(g.numGroups + 255) / 256 < 1024u ? (g.numGroups + 255) / 256 : 1024u, 256, 0, s>>>(g, active, mm);
+    return hipGetLastError();
+}
+
+hipError_t groupMin(const GroupArgs& g, const float* v, float* groupDt, hipStream_t s)
+{
+    if (g.numGroups) groupMinKernel<<<(g.numGroups + 255) / 256, 256, 0, s>>>(g, v, groupDt);
+    return hipGetLastError();
+}
+
+hipError_t updateHGroups(const GroupArgs& g, uint32_t ng0, const uint32_t* nc, float* h, const float* powTab,
+                         hipStream_t s)
+{
+    if (g.numGroups) updateHGroupsKernel<<<waveGrid(g.numGroups), 256, 0, s>>>(g, ng0, nc, h, powTab);
+    return hipGetLastError();
+}
 
 hipError_t rungPositions(const RungPosArgs& a, hipStream_t s)
 {

@@ -45,5 +45,11 @@ hipError_t groupDivvTimestep(float Krho, const GroupArgs& g, const float* divv, 
 hipError_t groupAccTimestep(float etaAcc, const GroupArgs& g, const float* ax, const float* ay, const float* az,
                             float* groupDt, hipStream_t s);
 hipError_t storeRung(const GroupArgs& g, uint8_t rung, uint8_t* rungs, hipStream_t s);
+//! group views of the pair kernels: active[] marks for the view's targets and [min start, max end) into mm
+//! (preset {UINT32_MAX, 0}); per-group minimum of per-target values; h update over the view's targets
+hipError_t viewRange(const GroupArgs& g, uint8_t* active, uint32_t* mm, hipStream_t s);
+hipError_t groupMin(const GroupArgs& g, const float* v, float* groupDt, hipStream_t s);
+hipError_t updateHGroups(const GroupArgs& g, uint32_t ng0, const uint32_t* nc, float* h, const float* powTab,
+                         hipStream_t s);
 
 } // namespace sx

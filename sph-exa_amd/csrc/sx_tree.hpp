@@ -209,10 +209,13 @@ struct NsArgs
     const double*   sizes;
     DevBox          box;
     double          margin; // node-box inflation covering key quantisation round-off
+    double          extFactor; // OctreeNsView::searchExtFactor (findneighbors.hpp:112): tree-node reach radius
+                               // scaled by it (> 1 on ve-bdt substeps: particles drifted out of their cells); 0 = 1
     const float*    powTab; // glibc powf(1 + 1023*ng0/nc, 0.1f) by nc (updateH)
     int             prefilter; // 1: packed f32 distance test in the cluster frame, exact double test only for the
                                // ambiguous chunks; 0: the exact double test for every candidate
     uint32_t*       stats;     // kStatsWords words, see above
+    const uint8_t*  active;    // nullable: targets with active[i] == 0 are skipped (no h iteration, h and nc kept)
     uint4*          clStats;   // per cluster {max count, stored, tested, union}: reduced into stats by one small
                                // kernel after the search (per-wave atomics on the stats words serialised: 10 ms of a
                                // 64M-particle search)

@@ -449,8 +449,8 @@ template<class GroupView, class Th>
 void updateSmoothingLengthGpu(const GroupView& grp, unsigned ng0, const unsigned* nc, Th* h)
 {
     namespace sa = sphexa_amd;
-    sa::check(sx_update_h(sa::context(), (uint32_t)grp.firstBody, (uint32_t)grp.lastBody, ng0, nc, h),
-              "updateSmoothingLengthGpu");
+    const sx_groups g = sa::toGroups(grp);
+    sa::check(sx_update_h_groups(sa::context(), &g, ng0, nc, h), "updateSmoothingLengthGpu");
 }
 
 } // namespace sph

@@ -164,6 +164,7 @@ def lib():
         "sx_positions": (C.c_int, [vp, u32, u32, C.c_double, C.c_double, C.POINTER(SxFields), C.c_double,
                                    C.c_float, C.POINTER(SxBox)]),
         "sx_update_h": (C.c_int, [vp, u32, u32, u32, vp, vp]),
+        "sx_update_h_groups": (C.c_int, [vp, vp, u32, vp, vp]),
         "sx_max_divv": (C.c_int, [vp, u32, u32, vp, C.POINTER(C.c_float)]),
         "sx_sim_create": (C.c_int, [C.POINTER(vp), vp, sz, C.POINTER(SxParams), C.POINTER(SxBox), u32]),
         "sx_sim_destroy": (None, [vp]),
