@@ -48,6 +48,10 @@ namespace sx
 #define SX_NS_GROUP 4
 #endif
 constexpr int kNsGroup = SX_NS_GROUP;
+#ifndef SX_NS_CCAP
+#define SX_NS_CCAP 2048
+#endif
+constexpr int kCCap = SX_NS_CCAP; //!< candidate leaves per cluster (this build's namespace: sx or sx::small)
 
 #ifndef SX_NS_CAND_LOG2
 #define SX_NS_CAND_LOG2 16
@@ -211,7 +215,7 @@ findNeighborsKernel(NsArgs a)
         {
             bool      overflow = false;
             const int nCand    = (a.experiment & 16) ? 0
-                                                     : waveCollectLeaves(
+                                                     : waveCollectLeaves<kCCap>(
                                                         a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; },
                                                         s_queue, s_cand, lane, overflow);
             if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short

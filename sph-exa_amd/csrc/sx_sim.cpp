@@ -321,13 +321,14 @@ __global__ __launch_bounds__(256) void markHalosKernel(const ReqBox* boxes, int 
                                                        unsigned long long* mark, uint32_t* err)
 {
     __shared__ int s_queue[4][kQCap];
+    constexpr int  kCCap = 2048; // candidate leaves per wave of the halo discovery
     __shared__ int s_cand[4][kCCap];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bi   = blockIdx.x * 4 + wave;
     if (bi >= numBoxes) return;
     const ReqBox b = boxes[bi];
     bool         overflow;
-    const int    numCand = waveCollectLeaves(
+    const int    numCand = waveCollectLeaves<kCCap>(
         childOffsets,
         [&](int node) {
             return boxDist2(centers + 3 * (size_t)node, sizes + 3 * (size_t)node, b.c[0], b.c[1], b.c[2],

@@ -15,14 +15,12 @@ namespace sx
 {
 
 constexpr int kQCap = 512;  //!< internal-node ring per wave (power of 2)
-#ifndef SX_NS_CCAP
-#define SX_NS_CCAP 2048
-#endif
-constexpr int kCCap = SX_NS_CCAP; //!< candidate leaves per wave
 
-/*! Collect every leaf node passing `overlaps` (whose ancestors all pass) into cand[0..return).
- *  Sets `overflow` if the queue or the candidate list ran out of space (the caller reports an error). */
-template<class Overlaps>
+/*! Collect every leaf node passing `overlaps` (whose ancestors all pass) into cand[0..return), at most CCap leaves.
+ *  Sets `overflow` if the queue or the candidate list ran out of space (the caller reports an error).  The capacity
+ *  is a template parameter: the search builds (sx_neighbors.hip) and the halo discovery (sx_sim.cpp) size it
+ *  differently, each in its own translation unit. */
+template<int CCap, class Overlaps>
 __device__ __forceinline__ int waveCollectLeaves(const int32_t* __restrict__ childOffsets, Overlaps&& overlaps,
                                                  int* queue, int* cand, int lane, bool& overflow)
 {
@@ -49,7 +47,7 @@ __device__ __forceinline__ int waveCollectLeaves(const int32_t* __restrict__ chi
         if (leaf)
         {
             int pos = numCand + __popcll(bl & ltMask);
-            if (pos < kCCap) cand[pos] = child;
+            if (pos < CCap) cand[pos] = child;
         }
         if (inner) { queue[(qt + __popcll(bi & ltMask)) & (kQCap - 1)] = child; }
         numCand += __popcll(bl);
@@ -58,10 +56,10 @@ __device__ __forceinline__ int waveCollectLeaves(const int32_t* __restrict__ chi
         if (qt - qh > kQCap) overflow = true;
         __builtin_amdgcn_wave_barrier();
     }
-    if (numCand > kCCap)
+    if (numCand > CCap)
     {
         overflow = true;
-        numCand  = kCCap;
+        numCand  = CCap;
     }
     return numCand;
 }
