@@ -145,7 +145,7 @@ __device__ __forceinline__ void combineShares(const Clu& cu, float (&v)[NV], flo
  *  of particle j.  `resident` carries "the whole union is already in LDS" from a previous pass over the same records.
  *  With the union resident the loop is software-pipelined: the LDS records of the next two neighbors (one list
  *  word) are read while the current two are computed, and list words are prefetched four ahead. */
-template<int CH, int SPLIT, class Stage, class Load, class Compute>
+template<int CH, int SPLIT, bool PF = true, class Stage, class Load, class Compute>
 __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&& load, Compute&& compute,
                                              bool& resident)
 {
@@ -169,16 +169,42 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
 
     if (cu.U <= (uint32_t)CH)
     {
+#ifdef SX_PAIR_PROFILE
+        const uint64_t tp0 = __builtin_readcyclecounter();
+#endif
         if (!resident)
         {
             fill(0, cu.U);
             __syncthreads();
             resident = true;
         }
+#ifdef SX_PAIR_PROFILE
+        const uint64_t tp1 = __builtin_readcyclecounter();
+#endif
         const uint32_t wBeg = cu.wBeg, wEnd = cu.wEnd;
+#ifdef SX_PAIR_PROFILE
+        auto profOut = [&]() {
+            const uint64_t t2 = __builtin_readcyclecounter();
+            if (threadIdx.x == 0 && (blockIdx.x % 20000) == 7)
+                printf("pairprof CH %d SPLIT %d U %u fill %llu loop %llu\n", CH, SPLIT, cu.U,
+                       (unsigned long long)(tp1 - tp0), (unsigned long long)(t2 - tp1));
+        };
+        if (wBeg >= wEnd) return profOut();
+#else
         if (wBeg >= wEnd) return;
+#endif
         const uint32_t* nl = cu.nl;
-        auto            ld = [&](uint32_t w) { return w < wEnd ? nl[(size_t)w * kWave] : 0u; };
+        // PF: list words beyond the share read the share's last word again (always in bounds) and every prefetch
+        // below is unconditional, so the LDS reads of the next pair are issued on one path and the wait before a
+        // computation covers only the records it consumes (a masked prefetch leaves a path on which the previous
+        // pair's reads may still be outstanding, and the merged wait then also waits for the new reads).  Measured
+        // (Sedov 64M): IAD -0.4 ms, AV -0.3 ms; momentum +0.3..0.7 ms (its records are 80 B: the extra registers of
+        // the unmasked form cost more than the wait), so momentum keeps the masked form.
+        const uint32_t  wLast = wEnd - 1;
+        auto            ld    = [&](uint32_t w) {
+            if constexpr (PF) return nl[(size_t)min(w, wLast) * kWave];
+            else return w < wEnd ? nl[(size_t)w * kWave] : 0u;
+        };
         // two record buffers used alternately (2x unrolled, no register copies); list words prefetched ahead
         uint32_t        q0 = ld(wBeg + 1), q1 = ld(wBeg + 2), q2 = ld(wBeg + 3);
         const uint32_t  w0 = nl[(size_t)wBeg * kWave];
@@ -188,7 +214,7 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
         uint32_t        w = wBeg;
         while (true)
         {
-            if (w + 1 < wEnd)
+            if (PF || w + 1 < wEnd) // past the share's end (PF): a valid slot that is never computed
             {
                 a1 = load(q0 & 0xffffu);
                 b1 = load(q0 >> 16);
@@ -197,7 +223,7 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             compute(a0);
             if (2 * w + 1 < cu.cnt) compute(b0);
             if (++w >= wEnd) break;
-            if (w + 1 < wEnd)
+            if (PF || w + 1 < wEnd)
             {
                 a0 = load(q1 & 0xffffu);
                 b0 = load(q1 >> 16);
@@ -209,6 +235,9 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             const uint32_t t = q0;
             q0 = q2, q2 = q1, q1 = t;
         }
+#ifdef SX_PAIR_PROFILE
+        profOut();
+#endif
     }
     else
     {
@@ -467,7 +496,8 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
     __shared__ float4 sP[CH]; // x, y, z, vol = xm/kx
     __shared__ float4 sV[CH]; // vx, vy, vz, xm
     __shared__ float  s_red[kClusterWaves * SPLIT];
-    __shared__ float  s_scr[SPLIT > 1 ? 6 * SPLIT * kCluster : 1];
+    static_assert(SPLIT == 1 || (6 * SPLIT * kCluster <= 4 * CH && 9 * SPLIT * kCluster <= 4 * CH),
+                  "the share sums are combined in the record arrays");
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
@@ -511,11 +541,12 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
         },
         res);
     {
+        // tau shares in sP's space, M shares in sV's (both read only by the neighbor loop, done at the first sync)
         float v[6] = {t11, t12, t13, t22, t23, t33};
-        combineShares<SPLIT>(cu, v, s_scr);
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 0u, true);
         t11 = v[0], t12 = v[1], t13 = v[2], t22 = v[3], t23 = v[4], t33 = v[5];
         float w[9] = {M[0][0], M[0][1], M[0][2], M[1][0], M[1][1], M[1][2], M[2][0], M[2][1], M[2][2]};
-        combineShares<SPLIT>(cu, w, reinterpret_cast<float*>(sP), 0u, true);
+        combineShares<SPLIT>(cu, w, reinterpret_cast<float*>(sV));
 #pragma unroll
         for (int k = 0; k < 9; ++k)
             M[k / 3][k % 3] = w[k];
@@ -701,7 +732,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
         gradV_i[3] = a.dV22[q], gradV_i[4] = a.dV23[q], gradV_i[5] = a.dV33[q];
         eta_crit   = avEtaCrit(cu.cnt);
     }
-    neighborLoop<CH, SPLIT>(
+    neighborLoop<CH, SPLIT, false>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r   = a.rx[j];
@@ -856,7 +887,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
     float maxvsignali = 0.0f;
     float mx = 0, my = 0, mz = 0, energy = 0;
     bool  res = false;
-    neighborLoop<CH, SPLIT>(
+    neighborLoop<CH, SPLIT, false>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r  = a.rx[j];
@@ -960,7 +991,13 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #define SX_SPLIT_ME_AVC 2 // the avClean variant needs 190 VGPRs: two waves per SIMD
 #endif
 // kChVd = 2000: 40 KB of records, four VeDefGradh workgroups per CU (eight waves per SIMD)
-constexpr int kChXm = 2048, kChVd = 2000, kChIad = 1900, kChAv = 2048, kChMe = SX_CH_ME, kChMeAvc = 1536;
+#ifndef SX_CH_IAD
+#define SX_CH_IAD 1700 // 54 KB: three IAD workgroups per CU (24 waves at 79 VGPRs; 2 at CH 1900: 10.3 -> 9.4 ms at 64M)
+#endif
+#ifndef SX_CH_AV
+#define SX_CH_AV 2048
+#endif
+constexpr int kChXm = 2048, kChVd = 2000, kChIad = SX_CH_IAD, kChAv = SX_CH_AV, kChMe = SX_CH_ME, kChMeAvc = 1536;
 
 static inline unsigned clusters(const PairArgs& a)
 {
