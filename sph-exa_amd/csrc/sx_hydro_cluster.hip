@@ -992,7 +992,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #endif
 // kChVd = 2000: 40 KB of records, four VeDefGradh workgroups per CU (eight waves per SIMD)
 #ifndef SX_CH_IAD
-#define SX_CH_IAD 1700 // 54 KB: three IAD workgroups per CU (24 waves at 79 VGPRs; 2 at CH 1900: 10.3 -> 9.4 ms at 64M)
+#define SX_CH_IAD 1660 // 53 KB: three IAD workgroups per CU (24 waves at 79 VGPRs; 2 at CH 1900: 10.3 -> 9.4 ms at 64M)
 #endif
 #ifndef SX_CH_AV
 #define SX_CH_AV 2048
