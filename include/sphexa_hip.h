@@ -33,6 +33,10 @@
  *   sx_group_divv_timestep sph::groupDivvTimestepGpu            sph_gpu.hpp:80, ts_groups.cu:17-46
  *   sx_group_acc_timestep  sph::groupAccTimestepGpu             sph_gpu.hpp:83, ts_groups.cu:48-81
  *   sx_store_rung          sph::storeRungGpu                    sph_gpu.hpp:86, ts_groups.cu:84-108
+ *   sx_rung_timestep       sph::rungTimestep                    sph/include/sph/ts_rungs.hpp:132-145 (sortGroupDt :67-78,
+ *                                                               computeMinTimestep :89-105, findRungRanges :116-130)
+ *   sx_minimum_group_dt    sph::minimumGroupDt                  ts_rungs.hpp:147-157
+ *   sx_extract_groups      sph::extractGroupGpu                 sph/include/sph/groups.hpp:31-48
  *   sx_update_h            sph::updateSmoothingLengthGpu        sph_gpu.hpp:78, update_h_gpu.cu:49-60
  *   sx_max_divv            cstone::MinMaxGpu (rhoTimestep)      sph/ts_global.hpp:72-94
  *   sx_sim_*               one HydroVeProp step (sync + computeForces + integrate), main/src/propagator/ve_hydro.hpp:132-218
@@ -345,6 +349,32 @@ int  sx_comm_unique_id(void* id128);
 int  sx_comm_create_rccl(sx_comm** comm, int rank, int size, const void* id128);
 int  sx_comm_create_host(sx_comm** comm, int rank, int size, sx_alltoallv_cb a2a, sx_allreduce_cb ar, void* user);
 void sx_comm_destroy(sx_comm* comm);
+
+/* ---- block time-step host bookkeeping (HydroVeBdtProp::computeRungs, ve_hydro_bdt.hpp:292-331) ---------------- */
+/*! sph::Timestep (sph/timestep.h:38-48) */
+typedef struct sx_timestep
+{
+    float    nextDt, elapsedDt, totDt;
+    int      numRungs, substep;
+    uint32_t rungRanges[SX_MAX_RUNGS + 1];
+    float    dt_m1[SX_MAX_RUNGS], dt_drift[SX_MAX_RUNGS];
+} sx_timestep;
+/*! rungTimestep (ts_rungs.hpp:132-145): sorts groupDt[0, numGroups) ascending in place with groupIndices (the group
+ *  of each sorted entry), min-reduces {groupDt[0], groupDt[(uint32_t)(0.4f * numGroups)]} over comm's ranks
+ *  (comm NULL: this rank only), numRungs = min(int(log2(dt40 / dtMin)) + 1, SX_MAX_RUNGS), rungRanges by lower bound
+ *  of 2^r dtMin, nextDt = min(maxDt, dtMin), totDt = nextDt 2^numRungs; elapsedDt, substep, dt_m1, dt_drift = 0.
+ *  numGroups >= 1.  Synchronises the context stream (the results are host values, as in the reference). */
+int sx_rung_timestep(sx_ctx* ctx, float* groupDt, uint32_t* groupIndices, uint32_t numGroups, float maxDt,
+                     sx_comm* comm, sx_timestep* out);
+/*! minimumGroupDt (ts_rungs.hpp:147-157) for the numGroups active groups of substep ts->substep: sorts them as
+ *  above, groupIndices[numGroups, ts->rungRanges[SX_MAX_RUNGS]) = the identity; *dt = min(dtMin, (totDt -
+ *  elapsedDt) / substeps left), rungRanges over all SX_MAX_RUNGS rungs.  Synchronises the context stream. */
+int sx_minimum_group_dt(sx_ctx* ctx, const sx_timestep* ts, float* groupDt, uint32_t* groupIndices, uint32_t numGroups,
+                        sx_comm* comm, float* dt, uint32_t* rungRanges);
+/*! extractGroupGpu (groups.hpp:31-48): group k of the output = group indices[first + k] of grp, k < last - first
+ *  (device arrays outStart/outEnd; the view they form has firstBody = lastBody = 0) */
+int sx_extract_groups(sx_ctx* ctx, const sx_groups* grp, const uint32_t* indices, uint32_t first, uint32_t last,
+                      uint32_t* outStart, uint32_t* outEnd);
 
 /* ---- host-side decisions of the SFC domain decomposition (sph-exa_amd/csrc/sx_domain.cpp) -------------- */
 /*! equal-count SFC splitters from the all-reduced histogram of 2^histBits key bins (bin = key >> (63-histBits)):

@@ -493,3 +493,63 @@ def conserved_quantities(st, first=0, last=None, mui=np.float32(10.0), gamma=5.0
     lin = np.sum(m[:, None] * V, 0)
     ang = np.sum(m[:, None] * np.cross(X, V), 0)
     return ekin, eint, lin, ang, int(np.sum(st.nc[s].astype(np.int64)))
+
+
+# ---- block time-step rung bookkeeping (numpy restatement of sph/include/sph/ts_rungs.hpp) -----------------------
+# ts_rungs.hpp includes <mpi.h>, which this image lacks, so oracle/_ref cannot compile it: this restatement is pinned
+# by the reference text (cited per line) and by hand-checked cases in tests/test_rungs_oracle.py, not by the
+# reference binary.
+MAX_NUM_RUNGS = 4  # sph::Timestep::maxNumRungs (sph/timestep.h:42)
+
+
+def sort_group_dt(group_dt, num_groups, num_groups_tot):
+    """sortGroupDt (ts_rungs.hpp:67-78) + the index sequence of computeMinTimestep (:97-98): a stable sort of
+    groupDt[0, numGroups) by value (thrust sort_by_key on the identity), indices numGroups.. past it"""
+    dt = np.asarray(group_dt, np.float32).copy()
+    order = np.argsort(dt[:num_groups], kind="stable").astype(np.uint32)
+    dt[:num_groups] = dt[:num_groups][order]
+    idx = np.concatenate([order, np.arange(num_groups, num_groups_tot, dtype=np.uint32)])
+    return dt, idx
+
+
+def min_timestep(group_dt, num_groups, num_groups_tot):
+    """computeMinTimestep (ts_rungs.hpp:89-105), one rank: sorted dt, indices, {dt[0], dt[LocalIndex(0.4f n)]}"""
+    dt, idx = sort_group_dt(group_dt, num_groups, num_groups_tot)
+    k = int(np.float32(0.4) * np.float32(num_groups))  # float fastFraction * LocalIndex, truncated (:85)
+    return dt, idx, (dt[0], dt[k])
+
+
+def find_rung_ranges(min_dt, dt_sorted, num_groups, num_rungs):
+    """findRungRanges (ts_rungs.hpp:116-130): [0, lower_bound(2^r minDt) for 0 < r < numRungs, numGroups ...]"""
+    rr = [0] + [num_groups] * MAX_NUM_RUNGS
+    for r in range(1, num_rungs):
+        max_dt_rung = np.float32(np.float32(1 << r) * np.float32(min_dt))  # (1 << rung) * minDt in float
+        rr[r] = int(np.searchsorted(dt_sorted[:num_groups], max_dt_rung, side="left"))
+    return rr
+
+
+def rung_timestep(group_dt, num_groups, max_dt):
+    """rungTimestep (ts_rungs.hpp:132-145) -> (sorted dt, indices, Timestep as a dict)"""
+    dt, idx, (d0, d1) = min_timestep(group_dt, num_groups, num_groups)
+    # unqualified log2 of a float quotient in namespace sph: ::log2(double)
+    num_rungs = min(int(math.log2(float(np.float32(d1 / d0)))) + 1, MAX_NUM_RUNGS)
+    rr = find_rung_ranges(d0, dt, num_groups, num_rungs)
+    d0 = min(np.float32(max_dt), d0)
+    ts = dict(nextDt=np.float32(d0), elapsedDt=np.float32(0), totDt=np.float32(d0 * np.float32(1 << num_rungs)),
+              numRungs=num_rungs, substep=0, rungRanges=rr)
+    return dt, idx, ts
+
+
+def minimum_group_dt(ts, group_dt, num_groups):
+    """minimumGroupDt (ts_rungs.hpp:147-157) -> (sorted dt, indices, dt, rungRanges)"""
+    dt, idx, (d0, _) = min_timestep(group_dt, num_groups, ts["rungRanges"][MAX_NUM_RUNGS])
+    rr = find_rung_ranges(d0, dt, num_groups, MAX_NUM_RUNGS)
+    time_left = np.float32(np.float32(ts["totDt"]) - np.float32(ts["elapsedDt"]))
+    substeps_left = (1 << ts["numRungs"]) - ts["substep"]
+    return dt, idx, min(d0, np.float32(time_left / np.float32(substeps_left))), rr
+
+
+def extract_groups(group_start, group_end, indices, first, last):
+    """extractGroupGpu (sph/groups.hpp:31-48)"""
+    sel = np.asarray(indices[first:last], np.int64)
+    return np.asarray(group_start)[sel].astype(np.uint32), np.asarray(group_end)[sel].astype(np.uint32)

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/sphexa_hip.h"
+#include "sx_comm.hpp"
 #include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
 #include "sx_kernel_poly.hpp"
@@ -945,6 +946,93 @@ extern "C"
     {
         if (!groupsOk(g) || (g->numGroups && !rungs)) return fail(c, SX_ERR_ARG, "sx_store_rung: bad arguments");
         SX_HIP(c, storeRung(toGroups(g), rung, rungs, c->stream));
+        return SX_OK;
+    }
+
+    // ---- rung bookkeeping (ts_rungs.hpp:67-157): device sort and lower bounds, host decisions -------------------
+
+    sx::Transport* sx_comm_transport_internal(sx_comm* c);
+
+    //! computeMinTimestep (ts_rungs.hpp:89-105): sortGroupDt, the index sequence up to numGroupsTot, the minimum and
+    //! the fast-fraction time-step {groupDt[0], groupDt[LocalIndex(0.4f * numGroups)]}, min-reduced over the ranks
+    static int computeMinTimestep(sx_ctx* c, float* groupDt, uint32_t* groupIndices, uint32_t numGroups,
+                                  uint32_t numGroupsTot, sx_comm* comm, float out[2])
+    {
+        RungScratch sc{};
+        sc.keys     = c->arena.get<float>("rung.keys", numGroups);
+        sc.vals     = c->arena.get<uint32_t>("rung.vals", numGroups);
+        sc.tmpBytes = sortGroupDtTmpBytes(numGroups);
+        sc.tmp      = c->arena.get<char>("rung.tmp", std::max<size_t>(1, sc.tmpBytes));
+        double* d   = c->arena.get<double>("rung.mins", 2);
+        if (!sc.keys || !sc.vals || !sc.tmp || !d) return fail(c, SX_ERR_NOMEM, "rung scratch");
+        SX_HIP(c, sortGroupDt(groupDt, groupIndices, numGroups, numGroupsTot, sc, c->stream));
+        const float    fastFraction = 0.4f;
+        const uint32_t kFast        = (uint32_t)(fastFraction * (float)numGroups);
+        SX_HIP(c, pickDt(groupDt, kFast, d, c->stream));
+        if (sx::Transport* t = sx_comm_transport_internal(comm); t && t->size() > 1)
+            if (!t->allreduceMinF64(d, 2, c->stream)) return fail(c, SX_ERR_HIP, "rung time-step: allreduce failed");
+        double h[2];
+        SX_HIP(c, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        out[0] = (float)h[0], out[1] = (float)h[1];
+        return SX_OK;
+    }
+
+    //! findRungRanges (ts_rungs.hpp:116-130) on the sorted groupDt
+    static int findRungRanges(sx_ctx* c, float minDt, const float* groupDt, uint32_t numGroups, int numRungs,
+                              uint32_t* out)
+    {
+        uint32_t* d = c->arena.get<uint32_t>("rung.ranges", kMaxNumRungs + 1);
+        if (!d) return fail(c, SX_ERR_NOMEM, "rung ranges");
+        SX_HIP(c, rungRanges(groupDt, numGroups, minDt, numRungs, d, c->stream));
+        SX_HIP(c, hipMemcpyAsync(out, d, 4 * (kMaxNumRungs + 1), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        return SX_OK;
+    }
+
+    int sx_rung_timestep(sx_ctx* c, float* groupDt, uint32_t* groupIndices, uint32_t numGroups, float maxDt,
+                         sx_comm* comm, sx_timestep* out)
+    {
+        if (!groupDt || !groupIndices || !out || numGroups == 0)
+            return fail(c, SX_ERR_ARG, "sx_rung_timestep: bad arguments");
+        float mins[2];
+        if (int e = computeMinTimestep(c, groupDt, groupIndices, numGroups, numGroups, comm, mins)) return e;
+        // the reference's unqualified log2 on a float quotient inside namespace sph is ::log2(double)
+        const int numRungs = std::min(int(::log2(mins[1] / mins[0])) + 1, kMaxNumRungs);
+        sx_timestep ts{};
+        if (int e = findRungRanges(c, mins[0], groupDt, numGroups, numRungs, ts.rungRanges)) return e;
+        mins[0]      = std::min(maxDt, mins[0]);
+        ts.nextDt    = mins[0];
+        ts.totDt     = mins[0] * (float)(1 << numRungs);
+        ts.numRungs  = numRungs;
+        ts.elapsedDt = 0.0f;
+        ts.substep   = 0;
+        *out         = ts;
+        return SX_OK;
+    }
+
+    int sx_minimum_group_dt(sx_ctx* c, const sx_timestep* ts, float* groupDt, uint32_t* groupIndices,
+                            uint32_t numGroups, sx_comm* comm, float* dt, uint32_t* ranges)
+    {
+        if (!ts || !groupDt || !groupIndices || !dt || !ranges || numGroups == 0 ||
+            numGroups > ts->rungRanges[kMaxNumRungs])
+            return fail(c, SX_ERR_ARG, "sx_minimum_group_dt: bad arguments");
+        float mins[2];
+        if (int e = computeMinTimestep(c, groupDt, groupIndices, numGroups, ts->rungRanges[kMaxNumRungs], comm, mins))
+            return e;
+        if (int e = findRungRanges(c, mins[0], groupDt, numGroups, kMaxNumRungs, ranges)) return e;
+        const float timeLeft     = ts->totDt - ts->elapsedDt;
+        const int   substepsLeft = (1 << ts->numRungs) - ts->substep;
+        *dt                      = std::min(mins[0], timeLeft / (float)substepsLeft);
+        return SX_OK;
+    }
+
+    int sx_extract_groups(sx_ctx* c, const sx_groups* g, const uint32_t* indices, uint32_t first, uint32_t last,
+                          uint32_t* outStart, uint32_t* outEnd)
+    {
+        if (!groupsOk(g) || last < first || (last > first && (!indices || !outStart || !outEnd)))
+            return fail(c, SX_ERR_ARG, "sx_extract_groups: bad arguments");
+        SX_HIP(c, extractGroups(toGroups(g), indices, first, last, outStart, outEnd, c->stream));
         return SX_OK;
     }
 

@@ -3,13 +3,17 @@
  *        update and the drift of inactive rungs.  Compiled -ffp-contract=off: the formulas round exactly like the
  *        reference's (positions.hpp:54-88 energyUpdate / positionUpdate, eos.hpp:13-18 idealGasCv).
  *
- * Replaces sph/include/sph/ts_groups.cu:17-108 (groupDivvTimestepGpu, groupAccTimestepGpu, storeRungGpu) and
- * sph/include/sph/positions_gpu.cu:45-179 (driftPositionsGpu, computePositionsGpu with dt_m1 per rung).
+ * Replaces sph/include/sph/ts_groups.cu:17-108 (groupDivvTimestepGpu, groupAccTimestepGpu, storeRungGpu),
+ * sph/include/sph/positions_gpu.cu:45-179 (driftPositionsGpu, computePositionsGpu with dt_m1 per rung) and the device
+ * work of the rung bookkeeping in sph/include/sph/ts_rungs.hpp:67-157 (sortGroupDt, the fast-fraction pick,
+ * findRungRanges' lower bounds) and sph/include/sph/groups.hpp:31-48 (extractGroupGpu).
  *
  * Target groups: one wavefront per group (the reference's warp on AMD, 64 lanes), groups given as
  * [groupStart[g], groupEnd[g]) (computeSpatialGroups / sliced rung views) or, with groupStart == nullptr, the
  * fixed 64-particle blocks of [first, last).
  */
+#include <hipcub/hipcub.hpp>
+
 #include "sx_timestep.hpp"
 
 namespace sx
@@ -279,6 +283,108 @@ hipError_t groupAccTimestep(float etaAcc, const GroupArgs& g, const float* ax, c
 hipError_t storeRung(const GroupArgs& g, uint8_t rung, uint8_t* rungs, hipStream_t s)
 {
     if (g.numGroups) storeRungKernel<<<waveGrid(g.numGroups), 256, 0, s>>>(g, rung, rungs);
+    return hipGetLastError();
+}
+
+// ---- rung bookkeeping (ts_rungs.hpp:67-157, groups.hpp:31-48) ----------------------------------------------------
+
+__global__ void sequenceKernel(uint32_t* v, uint32_t n, uint32_t start)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = start + i;
+}
+
+hipError_t sortGroupDt(float* groupDt, uint32_t* groupIndices, uint32_t numGroups, uint32_t numGroupsTot,
+                       RungScratch& sc, hipStream_t s)
+{
+    if (numGroups)
+    {
+        sequenceKernel<<<(numGroups + 255) / 256, 256, 0, s>>>(groupIndices, numGroups, 0u);
+        size_t bytes = 0;
+        hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, groupDt, sc.keys, groupIndices, sc.vals, (int)numGroups, 0,
+                                           32, s);
+        if (bytes > sc.tmpBytes) return hipErrorOutOfMemory;
+        if (hipError_t e = hipcub::DeviceRadixSort::SortPairs(sc.tmp, bytes, groupDt, sc.keys, groupIndices, sc.vals,
+                                                              (int)numGroups, 0, 32, s))
+            return e;
+        if (hipError_t e = hipMemcpyAsync(groupDt, sc.keys, 4ull * numGroups, hipMemcpyDeviceToDevice, s)) return e;
+        if (hipError_t e = hipMemcpyAsync(groupIndices, sc.vals, 4ull * numGroups, hipMemcpyDeviceToDevice, s))
+            return e;
+    }
+    if (numGroupsTot > numGroups)
+        sequenceKernel<<<(numGroupsTot - numGroups + 255) / 256, 256, 0, s>>>(groupIndices + numGroups,
+                                                                            numGroupsTot - numGroups, numGroups);
+    return hipGetLastError();
+}
+
+size_t sortGroupDtTmpBytes(uint32_t numGroups)
+{
+    size_t bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (float*)nullptr, (float*)nullptr, (uint32_t*)nullptr,
+                                       (uint32_t*)nullptr, (int)numGroups, 0, 32);
+    return bytes;
+}
+
+//! {groupDt[0], groupDt[k]} as doubles (the values the reference copies to the host, then min-reduces over ranks)
+__global__ void pickDtKernel(const float* groupDt, uint32_t k, double* out)
+{
+    if (threadIdx.x == 0) out[0] = groupDt[0], out[1] = groupDt[k];
+}
+
+hipError_t pickDt(const float* groupDt, uint32_t k, double* out, hipStream_t s)
+{
+    pickDtKernel<<<1, 64, 0, s>>>(groupDt, k, out);
+    return hipGetLastError();
+}
+
+//! findRungRanges (ts_rungs.hpp:116-130): out[0] = 0, out[r] = lower_bound((1 << r) * minDt) for 0 < r < numRungs,
+//! numGroups for the others
+__global__ void rungRangesKernel(const float* groupDt, uint32_t numGroups, float minDt, int numRungs, uint32_t* out)
+{
+    const int r = threadIdx.x;
+    if (r > kMaxNumRungs) return;
+    uint32_t v = r == 0 ? 0u : numGroups;
+    if (r >= 1 && r < numRungs)
+    {
+        const float maxDtRung = (float)(1 << r) * minDt;
+        uint32_t    lo = 0, hi = numGroups;
+        while (lo < hi)
+        {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (groupDt[mid] < maxDtRung) lo = mid + 1;
+            else hi = mid;
+        }
+        v = lo;
+    }
+    out[r] = v;
+}
+
+hipError_t rungRanges(const float* groupDt, uint32_t numGroups, float minDt, int numRungs, uint32_t* out,
+                      hipStream_t s)
+{
+    rungRangesKernel<<<1, 64, 0, s>>>(groupDt, numGroups, minDt, numRungs, out);
+    return hipGetLastError();
+}
+
+//! extractGroupGpu (groups.hpp:31-48): out group k = group indices[first + k] of grp
+__global__ void extractGroupsKernel(GroupArgs g, const uint32_t* indices, uint32_t first, uint32_t n, uint32_t* outStart,
+                                    uint32_t* outEnd)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t j = indices[first + k];
+    uint32_t       s = 0, e = 0;
+    groupBounds(g, j, s, e);
+    outStart[k] = s;
+    outEnd[k]   = e;
+}
+
+hipError_t extractGroups(const GroupArgs& g, const uint32_t* indices, uint32_t first, uint32_t last,
+                         uint32_t* outStart, uint32_t* outEnd, hipStream_t s)
+{
+    if (last > first)
+        extractGroupsKernel<<<(last - first + 255) / 256, 256, 0, s>>>(g, indices, first, last - first, outStart,
+                                                                       outEnd);
     return hipGetLastError();
 }
 

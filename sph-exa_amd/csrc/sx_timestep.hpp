@@ -52,4 +52,22 @@ hipError_t groupMin(const GroupArgs& g, const float* v, float* groupDt, hipStrea
 hipError_t updateHGroups(const GroupArgs& g, uint32_t ng0, const uint32_t* nc, float* h, const float* powTab,
                          hipStream_t s);
 
+//! rung bookkeeping (ts_rungs.hpp:67-157): sort buffers of numGroups keys / values and the radix-sort temp storage
+struct RungScratch
+{
+    float*    keys;
+    uint32_t* vals;
+    void*     tmp;
+    size_t    tmpBytes;
+};
+size_t     sortGroupDtTmpBytes(uint32_t numGroups);
+//! sortGroupDt (ts_rungs.hpp:67-78) + the index sequence past numGroups (computeMinTimestep, :98)
+hipError_t sortGroupDt(float* groupDt, uint32_t* groupIndices, uint32_t numGroups, uint32_t numGroupsTot,
+                       RungScratch& sc, hipStream_t s);
+hipError_t pickDt(const float* groupDt, uint32_t k, double* out, hipStream_t s);
+hipError_t rungRanges(const float* groupDt, uint32_t numGroups, float minDt, int numRungs, uint32_t* out,
+                      hipStream_t s);
+hipError_t extractGroups(const GroupArgs& g, const uint32_t* indices, uint32_t first, uint32_t last,
+                         uint32_t* outStart, uint32_t* outEnd, hipStream_t s);
+
 } // namespace sx

@@ -60,6 +60,13 @@ class SxGroups(C.Structure):
                 ("groupStart", _P), ("groupEnd", _P)]
 
 
+class SxTimestep(C.Structure):
+    """sph::Timestep (sph/timestep.h:38-48)"""
+    _fields_ = [("nextDt", C.c_float), ("elapsedDt", C.c_float), ("totDt", C.c_float), ("numRungs", C.c_int),
+                ("substep", C.c_int), ("rungRanges", C.c_uint32 * 5), ("dt_m1", C.c_float * 4),
+                ("dt_drift", C.c_float * 4)]
+
+
 class SxOctree(C.Structure):
     _fields_ = [("prefixes", _P), ("childOffsets", _P), ("parents", _P), ("levelRange", _P),
                 ("internalToLeaf", _P), ("leafToInternal", _P)]
@@ -132,6 +139,9 @@ def lib():
         "sx_group_divv_timestep": (C.c_int, [vp, C.c_float, C.POINTER(SxGroups), vp, vp]),
         "sx_group_acc_timestep": (C.c_int, [vp, C.c_float, C.POINTER(SxGroups), vp, vp, vp, vp]),
         "sx_store_rung": (C.c_int, [vp, C.POINTER(SxGroups), C.c_uint8, vp]),
+        "sx_rung_timestep": (C.c_int, [vp, vp, vp, u32, C.c_float, vp, C.POINTER(SxTimestep)]),
+        "sx_minimum_group_dt": (C.c_int, [vp, C.POINTER(SxTimestep), vp, vp, u32, vp, C.POINTER(C.c_float), vp]),
+        "sx_extract_groups": (C.c_int, [vp, C.POINTER(SxGroups), vp, u32, u32, vp, vp]),
         "sx_spatial_groups": (C.c_int, [vp, u32, u32, vp, vp, vp, C.POINTER(SxTree), C.POINTER(SxBox), C.c_float,
                                         vp, u32, C.POINTER(SxGroups)]),
         "sx_find_neighbors": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.POINTER(SxBox),
