@@ -148,7 +148,17 @@ class BdtOracle:
         st.nc[act] = nc[act]
         self.rows, self.act = rows, act
         nbr = lists(self, act, rows) if lists is not None else None
-        if nbr is None:
+        if nbr is not None:
+            # the kernels below run over every target and keep only the active ones; an external list holds
+            # whatever an earlier search left for inactive targets (indices possibly beyond n), so those rows get
+            # the oracle's own in-range rows before the C oracle reads them
+            nbr = nbr.copy()
+            m = nbr.reshape(-1, self.ngmax)
+            for i in np.nonzero(~act)[0]:
+                r = rows[i]
+                m[i] = 0
+                m[i, :r.size] = r
+        else:
             nbr = np.zeros(self.n * self.ngmax, np.uint32)
             for i in np.nonzero(act)[0]:
                 r = rows[i]

@@ -88,8 +88,8 @@ def compare(prop, orc, names, what):
         assert np.array_equal(g, r.astype(g.dtype)), (what, k, int(np.sum(g != r)))
 
 
-@pytest.mark.parametrize("ic,side,substeps", [("sedov", 14, 12), ("noh", 14, 10)])
-def test_ve_bdt_cycle_exact_bitwise(ctx, ic, side, substeps):
+@pytest.mark.parametrize("ic,side,substeps,min_rungs", [("sedov", 14, 12, 3), ("noh", 14, 10, 2)])
+def test_ve_bdt_cycle_exact_bitwise(ctx, ic, side, substeps, min_rungs):
     ora = po.load_oracle()
     st, obox = initial(ic, side, ora)
     host = {k: st.arrays[k].copy() for k in CONS}
@@ -120,7 +120,7 @@ def test_ve_bdt_cycle_exact_bitwise(ctx, ic, side, substeps):
             assert np.array_equal(np.array(ts.dt_m1[:], np.float32), orc.ts["dt_m1"])
             assert np.array_equal(np.array(ts.dt_drift[:], np.float32), orc.ts["dt_drift"])
         assert partial > 0, "no partial substep ran: the hierarchy had a single rung"
-        assert max(e["numRungs"] for e in prop.log) >= 3
+        assert max(e["numRungs"] for e in prop.log) >= min_rungs  # Noh 14^3 (1472 particles): two rungs
     finally:
         ctx.set_exact(False)
         ctx.free_all()
