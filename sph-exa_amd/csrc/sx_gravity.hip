@@ -220,12 +220,29 @@ __device__ __forceinline__ void m2pRec(float (&acc)[4], float tx, float ty, floa
     acc[3] += fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+//! sum over the four 16-lane rows, in every lane: (r0 + r1) + (r2 + r3) by the gfx950 row-swap permutes (VALU, no
+//! LDS crossbar round trip like __shfl_xor's ds_bpermute); the same sums in the same order as two xor shuffles
+__device__ __forceinline__ float rowSum4(float v)
+{
+    const unsigned u = __float_as_uint(v);
+    const auto     p = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    const float    a = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    const unsigned w = __float_as_uint(a);
+    const auto     q = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 struct __attribute__((aligned(16))) GSrc
 {
     double x, y, z;
     float  m, h;
 };
 
+#ifndef SX_GRAV_PAIR_P2P
+#define SX_GRAV_PAIR_P2P 1 // fast P2P: two sources per lane per iteration in packed FP32
+#endif
 #ifndef SX_GRAV_WPE
 #define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
 #endif
@@ -254,7 +271,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     __shared__ int  s_p2p[4][kGList];
     __shared__ GSrc   s_src[FAST ? 1 : 4][kWave];
     __shared__ float4 s_srcF[FAST ? 4 : 1][2][kWave]; // fast P2P: source x, y, z relative to the wave origin, m
-    __shared__ float  s_hF[FAST ? 4 : 1][2][kWave];
+    __shared__ __attribute__((aligned(16))) float s_hF[FAST ? 4 : 1][2][kWave];
+    __shared__ float4  s_tgt[4][kWave]; // the wave's targets relative to its origin, h
     __shared__ uint8_t s_idx[FAST ? 4 : 1][kWave]; // fast M2P: one quarter's accepted entries of the window
     __shared__ uint2   s_rng[FAST ? 4 : 1][FAST ? kGList : 1]; // fast P2P: particle range of each listed leaf
 
@@ -330,21 +348,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     // Per quarter the lanes fetch that quarter's targets (qx..qh), sum into fq, and the four partial sums of a target
     // are added across subs into the target's own lane (sub == qq), which accumulates fo and, per flush, acc.
     const int sub = lane >> 4, tq = lane & 15;
+    s_tgt[wave][lane] = make_float4(txr, tyr, tzr, hi); // SX_LOAD_QUARTER: one LDS read instead of five bpermutes
     float qx = 0, qy = 0, qz = 0, qh = 0;
     bool  qok = false;
     float fq[4] = {0, 0, 0, 0}, fo[4] = {0, 0, 0, 0};
 #define SX_LOAD_QUARTER(qq)                                                                                            \
     {                                                                                                                  \
-        const int src_ = 16 * (qq) + tq;                                                                               \
-        qx = __shfl(txr, src_), qy = __shfl(tyr, src_), qz = __shfl(tzr, src_), qh = __shfl(hi, src_);                 \
-        qok = __shfl((int)valid, src_) != 0;                                                                           \
+        const float4 t_ = s_tgt[wave][16 * (qq) + tq];                                                                 \
+        qx = t_.x, qy = t_.y, qz = t_.z, qh = t_.w;                                                                    \
+        qok = i0 + (uint32_t)(16 * (qq) + tq) < a.last;                                                                \
     }
 #define SX_FOLD_QUARTER(qq)                                                                                            \
     _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_)                                                                  \
     {                                                                                                                  \
-        float v_ = fq[c_];                                                                                             \
-        v_ += __shfl_xor(v_, 16);                                                                                      \
-        v_ += __shfl_xor(v_, 32);                                                                                      \
+        const float v_ = rowSum4(fq[c_]);                                                                              \
         if (sub == (qq)) fo[c_] += v_;                                                                                 \
         fq[c_] = 0.0f;                                                                                                 \
     }
@@ -467,7 +484,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             const uint32_t cn = jn;
             const unsigned cm = jm;
             __builtin_amdgcn_wave_barrier();
+#if SX_GRAV_PAIR_P2P
+            {
+                // source l goes to pair P = 4 (l / 8) + l % 4 as half (l / 4) % 2: the lane of sub s evaluates sources
+                // s + 8j and s + 8j + 4 together; lanes [cn, roundup8(cn)) write massless far-away padding
+                const uint32_t pad = (cn + 7u) & ~7u;
+                if ((uint32_t)lane < pad)
+                {
+                    const bool  in = (uint32_t)lane < cn;
+                    const int   P = (lane >> 3) * 4 + (lane & 3), hf = (lane >> 2) & 1;
+                    float*      d = reinterpret_cast<float*>(&s_srcF[wave][buf][0]) + P * 8 + hf;
+                    d[0] = in ? pv.x : 1e18f, d[2] = in ? pv.y : 1e18f, d[4] = in ? pv.z : 1e18f;
+                    d[6] = in ? pv.w : 0.0f;
+                    s_hF[wave][buf][P * 2 + hf] = in ? ph : 0.0f;
+                }
+            }
+#else
             if ((uint32_t)lane < cn) s_srcF[wave][buf][lane] = pv, s_hF[wave][buf][lane] = ph;
+#endif
             have = nextChunk();
             if (have) loadRegs();
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
@@ -480,6 +514,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                 continue;
 #endif
                 SX_LOAD_QUARTER(qq)
+#if SX_GRAV_PAIR_P2P
+                if (qok)
+                {
+                    // two sources per iteration in packed FP32 (v_pk_add/mul/fma_f32), the padding adds exact zeros
+                    const float* sp = reinterpret_cast<const float*>(&s_srcF[wave][buf][0]);
+                    const v2f    tx = {qx, qx}, ty = {qy, qy}, tz = {qz, qz}, th = {qh, qh};
+                    v2f          f2[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+                    for (uint32_t s = sub, P = sub; s < cn; s += 8, P += 4)
+                    {
+                        const float4 A = *reinterpret_cast<const float4*>(sp + P * 8);
+                        const float4 B = *reinterpret_cast<const float4*>(sp + P * 8 + 4);
+                        const float2 H = *reinterpret_cast<const float2*>(&s_hF[wave][buf][P * 2]);
+                        const v2f    dx = v2f{A.x, A.y} - tx, dy = v2f{A.z, A.w} - ty, dz = v2f{B.x, B.y} - tz;
+                        const v2f    R2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+                        const v2f    h_ij = th + v2f{H.x, H.y};
+                        const v2f    hh   = h_ij * h_ij;
+                        const v2f    invR = {__builtin_amdgcn_rsqf(fmaxf(R2.x, hh.x)),
+                                             __builtin_amdgcn_rsqf(fmaxf(R2.y, hh.y))}; // >= h^2: no denormals
+                        const v2f    invR3m = v2f{B.z, B.w} * invR * invR * invR;
+                        f2[0] = __builtin_elementwise_fma(-invR3m, R2, f2[0]);
+                        f2[1] = __builtin_elementwise_fma(dx, invR3m, f2[1]);
+                        f2[2] = __builtin_elementwise_fma(dy, invR3m, f2[2]);
+                        f2[3] = __builtin_elementwise_fma(dz, invR3m, f2[3]);
+                    }
+#pragma unroll
+                    for (int c_ = 0; c_ < 4; ++c_)
+                        fq[c_] += f2[c_].x + f2[c_].y;
+                }
+#else
                 if (qok)
                     for (uint32_t s = sub; s < cn; s += 4)
                     {
@@ -494,6 +557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                         fq[2] = fmaf(dy, invR3m, fq[2]);
                         fq[3] = fmaf(dz, invR3m, fq[3]);
                     }
+#endif
                 SX_FOLD_QUARTER(qq)
             }
             buf ^= 1;
