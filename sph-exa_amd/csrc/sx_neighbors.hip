@@ -515,14 +515,12 @@ findNeighborsKernel(NsArgs a)
                     const bool     two = lm != 0ull;
                     const uint32_t e2  = two ? sci[__builtin_ctzll(lm)] : 0u;
                     if (two) lm &= lm - 1ull;
-                    uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
-                    if (stored & 1u)
-                    {
-                        *dst = pend | (e1 << 16);
-                        pend = e2;
-                    }
-                    else if (two) { *dst = e1 | (e2 << 16); }
-                    else { pend = e1; }
+                    // one store site: odd parity completes the pending word, even parity writes a fresh pair (selects
+                    // instead of the three-way branch: -0.1 ms at 64M)
+                    const bool     odd = stored & 1u;
+                    const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
+                    if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
+                    pend = odd ? e2 : e1;
                     stored += two ? 2u : 1u;
                 }
 #endif
