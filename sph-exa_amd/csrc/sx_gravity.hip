@@ -240,6 +240,9 @@ struct __attribute__((aligned(16))) GSrc
     float  m, h;
 };
 
+#ifndef SX_GRAV_MERGE_LEAVES
+#define SX_GRAV_MERGE_LEAVES 1 // fast P2P: contiguous same-mask leaves share a chunk
+#endif
 #ifndef SX_GRAV_PAIR_P2P
 #define SX_GRAV_PAIR_P2P 1 // fast P2P: two sources per lane per iteration in packed FP32
 #endif
@@ -460,6 +463,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     jm = (unsigned)(e & 15);
                     ec0 += kWave;
                     if (s0 + ec0 >= s1) ++ek, ec0 = 0;
+#if SX_GRAV_MERGE_LEAVES
+                    // following list leaves with the same quarter mask whose particles continue this range (siblings
+                    // of one node, appended together in SFC order) join the chunk up to 64 sources
+                    while (ec0 == 0 && jn < (uint32_t)kWave && ek < nP)
+                    {
+                        const int      e2 = __builtin_amdgcn_readfirstlane(s_p2p[wave][ek]);
+                        const uint32_t r0 = __builtin_amdgcn_readfirstlane(s_rng[wave][ek].x);
+                        const uint32_t r1 = __builtin_amdgcn_readfirstlane(s_rng[wave][ek].y);
+                        if ((unsigned)(e2 & 15) != jm || r0 != js + jn) break;
+                        const uint32_t take = min((uint32_t)kWave - jn, r1 - r0);
+                        jn += take;
+                        if (take == r1 - r0) ++ek;
+                        else ec0 = take;
+                    }
+#endif
                     return true;
                 }
                 ++ek, ec0 = 0;
