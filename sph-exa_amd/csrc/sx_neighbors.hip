@@ -583,12 +583,24 @@ findNeighborsKernel(NsArgs a)
                 }
                 rm = __ballot(r);
             }
-            const int k = __builtin_ctzll(rm);
+            int k = __builtin_ctzll(rm);
             rm &= rm - 1ull;
             q.cc   = wb + k;
             q.s    = __builtin_amdgcn_readlane(wp0, k);
             q.p1   = q.s + __builtin_amdgcn_readlane(wcnt, k);
             q.base = __builtin_amdgcn_readlane(wco, k) - q.s;
+#ifndef SX_NS_NO_MERGE
+            // the next reachable candidate leaves of the window whose particles continue this range (SFC-adjacent
+            // leaves) join the block span: their candidate numbers continue it too (same base), so the stream and
+            // its order are unchanged, only fewer and fuller 64-particle blocks
+            while (k + 1 < kWave && ((rm >> (k + 1)) & 1ull))
+            {
+                if ((uint32_t)__builtin_amdgcn_readlane(wp0, k + 1) != q.p1) break;
+                ++k;
+                rm &= rm - 1ull;
+                q.p1 += __builtin_amdgcn_readlane(wcnt, k);
+            }
+#endif
         };
         auto load = [&](const Blk& q, double& X, double& Y, double& Z) {
             if (q.cc < numCand && q.s + lane < q.p1)
@@ -636,8 +648,9 @@ findNeighborsKernel(NsArgs a)
                 P[0] = px, P[2] = py, P[4] = pz, P[6] = fmaf(px, px, fmaf(py, py, pz * pz));
                 sci[slot] = cur.base + j;
             }
-            // this lane's own particle in the block (it always passes: it lies in the wave box)
-            if (valid && i >= cur.s && i < cur.p1)
+            // this lane's own particle in the block (it always passes: it lies in the wave box); this block only, a
+            // span of merged leaves holds several blocks
+            if (valid && i >= cur.s && i - cur.s < (uint32_t)kWave && i < cur.p1)
                 selfSeq = seq + (uint32_t)(fill + __popcll(bm & ((1ull << (i - cur.s)) - 1ull)));
             fill += n;
             if (fill == kWave || (nxt.cc >= numCand && fill > 0)) testChunk();
