@@ -10,7 +10,7 @@ Inputs are generated and kept in HBM; nothing leaves the device inside the timed
 N (strong scaling: N=1 holds all 64M particles on one MI355X, N=8 holds 8M + halos per GPU); --side 200 gives
 BASELINE config 2.
 Rank 0 prints ONE JSON line.  Its "roofline" is the dominant kernel's (largest share of the step): HBM bytes per
-launch from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_latest.json) over the kernel's
+launch from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_<init>_n<side>.json) over the kernel's
 average launch time measured here with HIP events on its stream.
 """
 import argparse
@@ -53,14 +53,18 @@ MOM_STD_EDGE_BYTES = 4 + 80
 # kernel-time slots of sx_sim in std mode (sx_sim.cpp: density in "xmass", IAD in "iadDivvCurlv")
 STD_KERNEL_NAMES = {"findNeighbors": "findNeighbors", "xmass": "density", "iadDivvCurlv": "iad",
                     "momentumEnergy": "momentumEnergySTD", "gravity": "gravity"}
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
-def load_pmc(particles, workload):
-    """per-kernel rocprofv3 --pmc summary of the same workload (scripts/gpu_pmc.sh + scripts/pmc_summary.py:
-    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, KB units), or None when it was taken on another workload"""
+def pmc_file(key):
+    """the committed rocprofv3 --pmc summary of one workload: profiles/pmc_<init>_n<side>[_<variant>].json"""
+    return os.path.join(ROOT, "profiles", f"pmc_{key}.json")
+
+
+def load_pmc(key, particles, workload):
+    """per-kernel rocprofv3 --pmc summary of the same workload (scripts/gpu_pmc.sh + scripts/pmc_summary.py, KB
+    units), or None when absent or taken on another workload"""
     try:
-        with open(PMC_FILE) as f:
+        with open(pmc_file(key)) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
@@ -219,21 +223,23 @@ def main():
     comm = None
     transport = args.backend
     if world > 1:
+        # no silent fallback: a scaling run that cannot create its RCCL communicator fails (a host-staged run would
+        # time PCIe + gloo instead of xGMI)
         try:
             comm = sx.Comm(args.backend)
             ok = 1
-        except sx.SxError as e:  # e.g. RCCL refusing the node's topology: keep the run alive on the staged path
-            print(f"rank {rank}: {e}; falling back to the host-staged transport", file=sys.stderr)
+        except sx.SxError as e:
+            print(f"rank {rank}: {e}", file=sys.stderr)
             ok = 0
         import torch
 
         flag = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank must use the same transport
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank learns whether some rank failed
         if int(flag.item()) == 0:
-            if comm is not None:
-                comm.close()
-            comm = sx.Comm("host")
-            transport = f"host (fallback: {args.backend} communicator creation failed)"
+            print(f"rank {rank}: {args.backend} communicator creation failed on some rank; no bench line",
+                  file=sys.stderr)
+            dist.destroy_process_group()
+            sys.exit(3)
         sim.set_comm(comm)
     if ic_arrays is None:
         sim.init_sedov(side, rank, world)
@@ -277,7 +283,8 @@ def main():
                 f"{'std (HydroProp)' if std_prop else 'VE'} propagator"
                 f"{' + self-gravity' if args.init == 'evrard' else ''}"
                 f"{' + AV cleaning' if args.av_clean else ''}, {args.steps} steps")
-    pmc = load_pmc(n_local, workload) if not std_prop else None
+    pmc_key = f"{args.init}_n{side}" + ("_avclean" if args.av_clean else "") + ("_std" if std_prop else "")
+    pmc = load_pmc(pmc_key, n_local, workload) if not std_prop else None
     per_kernel = {}
     for k, ms in kern_ms.items():
         if ms > 0.01 and (k in EDGE_MODEL or k == "gravity"):
@@ -290,7 +297,7 @@ def main():
                 "share_of_step": dom.get("avg_launch_ms", 0.0) / ms_step,
                 "binding": ("valu-issue/latency (HBM frac < 0.5; see valu_issue_frac, lds_conflict_frac)"
                             if (dom.get("frac") or 0) < 0.5 else "hbm"),
-                "traffic_source": os.path.relpath(PMC_FILE, ROOT) if pmc else None,
+                "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) if pmc else None,
                 "definition": "achieved = rocprofv3 PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, same "
                               "workload) / avg launch time measured live with HIP events; frac = achieved / 8 TB/s; "
                               "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); lds_conflict_frac = "

@@ -165,7 +165,7 @@ def sedov_state(side):
 
 def noh_state(side):
     """Noh substitute: side^3 lattice in [-0.5,0.5]^3 cut to r<=0.5, open box,
-    v = -r_hat, T = 1e-20/cv, dt0 = 1e-4 (noh_init.hpp:46-100 field values)."""
+    v = -r_hat, x_m1 = v dt0, T = 1e-20/cv, dt0 = 1e-4 (noh_init.hpp:46-100 field values)."""
     r = 0.5
     step = (2.0 * r) / side
     r_ini = -r + 0.5 * step
@@ -191,6 +191,9 @@ def noh_state(side):
     st.vy[:] = (-y * inv).astype(np.float32)
     st.vz[:] = (-z * inv).astype(np.float32)
     st.temp[:] = 1e-20 / np.float64(ideal_gas_cv())
+    # the integrator's previous displacement: x_m1 = v * minDt (noh_init.hpp:96-98, float storage of a double product)
+    for d in ("x", "y", "z"):
+        st.arrays[d + "_m1"][:] = (st.arrays["v" + d].astype(np.float64) * 1e-4).astype(np.float32)
     st.id[:] = np.arange(n, dtype=np.uint64)
     st.minDt = 1e-4
     st.minDt_m1 = 1e-4

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (separate runs, kernel-trace only; no sys/runtime trace -- see the HIP guide) over a short bench of the
-# default workload, then the per-kernel summary bench.py reads (profiles/pmc_latest.json after copying).
+# default workload, then the per-kernel summary bench.py reads (profiles/pmc_<key>.json after copying; scripts/gpu_profile.sh).
 #   TAG=r2 scripts/gpu_pmc.sh      -> gpurun_out/pmc_$TAG/{p*/,summary.json,summary.txt}
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

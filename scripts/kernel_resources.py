@@ -16,7 +16,7 @@ BASE = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-f
 SOURCES = {
     "sx_neighbors (large)": ("csrc/sx_neighbors.hip", ["-ffp-contract=off"]),
     "sx_neighbors (small)": ("csrc/sx_neighbors.hip", ["-ffp-contract=off", "-DSX_NS_SMALL", "-DSX_NS_CCAP=1024",
-                                                       "-DSX_NS_CAND_LOG2=14", "-DSX_NS_WAVES_PER_EU=4"]),
+                                                       "-DSX_NS_CAND_LOG2=14", "-DSX_NS_BATCH=24", "-DSX_NS_WAVES_PER_EU=4"]),
     "sx_hydro_cluster": ("csrc/sx_hydro_cluster.hip", ["-ffp-contract=fast", "-fno-slp-vectorize",
                                                        "-fgpu-flush-denormals-to-zero"]),
     "sx_hydro (fast)": ("csrc/sx_hydro.hip", ["-ffp-contract=fast", "-DSX_VARIANT=fast"]),

@@ -433,7 +433,9 @@ extern "C"
         a.policy         = &c->nsPolicy;
         a.clStats        = c->arena.get<uint4>("ns.clstats", (a.numGroups + kClusterWaves - 1) / kClusterWaves);
         a.active         = c->viewActive;
-        if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab || !a.clStats)
+        a.work           = c->arena.get<uint32_t>("ns.work", 16);
+        a.hitMasks       = c->arena.get<uint64_t>("ns.masks", searchScratchBytes() / sizeof(uint64_t));
+        if (!c->nb.reserve(c->arena, first, last, p->ngmax, true) || !a.powTab || !a.clStats || !a.work || !a.hitMasks)
             return fail(c, SX_ERR_NOMEM, "neighbor list allocation failed");
         a.setLists(c->nb);
         SX_HIP(c, hipMemsetAsync(c->stats, 0, kStatsWords * 4, c->stream));

@@ -6,33 +6,46 @@
  * sph/find_neighbors.hpp:10-44) and the traversal inside xmassGpu (hydro_ve/xmass_gpu.cu:56-101).
  *
  * Per cluster (workgroup):
- *   1. wave + LDS reductions give the cluster's bounding box and max h;
- *   2. wave 0 collects every leaf whose geometric box comes within 2*hmax_w of some wave's box (waveCollectLeaves,
+ *   1. search regions in registers (wave / 16-particle sub-group boxes, particle spheres where the SFC range jumps);
+ *   2. wave 0 collects every leaf whose geometric box comes within 2*h*ext of some region (waveCollectLeaves,
  *      sx_traverse.hpp; minimum image on periodic axes, inflated by the key-quantisation margin) and numbers the
  *      particles of those leaves consecutively: the cluster's CANDIDATE SPACE (leaf cc's particles start at
  *      s_cOff[cc]);
- *   3. each wave independently streams the candidate leaves that one of its lanes can reach, in chunks of 64
- *      particles loaded coalesced one per lane and broadcast lane by lane with v_readlane; every lane tests them
- *      against its own particle with the reference CPU criterion, in double, without FMA contraction (this file is
- *      compiled -ffp-contract=off):
- *          d2 = dx*dx + dy*dy + dz*dz  <  (double)(4.0f*h*h),   j != i,
- *      dx folded with rint() on periodic axes when the particle is within 2h of the box edge (findneighbors.hpp:118).
- *      Stored hits (the first ngmax, like the reference's capped list) are appended to the lane's list -- the global
- *      index (nidx, gather kernels) or the u16 candidate index (cluster lists) -- and, for cluster lists, OR-ed into
- *      an LDS bitmap over the candidate space (one atomic per chunk and wave; no workgroup barrier in the stream);
+ *   3. each wave streams the candidate leaves one of its lanes can reach in blocks of 64 particles, culls them
+ *      against the wave box grown by 2 hmax and stages the survivors into 64-slot CHUNKS (records in LDS, the
+ *      slot's candidate index in the wave's chunk table); every lane tests a chunk against its own particle with a
+ *      packed f32 test whose ambiguous chunks go to the reference CPU criterion in double
+ *          d2 = dx*dx + dy*dy + dz*dz  <  (double)(4.0f*h*h),   j != i
+ *      (dx minimum-image on periodic axes, findneighbors.hpp:118-158); a lane's hits in a chunk are one 64-bit
+ *      HIT MASK, capped to the first ngmax hits in stream order like the reference's list;
  *   4. lanes with nc = count+1 outside [ng0/4, ngmax+1] update h (updateH) and the cluster repeats, at most 10
  *      updates per lane (the CPU loop's `iteration++ < 10`), so h, nc and the neighbor SET are identical to the
  *      CPU reference;
- *   5. cluster lists: a prefix popcount of the bitmap numbers the UNION of the cluster's neighbors (uni[], in
- *      candidate order, i.e. leaf runs), and every lane rewrites its candidate indices as union positions -- still
- *      ascending, which the chunked LDS staging of sx_hydro_cluster.hip relies on.
+ *   5. cluster lists: the union bitmap over the candidate space (OR-ed per chunk) is numbered by a prefix popcount:
+ *      the UNION of the cluster's neighbors (uni[], candidate order = leaf runs); the chunk tables are translated to
+ *      union positions and every lane expands its hit masks into its u16 list (ascending, which the chunked LDS
+ *      staging of sx_hydro_cluster.hip relies on).
+ *
+ * Deferred list expansion (step 5).  Appending a chunk's hits right after its test walks the chunk's hit masks in a
+ * divergent loop whose trip count is the MAX over the wave's lanes of the hits in that chunk; a chunk is a compact
+ * region, so the lanes near it have many hits and the others few, and the sum of these maxima was ~3.9x a lane's
+ * own hit count (Sedov lattice: 180 iterations per wave against 46).  The masks of the last h pass are therefore
+ * kept (global scratch per resident workgroup, the chunk tables in LDS) and expanded once after the pass, each
+ * lane walking its own nonzero masks: trip count = max over lanes of its own hits / 2.  A wave with more chunks
+ * than its table holds expands the full batch early with candidate indices, which the final pass rewrites to union
+ * positions.
+ *
+ * Work distribution: a persistent grid (the occupancy's worth of workgroups) takes clusters from eight work
+ * counters, one per XCD range of the SFC order (blocks are dealt round-robin to the XCDs, so workgroup b serves XCD
+ * range b % 8 and steals from the other ranges when its own is done): consecutive clusters share neighbors in the
+ * XCD's L2, and every workgroup owns a fixed slot of the hit-mask scratch.
  */
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
 // Two builds of this file: the default one (large capacities: 2048 candidate leaves, 2^16 candidate particles per
 // cluster, 53 KB of LDS, three workgroups per CU) and, with SX_NS_SMALL, a compact one in namespace sx::small
-// (1024 leaves, 2^14 particles, 28 KB, four workgroups per CU; Makefile).  findNeighbors runs the compact one
+// (1024 leaves, 2^14 particles, 36 KB, four workgroups per CU; Makefile).  findNeighbors runs the compact one
 // and falls back to the large one when a cluster exceeds its capacities.
 #ifdef SX_NS_SMALL
 namespace sx
@@ -44,10 +57,6 @@ namespace sx
 {
 #endif
 
-#ifndef SX_NS_GROUP
-#define SX_NS_GROUP 4
-#endif
-constexpr int kNsGroup = SX_NS_GROUP;
 #ifndef SX_NS_CCAP
 #define SX_NS_CCAP 2048
 #endif
@@ -57,9 +66,13 @@ constexpr int kCCap = SX_NS_CCAP; //!< candidate leaves per cluster (this build'
 #define SX_NS_CAND_LOG2 16
 #endif
 constexpr int kCandSpace = 1 << SX_NS_CAND_LOG2; //!< candidate particles per cluster (u16 list entries)
-constexpr int kSubGroups  = kCluster / 16; //!< 16-particle sub-groups per cluster
 constexpr int kMaxRegions = 128;           //!< search regions per cluster (boxes or particle spheres)
 constexpr int kCandWords = kCandSpace / 32;
+#ifndef SX_NS_BATCH
+#define SX_NS_BATCH 8
+#endif
+constexpr int kBatch = SX_NS_BATCH; //!< chunks whose hit masks a wave keeps before expanding them into its lists
+static_assert(kBatch <= 32, "nonzero-chunk bits per lane");
 
 __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t* pre, uint32_t idx)
 {
@@ -73,35 +86,71 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 #define SX_NS_WAVES_PER_EU 3
 #endif
 
+//! per-wave LDS of the stream: 64 staged candidate records (pair layout) and the batch's chunk tables (candidate
+//! index, later union position, of every slot).  The search regions alias it (they are only used before the stream).
+struct NsWaveLds
+{
+    float4   rec[kWave];
+    uint16_t tab[kBatch][kWave];
+};
+constexpr int kRegionBytes = 2 * kMaxRegions * (int)sizeof(double4);
+constexpr int kWaveLdsBytes = (int)sizeof(NsWaveLds) * kClusterWaves;
+union NsStreamLds
+{
+    NsWaveLds w[kClusterWaves];
+    double4   reg[2 * kMaxRegions];
+};
+
+//! next cluster of this workgroup: the XCD range of blockIdx % 8 first, then the other ranges (work stealing);
+//! numClusters when every range is done
+__device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClusters)
+{
+    const uint32_t x0 = blockIdx.x & 7;
+    for (uint32_t t = 0; t < 8; ++t)
+    {
+        const uint32_t x  = (x0 + t) & 7;
+        const uint32_t lo = (uint32_t)((uint64_t)numClusters * x / 8), hi = (uint32_t)((uint64_t)numClusters * (x + 1) / 8);
+        if (__hip_atomic_load(&work[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi - lo) continue;
+        const uint32_t k = atomicAdd(&work[x], 1u);
+        if (lo + k < hi) return lo + k;
+    }
+    return numClusters;
+}
+
 __global__ __launch_bounds__(kCluster) __attribute__((amdgpu_waves_per_eu(SX_NS_WAVES_PER_EU))) void
 findNeighborsKernel(NsArgs a)
 {
-    __shared__ int      s_queue[kQCap];
-    __shared__ int      s_cand[kCCap];
-    __shared__ uint32_t s_cOff[kCCap + 1];
-    __shared__ uint32_t s_p0[kCCap];    // first particle of candidate leaf cc
-    __shared__ uint8_t  s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
-    __shared__ uint32_t s_bits[kCandWords];
-    __shared__ uint32_t s_pre[kCandWords];
-    __shared__ int      s_nreg;
-    __shared__ int      s_again[kClusterWaves];
-    __shared__ uint32_t s_wsum[kClusterWaves];
-    // per wave: [0] 64 staged candidate records (pair layout), [1] the candidate index of each staged slot
-    __shared__ float4   s_chunk[kClusterWaves][2][kWave];
-    __shared__ int      s_numCand;
-    __shared__ uint4    s_cst[kClusterWaves]; // per-wave statistics
-    // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}; s_chunk is only used inside the stream
-    double4* const s_reg = reinterpret_cast<double4*>(&s_chunk[0][0][0]);
-    static_assert(sizeof(s_chunk) >= 2 * kMaxRegions * sizeof(double4), "search regions alias s_chunk");
+    __shared__ int         s_queue[kQCap];
+    __shared__ int         s_cand[kCCap];
+    __shared__ uint32_t    s_cOff[kCCap + 1];
+    __shared__ uint32_t    s_p0[kCCap];    // first particle of candidate leaf cc
+    __shared__ uint8_t     s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
+    __shared__ uint32_t    s_bits[kCandWords];
+    __shared__ uint32_t    s_pre[kCandWords];
+    __shared__ int         s_nreg;
+    __shared__ int         s_again[kClusterWaves];
+    __shared__ uint32_t    s_wsum[kClusterWaves];
+    __shared__ NsStreamLds s_str;
+    __shared__ int         s_numCand;
+    __shared__ uint4       s_cst[kClusterWaves]; // per-wave statistics
+    __shared__ uint32_t    s_next;               // the cluster this workgroup takes next
+    double4* const s_reg = s_str.reg;            // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}
 
-    // the fallback launch (a.gate) is a small persistent grid that exits at once unless the compact build overflowed
+    // the fallback launch (a.gate) exits at once unless the compact build overflowed
     if (a.gate && *a.gate == 0u) return;
     const uint32_t numClusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    for (uint32_t blk = blockIdx.x; blk < numClusters; blk += gridDim.x)
+    const int      wave        = threadIdx.x >> 6;
+    const int      lane        = threadIdx.x & 63;
+    NsWaveLds&     wl          = s_str.w[wave];
+    // this wave's hit-mask rows (kBatch x 64 lanes), one slot per workgroup of the persistent grid
+    uint64_t* const maskRow = a.hitMasks + ((size_t)blockIdx.x * kClusterWaves + wave) * kBatch * kWave + lane;
+    if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters);
+    __syncthreads();
+    uint32_t c = s_next;
+    while (c < numClusters)
     {
-    const int      wave  = threadIdx.x >> 6;
-    const int      lane  = threadIdx.x & 63;
-    const uint32_t c     = gridDim.x >= numClusters ? xcdBlock(blk, numClusters) : blk;
+    __syncthreads(); // every thread has read s_next
+    if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters); // in flight while this cluster is searched
     const uint32_t g     = c * kClusterWaves + wave;
     const uint32_t c0    = a.first + c * kCluster;
     const uint32_t i     = c0 + threadIdx.x;
@@ -121,28 +170,74 @@ findNeighborsKernel(NsArgs a)
     bool               active     = valid;
     unsigned           count      = 0;
     unsigned           stored     = 0;
+    uint32_t           pend       = 0; // low half of the next u16-pair word
     unsigned long long candTested = 0;
+    int                nq         = 0; // chunks of the current batch (wave-uniform)
+    uint32_t           nzq        = 0; // bit q: this lane hit something in chunk q of the batch
+    uint32_t           nEarly     = 0; // list entries written as candidate indices by early batch expansions
 
-    // search regions.  An SFC range can jump across empty space (the curve leaves and re-enters a sphere's
-    // surface), so a cluster or wave box may span a gap; regions are therefore the boxes of the 16 sub-groups of
-    // 16 consecutive particles, and a sub-group whose box is wider than 8 of its search radii (it straddles such a
-    // jump) is replaced by the spheres of its particles.  Positions do not change over the h iteration.
+    // expand the batch's hit masks into this lane's list: candidate indices (early, the union is not known yet) or
+    // union positions (final: the chunk tables translated first).  Per lane, its nonzero chunks in order, two hits
+    // per iteration; the next nonzero chunk's mask is loaded while the current one is expanded.
+    auto expandBatch = [&](bool final) {
+        if (final)
+        {
+            for (int q = 0; q < nq; ++q)
+            {
+                // slots nobody hit hold stale indices: bounded into the candidate space, never referenced
+                const uint32_t ci = wl.tab[q][lane] & (kCandSpace - 1);
+                wl.tab[q][lane]   = (uint16_t)bitRank(s_bits, s_pre, ci);
+            }
+        }
+        // the mask stores of this wave precede their loads; the translated tables have landed
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t nz = nzq;
+        int      q  = nz ? __builtin_ctz(nz) : 0;
+        nz &= nz - 1u;
+        uint64_t m  = nzq ? __builtin_nontemporal_load(maskRow + (size_t)q * kWave) : 0ull;
+        int      qn = nz ? __builtin_ctz(nz) : 0;
+        uint64_t mn = nz ? __builtin_nontemporal_load(maskRow + (size_t)qn * kWave) : 0ull;
+        nz &= nz - 1u;
+        while (m)
+        {
+            const uint16_t* tq = wl.tab[q];
+            const uint32_t  e1 = tq[__builtin_ctzll(m)];
+            m &= m - 1ull;
+            const bool     two = m != 0ull;
+            const uint32_t e2  = two ? tq[__builtin_ctzll(m)] : 0u;
+            if (two) m &= m - 1ull;
+            // one store site: odd parity completes the pending word, even parity writes a fresh pair
+            const bool     odd = stored & 1u;
+            const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
+            if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
+            pend = odd ? e2 : e1;
+            stored += two ? 2u : 1u;
+            if (!m)
+            {
+                m  = mn, q = qn;
+                qn = nz ? __builtin_ctz(nz) : 0;
+                mn = nz ? __builtin_nontemporal_load(maskRow + (size_t)qn * kWave) : 0ull;
+                nz &= nz - 1u;
+            }
+        }
+        if (!final) nEarly = stored;
+        nq  = 0;
+        nzq = 0;
+        __builtin_amdgcn_wave_barrier(); // table reads precede the next chunk's staging writes
+    };
+
     int numCand = 0;
-#ifdef SX_NS_PROFILE
-    uint64_t prof[6] = {0, 0, 0, 0, 0, 0}; // cycles: candidates+scan, stream, tests, post-test, union; chunks
-#endif
     while (true)
     {
-#ifdef SX_NS_PROFILE
-        const uint64_t tB = __builtin_readcyclecounter();
-#endif
-        // ---- 2. candidate leaves within reach of some search region, numbered into the candidate space ----
+        // ---- 1./2. search regions, then the candidate leaves within reach of one, numbered into the candidate space
         if (threadIdx.x == 0) s_nreg = 0;
         __syncthreads();
         {
-            // regions: the wave box when it is coherent (no wider than 8 search radii), else its coherent 16-particle
-            // sub-group boxes and, for incoherent sub-groups, the spheres of their particles (all in registers:
-            // 16-lane then 64-lane shuffles over the valid lanes)
+            // regions: the wave box when it is coherent (no wider than 16 search radii), else its coherent
+            // 16-particle sub-group boxes and, for incoherent sub-groups, the spheres of their particles (all in
+            // registers: 16-lane then 64-lane shuffles over the valid lanes).  An SFC range can jump across empty
+            // space (the curve leaves and re-enters a sphere's surface), so a wave box may span a gap.
             double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
             double hb[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
             float  hq    = valid ? hi : 0.0f;
@@ -156,15 +251,15 @@ findNeighborsKernel(NsArgs a)
                 }
                 hq = fmaxf(hq, __shfl_xor(hq, o, 16));
             }
-            double wl[3] = {lo[0], lo[1], lo[2]}, wh[3] = {hb[0], hb[1], hb[2]};
-            float  hw    = hq;
+            double wlo[3] = {lo[0], lo[1], lo[2]}, whi[3] = {hb[0], hb[1], hb[2]};
+            float  hw     = hq;
 #pragma unroll
             for (int o = 16; o < 64; o <<= 1)
             {
                 for (int d = 0; d < 3; ++d)
                 {
-                    wl[d] = fmin(wl[d], __shfl_xor(wl[d], o, 64));
-                    wh[d] = fmax(wh[d], __shfl_xor(wh[d], o, 64));
+                    wlo[d] = fmin(wlo[d], __shfl_xor(wlo[d], o, 64));
+                    whi[d] = fmax(whi[d], __shfl_xor(whi[d], o, 64));
                 }
                 hw = fmaxf(hw, __shfl_xor(hw, o, 64));
             }
@@ -178,10 +273,10 @@ findNeighborsKernel(NsArgs a)
                     s_reg[2 * k + 1] = make_double4(0.5 * (x1 - x0), 0.5 * (y1 - y0), 0.5 * (z1 - z0), (double)wave);
                 }
             };
-            const double extW = fmax(wh[0] - wl[0], fmax(wh[1] - wl[1], wh[2] - wl[2]));
+            const double extW = fmax(whi[0] - wlo[0], fmax(whi[1] - wlo[1], whi[2] - wlo[2]));
             if (extW <= 16.0 * (double)hw)
             {
-                if (lane == 0 && hw > 0.0f) addRegion(wl[0], wh[0], wl[1], wh[1], wl[2], wh[2], hw);
+                if (lane == 0 && hw > 0.0f) addRegion(wlo[0], whi[0], wlo[1], whi[1], wlo[2], whi[2], hw);
             }
             else
             {
@@ -214,10 +309,9 @@ findNeighborsKernel(NsArgs a)
         if (wave == 0)
         {
             bool      overflow = false;
-            const int nCand    = (a.experiment & 16) ? 0
-                                                     : waveCollectLeaves<kCCap>(
-                                                        a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; },
-                                                        s_queue, s_cand, lane, overflow);
+            const int nCand    = waveCollectLeaves<kCCap>(
+                a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, lane,
+                overflow);
             if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short
             // exclusive scan of the candidate leaf sizes
             uint32_t run = 0;
@@ -250,15 +344,11 @@ findNeighborsKernel(NsArgs a)
                 if (a.forceOverflow) f |= 4u; // test hook (sx_set_search_mode 3): exercise the device-side fallback
 #endif
                 if (f) atomicOr(&a.stats[0], 1u | f);
-#ifdef SX_NS_DEBUG
-                if (f && atomicAdd(&a.stats[3], 1u) < 8)
-                    printf("ns overflow: cluster %u flags %u nCand %d run %u regions %d\n", c, f, nCand, run, s_nreg);
-#endif
                 s_numCand = f ? 0 : nCand;
             }
         }
         __syncthreads();
-        numCand = (a.experiment & 8) ? 0 : s_numCand;
+        numCand = s_numCand;
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
@@ -272,12 +362,8 @@ findNeighborsKernel(NsArgs a)
             for (uint32_t w = threadIdx.x; w < nw; w += kCluster)
                 s_bits[w] = 0;
         }
-        __syncthreads();
+        __syncthreads(); // the regions (aliasing the stream LDS) are no longer read
 
-#ifdef SX_NS_PROFILE
-        prof[0] += __builtin_readcyclecounter() - tB;
-        const uint64_t tS = __builtin_readcyclecounter();
-#endif
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f    = 4.0f * hi * hi;
         const double radSq  = (double)r2f;
@@ -325,10 +411,9 @@ findNeighborsKernel(NsArgs a)
         const float cr  = fmaf(xr, xr, fmaf(yr, yr, fmaf(zr, zr, -thr))); // |r|^2 - 4h^2
         const v2f   mrx = {-2.0f * xr, -2.0f * xr}, mry = {-2.0f * yr, -2.0f * yr}, mrz = {-2.0f * zr, -2.0f * zr},
                   c2 = {cr, cr};
-        float*         srec   = reinterpret_cast<float*>(&s_chunk[wave][0]); // 64 slots, pair layout
-        uint32_t*      sci    = reinterpret_cast<uint32_t*>(&s_chunk[wave][1][0]); // candidate index per slot
+        float*         srec   = reinterpret_cast<float*>(wl.rec); // 64 slots, pair layout
 
-        // candidate index -> global particle index (s_cOff ascending in cc): only for the rare exact chunks
+        // candidate index -> global particle index (s_cOff ascending in cc): the exact chunks and global lists
         auto globalOf = [&](uint32_t ci) -> uint32_t {
             int lo = 0, hi2 = numCand - 1;
             while (lo < hi2)
@@ -339,12 +424,12 @@ findNeighborsKernel(NsArgs a)
             }
             return s_p0[lo] + (ci - s_cOff[lo]);
         };
-        // the reference criterion in double for the m staged slots: this lane's hits as slot bits
-        auto exactChunk = [&](int m) -> uint64_t {
+        // the reference criterion in double for the m staged slots of table row tq: this lane's hits as slot bits
+        auto exactChunk = [&](int m, const uint16_t* tq) -> uint64_t {
             double xj = 0, yj = 0, zj = 0;
             if (lane < m)
             {
-                const uint32_t j = globalOf(sci[lane]);
+                const uint32_t j = globalOf(tq[lane]);
                 xj = a.x[j], yj = a.y[j], zj = a.z[j];
             }
             uint64_t hm = 0;
@@ -366,15 +451,18 @@ findNeighborsKernel(NsArgs a)
 
         count         = 0;
         stored        = 0;
-        uint32_t pend = 0; // low half of the next u16-pair word
+        nEarly        = 0;
+        nq            = 0;
+        nzq           = 0;
         uint32_t seq     = 0;           // candidates tested before the current chunk (wave-uniform)
         uint32_t selfSeq = 0xffffffffu; // stream sequence number of this lane's own particle once staged
         int      fill    = 0;
 
-        // test the fill staged slots, update counts, union bitmap and this lane's list
+        // test the fill staged slots of table row nq: hit mask -> count, union bitmap, the batch (or global lists)
         auto testChunk = [&]() {
             const int m = fill;
             candTested += m;
+            uint16_t* tq = wl.tab[nq];
             // pad the group of 8 with far-away records (t ~ 1e36: no hit, not ambiguous)
             const int mp = (m + 7) & ~7;
             if (lane >= m && lane < mp)
@@ -386,18 +474,14 @@ findNeighborsKernel(NsArgs a)
             __builtin_amdgcn_wave_barrier();
             uint64_t hm    = 0;
             bool     exact = !fastWave;
-            if (a.experiment & 4) exact = false;
-            else if (!exact)
+            if (!exact)
             {
                 // t = |p - r|^2 - 4h^2 = pw + (|r|^2 - 4h^2) - 2 p.r per candidate pair (packed f32, p from LDS);
                 // hit = sign bit of t, gathered by v_alignbit; |t| < tol defers the chunk to the exact double test
-                const float4* sc = reinterpret_cast<const float4*>(srec);
-#ifdef SX_NS_PROFILE
-                const uint64_t tT = __builtin_readcyclecounter();
-#endif
-                const int ng  = mp >> 3; // groups of 8 candidates (4 pairs)
-                uint32_t  acc = 0, wlo = 0, whi = 0;
-                float     am  = 3.0e38f;
+                const float4* sc  = reinterpret_cast<const float4*>(srec);
+                const int     ng  = mp >> 3; // groups of 8 candidates (4 pairs)
+                uint32_t      acc = 0, wlo = 0, whi = 0;
+                float         am  = 3.0e38f;
                 for (int g = 0; g < ng; ++g)
                 {
 #pragma unroll
@@ -418,9 +502,6 @@ findNeighborsKernel(NsArgs a)
                 // candidate k of a half sits at bit (n-1-k) of acc: reverse, then drop the unused low bits
                 if (ng < 4) wlo = __builtin_bitreverse32(acc) >> (32 - 8 * ng);
                 else if (ng > 4) whi = __builtin_bitreverse32(acc) >> (32 - 8 * (ng - 4));
-#ifdef SX_NS_PROFILE
-                prof[2] += __builtin_readcyclecounter() - tT;
-#endif
                 if (__ballot(am < tol)) exact = true;
                 else
                 {
@@ -428,13 +509,9 @@ findNeighborsKernel(NsArgs a)
                     if (m < 64) hm &= (1ull << m) - 1ull;
                 }
             }
-            if (exact) hm = exactChunk(m);
+            if (exact) hm = exactChunk(m, tq);
             const uint32_t sd = selfSeq - seq;
             if (sd < (uint32_t)m) hm &= ~(1ull << sd); // j != i
-#ifdef SX_NS_PROFILE
-            const uint64_t tP = __builtin_readcyclecounter();
-            prof[5] += (exact ? (1ull << 32) : 0ull) + 1ull;
-#endif
             const unsigned nh = __popcll(hm);
             if (count + nh > a.ngmax)
             {
@@ -450,94 +527,34 @@ findNeighborsKernel(NsArgs a)
                 hm = kept;
             }
             count += nh;
-            uint64_t lm = hm;
-            if (a.experiment & 1) {}
-            else if (local)
+            if (local)
             {
                 // union bitmap: slot k hit by some lane -> its candidate bit
-                const uint64_t wm = waveOr64(lm);
+                const uint64_t wm = waveOr64(hm);
                 if (lane < m && ((wm >> lane) & 1ull))
                 {
-                    const uint32_t ci = sci[lane];
+                    const uint32_t ci = tq[lane];
                     atomicOr(&s_bits[ci >> 5], 1u << (ci & 31));
                 }
-#ifdef SX_NS_UAPPEND
-                // append by a wave-uniform walk over the slots some lane hit: the slot's candidate index is
-                // broadcast from the lane that staged it (v_readlane), each hitting lane appends it
-                const uint32_t ciLane = lane < m ? sci[lane] : 0u;
-                uint64_t       wr     = wm;
-                while (wr)
-                {
-                    const int      k = __builtin_ctzll(wr);
-                    wr &= wr - 1ull;
-                    const uint32_t e = __builtin_amdgcn_readlane(ciLane, k);
-                    if ((lm >> k) & 1ull)
-                    {
-                        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend | (e << 16);
-                        pend = e;
-                        stored++;
-                    }
-                }
-#elif defined(SX_NS_APPEND_HALVES)
-                // append two hits per iteration, 32-bit halves one after the other (0.6 ms slower at 64M: the trip count
-                // is the sum of the two halves' maxima over lanes)
-#pragma unroll
-                for (int half = 0; half < 2; ++half)
-                {
-                    uint32_t       hb  = half ? (uint32_t)(lm >> 32) : (uint32_t)lm;
-                    const uint32_t hb0 = 32u * half;
-                    while (hb)
-                    {
-                        const uint32_t e1 = sci[hb0 + __builtin_ctz(hb)];
-                        hb &= hb - 1u;
-                        const bool     two = hb != 0u;
-                        const uint32_t e2  = two ? sci[hb0 + __builtin_ctz(hb)] : 0u;
-                        if (two) hb &= hb - 1u;
-                        uint32_t* dst = ll + (size_t)(stored >> 1) * kWave;
-                        if (stored & 1u)
-                        {
-                            *dst = pend | (e1 << 16);
-                            pend = e2;
-                        }
-                        else if (two) { *dst = e1 | (e2 << 16); }
-                        else { pend = e1; }
-                        stored += two ? 2u : 1u;
-                    }
-                }
+                // the chunk joins the batch: this lane's mask row (coalesced 512-B store per wave)
+                maskRow[(size_t)nq * kWave] = hm;
+                nzq |= (hm != 0ull ? 1u : 0u) << nq;
+#ifdef SX_NS_NO_EARLY
+                if (++nq == kBatch) { atomicOr(&a.stats[0], 1u | 4u); nq = 0; nzq = 0; }
 #else
-                // append two hits per iteration over the whole 64-bit mask: the trip count is the max over lanes of
-                // the chunk's hits / 2 (Sedov 64M: 35.9 -> 35.35 ms against
-                // 32-bit halves, whose trip count is the sum of each half's max)
-                while (lm)
-                {
-                    const uint32_t e1 = sci[__builtin_ctzll(lm)];
-                    lm &= lm - 1ull;
-                    const bool     two = lm != 0ull;
-                    const uint32_t e2  = two ? sci[__builtin_ctzll(lm)] : 0u;
-                    if (two) lm &= lm - 1ull;
-                    // one store site: odd parity completes the pending word, even parity writes a fresh pair (selects
-                    // instead of the three-way branch: -0.1 ms at 64M)
-                    const bool     odd = stored & 1u;
-                    const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
-                    if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
-                    pend = odd ? e2 : e1;
-                    stored += two ? 2u : 1u;
-                }
+                if (++nq == kBatch) expandBatch(false);
 #endif
             }
             else
             {
-                while (lm)
+                while (hm)
                 {
-                    const int k = __builtin_ctzll(lm);
-                    lm &= lm - 1ull;
-                    gl[(size_t)stored * kWave] = globalOf(sci[k]);
+                    const int k = __builtin_ctzll(hm);
+                    hm &= hm - 1ull;
+                    gl[(size_t)stored * kWave] = globalOf(tq[k]);
                     stored++;
                 }
             }
-#ifdef SX_NS_PROFILE
-            prof[3] += __builtin_readcyclecounter() - tP;
-#endif
             seq += m;
             fill = 0;
             __builtin_amdgcn_wave_barrier(); // every lane's slot reads precede the next staging writes
@@ -546,8 +563,7 @@ findNeighborsKernel(NsArgs a)
         // blocks of up to 64 consecutive particles of the reachable candidate leaves, in candidate order; the next
         // block's coordinates are loaded while the current one is culled, staged and (when the chunk fills) tested.
         // Reachable non-empty leaves are found 64 at a time: lane l of the window holds leaf wb + l, a ballot gives
-        // the window's reachable set (wave-uniform scalar iteration).  (Packing several small leaves into one block
-        // measured 2.2x slower: the segment selection costs registers and spills in this loop.)
+        // the window's reachable set (wave-uniform scalar iteration).
         const uint32_t wbit = 1u << wave;
         struct Blk
         {
@@ -589,7 +605,6 @@ findNeighborsKernel(NsArgs a)
             q.s    = __builtin_amdgcn_readlane(wp0, k);
             q.p1   = q.s + __builtin_amdgcn_readlane(wcnt, k);
             q.base = __builtin_amdgcn_readlane(wco, k) - q.s;
-#ifndef SX_NS_NO_MERGE
             // the next reachable candidate leaves of the window whose particles continue this range (SFC-adjacent
             // leaves) join the block span: their candidate numbers continue it too (same base), so the stream and
             // its order are unchanged, only fewer and fuller 64-particle blocks
@@ -600,7 +615,6 @@ findNeighborsKernel(NsArgs a)
                 rm &= rm - 1ull;
                 q.p1 += __builtin_amdgcn_readlane(wcnt, k);
             }
-#endif
         };
         auto load = [&](const Blk& q, double& X, double& Y, double& Z) {
             if (q.cc < numCand && q.s + lane < q.p1)
@@ -612,19 +626,13 @@ findNeighborsKernel(NsArgs a)
         Blk cur{-1, 0, 0, 0};
         advance(cur);
         double cx = 0, cy = 0, cz = 0;
-#ifndef SX_NS_NOPF
         load(cur, cx, cy, cz);
-#endif
         while (cur.cc < numCand)
         {
             Blk nxt = cur;
             advance(nxt);
             double nx = 0, ny = 0, nz = 0;
-#ifdef SX_NS_NOPF
-            load(cur, cx, cy, cz);
-#else
             load(nxt, nx, ny, nz);
-#endif
             const uint32_t j  = cur.s + lane;
             const bool     in = j < cur.p1;
             float          px = 0, py = 0, pz = 0;
@@ -646,7 +654,7 @@ findNeighborsKernel(NsArgs a)
                 const int slot = fill + __popcll(bm & ltMask);
                 float*    P    = srec + (slot >> 1) * 8 + (slot & 1);
                 P[0] = px, P[2] = py, P[4] = pz, P[6] = fmaf(px, px, fmaf(py, py, pz * pz));
-                sci[slot] = cur.base + j;
+                wl.tab[nq][slot] = (uint16_t)(cur.base + j);
             }
             // this lane's own particle in the block (it always passes: it lies in the wave box); this block only, a
             // span of merged leaves holds several blocks
@@ -656,11 +664,7 @@ findNeighborsKernel(NsArgs a)
             if (fill == kWave || (nxt.cc >= numCand && fill > 0)) testChunk();
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
-        if (local && (stored & 1u)) ll[(size_t)(stored >> 1) * kWave] = pend;
 
-#ifdef SX_NS_PROFILE
-        prof[1] += __builtin_readcyclecounter() - tS;
-#endif
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -686,13 +690,10 @@ findNeighborsKernel(NsArgs a)
         for (int w = 0; w < kClusterWaves; ++w)
             any |= s_again[w];
         if (!any) break;
-        __syncthreads(); // s_again / s_hmax / candidate space are rewritten by the next iteration
+        __syncthreads(); // s_again / candidate space / regions are rewritten by the next iteration
     }
 
-#ifdef SX_NS_PROFILE
-    const uint64_t tU = __builtin_readcyclecounter();
-#endif
-    // ---- 5. cluster union: prefix popcount of the bitmap, union entries, list rewrite -----------------------
+    // ---- 5. cluster union: prefix popcount of the bitmap, union entries, list expansion ------------------------
     uint32_t ucnt = 0;
     if (local)
     {
@@ -752,39 +753,38 @@ findNeighborsKernel(NsArgs a)
                 ++run;
             }
         }
-        __syncthreads();
-        // candidate indices -> union positions (ascending either way)
-        // batches of 8 list words: the 8 loads are issued together (one L2 round trip per batch instead of one per
-        // word), then ranked in LDS and stored
-        const uint32_t nwl = (a.experiment & 2) ? 0u : (stored + 1) >> 1;
-        constexpr int  kRB = 8;
-        for (uint32_t k0 = 0; k0 < nwl; k0 += kRB)
+        __syncthreads(); // s_pre complete
+        // the last batch: union positions straight into the lists
+        if (nq > 0) expandBatch(true);
+        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
+        // entries written early as candidate indices -> union positions (ascending either way); batches of 8 list
+        // words, the 8 loads issued together (one L2 round trip per batch)
+        if (__ballot(nEarly > 0))
         {
-            uint32_t v[kRB];
-#pragma unroll
-            for (int u = 0; u < kRB; ++u)
-                v[u] = (k0 + u < nwl) ? ll[(size_t)(k0 + u) * kWave] : 0u;
-#pragma unroll
-            for (int u = 0; u < kRB; ++u)
+            const uint32_t nwl = (nEarly + 1) >> 1;
+            constexpr int  kRB = 8;
+            for (uint32_t k0 = 0; k0 < nwl; k0 += kRB)
             {
-                const uint32_t k = k0 + u;
-                if (k < nwl)
+                uint32_t v[kRB];
+#pragma unroll
+                for (int u = 0; u < kRB; ++u)
+                    v[u] = (k0 + u < nwl) ? ll[(size_t)(k0 + u) * kWave] : 0u;
+#pragma unroll
+                for (int u = 0; u < kRB; ++u)
                 {
-                    const uint32_t lo = bitRank(s_bits, s_pre, v[u] & 0xffffu);
-                    const uint32_t hp = (2 * k + 1 < stored) ? bitRank(s_bits, s_pre, v[u] >> 16) : 0u;
-                    ll[(size_t)k * kWave] = lo | (hp << 16);
+                    const uint32_t k = k0 + u;
+                    if (k < nwl)
+                    {
+                        const uint32_t lo = bitRank(s_bits, s_pre, v[u] & 0xffffu);
+                        const uint32_t hp = (2 * k + 1 < nEarly) ? bitRank(s_bits, s_pre, v[u] >> 16) : (v[u] >> 16);
+                        ll[(size_t)k * kWave] = lo | (hp << 16);
+                    }
                 }
             }
         }
         if (threadIdx.x == 0) a.ucount[c] = ucnt;
     }
 
-#ifdef SX_NS_PROFILE
-    prof[4] = __builtin_readcyclecounter() - tU;
-    if (lane == 0)
-        for (int q = 0; q < 6; ++q)
-            atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 12 + 2 * q), (unsigned long long)prof[q]);
-#endif
     if (valid)
     {
         a.nc[i] = count + 1;
@@ -813,7 +813,8 @@ findNeighborsKernel(NsArgs a)
         t.w          = local ? ucnt : 0u;
         a.clStats[c] = t;
     }
-    __syncthreads(); // LDS is reused by the next cluster of a persistent launch
+    __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
+    c = s_next;
     }
 }
 
@@ -851,20 +852,46 @@ __global__ void importKernel(uint32_t* nidx, uint32_t first, uint32_t last, uint
         nidx[((size_t)g * ngmax + k) * kWave + lane] = in[(size_t)ni * ngmax + k];
 }
 
-//! this build's search over [first, last); grid 0: one workgroup per cluster, else a persistent grid of that size
-hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, unsigned grid)
+//! workgroups of this build resident on the whole chip (occupancy x CUs): the persistent grid of one search
+unsigned searchGrid()
+{
+    static unsigned grid = 0;
+    if (!grid)
+    {
+        int dev = 0, cus = 256, perCu = 1;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, findNeighborsKernel, kCluster, 0);
+        grid = (unsigned)std::max(1, cus) * (unsigned)std::max(1, perCu);
+#ifdef SX_NS_GRIDMUL
+        grid *= SX_NS_GRIDMUL;
+#endif
+        if (getenv("SX_NS_DEBUG_GRID")) fprintf(stderr, "search grid %u (%d per CU)\n", grid, perCu);
+    }
+    return grid;
+}
+
+//! hit-mask scratch of this build's persistent grid
+size_t searchScratchWords() { return (size_t)searchGrid() * kClusterWaves * kBatch * kWave; }
+
+//! this build's search over [first, last): a persistent grid taking clusters from the work counters a.work[0..8)
+//! (zeroed by the caller on the stream)
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
     const unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    findNeighborsKernel<<<grid ? std::min(grid, clusters) : clusters, kCluster, 0, s>>>(a);
+    findNeighborsKernel<<<std::min(searchGrid(), clusters), kCluster, 0, s>>>(a);
     return hipGetLastError();
 }
 
 #ifndef SX_NS_SMALL
 namespace small
 {
-hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s, unsigned grid);
-}
+hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s);
+size_t     searchScratchWords();
+} // namespace small
+
+size_t searchScratchBytes() { return std::max(searchScratchWords(), small::searchScratchWords()) * sizeof(uint64_t); }
 
 //! after the compact build: if it overflowed (stats bits 2 / 4), restore the saved h of its range
 __global__ void fallbackRestoreKernel(float* h, const float* hSave, uint32_t n, const uint32_t* stats)
@@ -920,26 +947,29 @@ static hipError_t reduceClusterStats(const NsArgs& a, hipStream_t s)
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
+    hipError_t e;
+    // work counters: [0, 8) the first launch, [8, 16) the fallback launch
+    if ((e = hipMemsetAsync(a.work, 0, 16 * sizeof(uint32_t), s))) return e;
     const int mode = a.policy ? a.policy->mode : 1;
     if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge()))
     {
-        if (hipError_t e = findNeighborsOnce(a, s, 0)) return e;
+        if ((e = findNeighborsOnce(a, s))) return e;
         return reduceClusterStats(a, s);
     }
     const uint32_t n = a.last - a.first;
-    hipError_t     e;
     if (a.iterateH &&
         (e = hipMemcpyAsync(a.hSave, a.h + a.first, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s)))
         return e;
     NsArgs c = a;
     c.forceOverflow = mode == 3;
-    if ((e = small::findNeighborsOnce(c, s, 0))) return e;
+    if ((e = small::findNeighborsOnce(c, s))) return e;
     if (a.iterateH)
         fallbackRestoreKernel<<<std::min(2048u, (n + 255) / 256), 256, 0, s>>>(a.h + a.first, a.hSave, n, a.stats);
     fallbackGateKernel<<<1, 64, 0, s>>>(a.stats);
     NsArgs b = a;
     b.gate   = a.stats + 10;
-    if ((e = findNeighborsOnce(b, s, 2048))) return e;
+    b.work   = a.work + 8;
+    if ((e = findNeighborsOnce(b, s))) return e;
     return reduceClusterStats(a, s);
 }
 #endif

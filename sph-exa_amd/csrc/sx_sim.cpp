@@ -745,9 +745,11 @@ __global__ void classifyClustersKernel(const uint32_t* uni, const uint32_t* ucou
     const uint32_t c    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     if (c >= numClusters) return;
-    const uint32_t  U = ucount[c];
+    // an overflowed union (ucount > ucap, stats bit 8, reported as an error after the step) is only partly stored:
+    // read what is there and treat the cluster as boundary
+    const uint32_t  U = min(ucount[c], ucap);
     const uint32_t* u = uni + (size_t)c * ucap;
-    bool            halo = false;
+    bool            halo = ucount[c] > ucap;
     for (uint32_t k = lane; k < U; k += 64)
     {
         const uint32_t j = u[k];
@@ -1526,14 +1528,15 @@ extern "C"
             na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(1, s->last - s->first));
             na.policy         = &s->nsPolicy;
             na.clStats        = s->mem.get<uint4>("ns.clstats", (na.numGroups + kClusterWaves - 1) / kClusterWaves);
-            if (!na.hSave || !na.clStats) return SX_ERR_NOMEM;
+            na.work           = s->mem.get<uint32_t>("ns.work", 16);
+            na.hitMasks       = s->mem.get<uint64_t>("ns.masks", searchScratchBytes() / sizeof(uint64_t));
+            if (!na.hSave || !na.clStats || !na.work || !na.hitMasks) return SX_ERR_NOMEM;
             if (const char* reps = getenv("SX_SEARCH_REPS"); reps && attempt == 0)
             {
-                // timing hook for search experiments (scripts/ab_search.sh): the search without the h iteration,
-                // repeated on this step's state before the real search; experiment bits from SX_SEARCH_EXP
+                // timing hook for search A/B runs (scripts/ab_search.sh): the search without the h iteration,
+                // repeated on this step's state before the real search
                 NsArgs x     = na;
                 x.iterateH   = 0;
-                x.experiment = getenv("SX_SEARCH_EXP") ? atoi(getenv("SX_SEARCH_EXP")) : 0;
                 NsPolicy pol;
                 pol.mode = getenv("SX_SEARCH_LARGE") ? 1 : 2; // compact build first (as in the real search)
                 x.policy = &pol;
@@ -1548,7 +1551,7 @@ extern "C"
                 SIM_HIP(hipEventSynchronize(s->kev[1]));
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, s->kev[0], s->kev[1]);
-                fprintf(stderr, "search-reps exp %d: %.3f ms per search (%d reps)\n", x.experiment, ms / R, R);
+                fprintf(stderr, "search-reps: %.3f ms per search (%d reps)\n", ms / R, R);
             }
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
@@ -1792,17 +1795,6 @@ extern "C"
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         s->lastStats.build         = s->nsPolicy.lastBuild;
-#ifdef SX_NS_PROFILE
-        {
-            const uint64_t* pr = reinterpret_cast<const uint64_t*>(s->statsHost + 12);
-            const double nwv = (double)((s->last - s->first) / 64);
-            fprintf(stderr,
-                    "nsprof cycles/wave: candidates %.0f stream %.0f tests %.0f post-test %.0f union %.0f; chunks/wave "
-                    "%.1f exact %.2f%%\n",
-                    pr[0] / nwv, pr[1] / nwv, pr[2] / nwv, pr[3] / nwv, pr[4] / nwv, (pr[5] & 0xffffffffu) / nwv,
-                    100.0 * (pr[5] >> 32) / std::max(1.0, (double)(pr[5] & 0xffffffffu)));
-        }
-#endif
         if (s->statsHost[0] & 1u)
         {
             fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 queue/candidate leaves, "

@@ -226,9 +226,10 @@ struct NsArgs
     NsPolicy*       policy;
     const uint32_t* gate; // set by findNeighbors for the fallback launch: the kernel runs only if *gate != 0
     int             forceOverflow; // compact build only: report a capacity overflow for every cluster (mode 3)
-    int             experiment;    // search-cost experiments of the SX_SEARCH_REPS timing hook (sx_sim.cpp), 0 in
-                                   // every real search: 1 no list append, 2 no union rewrite, 4 no distance test,
-                                   // 8 no candidate stream, 16 no tree walk
+    // persistent-grid state (findNeighbors sets up both): 16 work counters (8 XCD ranges per launch) and the
+    // per-workgroup hit-mask scratch, searchScratchBytes() bytes
+    uint32_t*       work;
+    uint64_t*       hitMasks;
 
     void setLists(const NbLists& L)
     {
@@ -277,6 +278,8 @@ hipError_t spatialGroups(Arena& arena, uint32_t first, uint32_t last, const doub
                          const DevBox& b, float tolFactor, uint32_t* groups, uint32_t cap, uint32_t* numGroups,
                          hipStream_t s);
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
+//! bytes of NsArgs::hitMasks the search needs (both builds' persistent grids)
+size_t     searchScratchBytes();
 //! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);
 hipError_t importNeighbors(uint32_t* nidx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in,

@@ -501,17 +501,39 @@ class Sim:
         (reference_attributes: ParticlesData::loadOrStoreAttributes, particles_data.hpp:142-193, and
         Box::loadOrStore, box.hpp:168-175), as an .npz (HDF5/H5Part is not in this image)"""
         st = self.get(self.CONSERVED)
-        attrs = reference_attributes(self.params, self.box, self.scalars(), self.iteration,
-                                     self.size() if num_particles_global is None else num_particles_global)
+        if num_particles_global is None:
+            num_particles_global = self.size()
+            comm = getattr(self, "comm", None)
+            if comm is not None and comm.size > 1:  # numParticlesGlobal is the sum over the ranks
+                import torch
+                import torch.distributed as dist
+
+                t = torch.tensor([num_particles_global], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                num_particles_global = int(t.item())
+        attrs = reference_attributes(self.params, self.box, self.scalars(), self.iteration, num_particles_global)
         np.savez(path, **st, **attrs)
 
+    # attributes ParticlesData::loadOrStoreAttributes restores (particles_data.hpp:170-190) that are parameters of
+    # this Sim (fixed at sx_sim_create): a restart must run with the stored values
+    PARAM_ATTRIBUTES = ["ng0", "ngmax", "Kcour", "Krho", "gravConstant", "gamma", "eps", "etaAcc", "muiConst",
+                        "alphamin", "alphamax", "decay_constant"]
+
     def load_checkpoint(self, path):
-        """continue from save_checkpoint's file: set_state with the saved fields and time-steps; returns the time"""
+        """continue from save_checkpoint's file: set_state with the saved fields and time-steps; returns the time.
+        The stored parameters must equal this Sim's (ValueError otherwise: the reference would load them, a Sim's
+        parameters are fixed at creation).  Files of the earlier format (time under 'ttot', no 'iteration') load
+        with iteration 0."""
         with np.load(path, allow_pickle=False) as d:
+            mine = reference_attributes(self.params, self.box, {"ttot": 0.0, "minDt": 0.0, "minDt_m1": 0.0}, 0, 0)
+            bad = [k for k in self.PARAM_ATTRIBUTES if k in d.files and d[k] != mine[k]]
+            if bad:
+                raise ValueError("restart file parameters differ from this Sim's: " +
+                                 ", ".join(f"{k}={d[k]!r} (Sim: {mine[k]!r})" for k in bad))
             st = {k: d[k] for k in self.CONSERVED}
             self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
-            self.iteration = int(d["iteration"])
-            return float(d["time"])
+            self.iteration = int(d["iteration"]) if "iteration" in d.files else 0
+            return float(d["time"] if "time" in d.files else d["ttot"])
 
     def step(self):
         rc = self.L.sx_sim_step(self.h)

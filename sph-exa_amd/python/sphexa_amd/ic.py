@@ -31,7 +31,8 @@ def _fields(n):
 
 
 def noh(side):
-    """Noh implosion (noh_init.hpp:46-100 field values): lattice cut to r <= 0.5, v = -r_hat, T = 1e-20/cv, dt0 = 1e-4,
+    """Noh implosion (noh_init.hpp:46-100 field values): lattice cut to r <= 0.5, v = -r_hat, x_m1 = v dt0,
+    T = 1e-20/cv, dt0 = 1e-4,
     open box.  Returns (arrays, box limits, boundary, dt0)."""
     r = 0.5
     x, y, z = _lattice(side, r)
@@ -46,6 +47,10 @@ def noh(side):
     f["m"][:] = np.float32(1.0 / n)
     inv = np.where(rad > 0, 1.0 / np.maximum(rad, 1e-300), 0.0)
     f["vx"][:], f["vy"][:], f["vz"][:] = -x * inv, -y * inv, -z * inv
+    # the integrator's previous displacement x_m1 = v * minDt (noh_init.hpp:96-98): the first positionUpdate takes
+    # the velocity from dX_n / dt_m1 (positions.hpp:77-88), so x_m1 = 0 would stop the inflow
+    for d in ("x", "y", "z"):
+        f[d + "_m1"][:] = (f["v" + d].astype(np.float64) * 1e-4).astype(np.float32)
     f["temp"] = np.full(n, 1e-20 / np.float64(ideal_gas_cv()))
     lo, hi = -0.5 - 1e-3, 0.5 + 1e-3
     return f, [lo, hi, lo, hi, lo, hi], [0, 0, 0], 1e-4

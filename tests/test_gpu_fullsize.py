@@ -1,29 +1,37 @@
-"""Full-size property test on the metric's own configuration: Sedov -n 400 (64M particles) on ONE MI355X.
+"""Full-size property tests on every single-GPU BASELINE configuration (BASELINE.json `configs`).
 
-The oracle cannot run 64M particles in test time, so this checks size-independent properties of the GPU path on
-the full problem (BASELINE.json metric, `main/src/init/sedov_init.hpp:106-130` IC):
-  * every particle of the periodic lattice has the same neighborhood: nc == 93 (92 neighbors + self, the value the
-    oracle gives at n=50, test_gpu_parity.py::test_sedov_n50_energy_and_counts) after the first step's h iteration,
-  * no search capacity error, no non-converged h, ids remain a permutation of 0..n-1 after two SFC re-sorts,
-  * total energy (computeConservedQuantities) drifts < 1e-6 over two steps.
+The oracle cannot run millions of particles in test time, so these check size-independent properties of the GPU path
+on the full problems:
+  * Sedov -n 400 (64M, the metric's workload) and -n 200 (8M, config 2), `main/src/init/sedov_init.hpp:106-130` IC:
+    every particle of the periodic lattice has the same neighborhood, nc == 93 (92 neighbors + self, the value the
+    oracle gives at n=50, test_gpu_parity.py::test_sedov_n50_energy_and_counts) after the first step's h iteration;
+    no search capacity error, no non-converged h; ids remain a permutation of 0..n-1 after the SFC re-sorts; total
+    energy (computeConservedQuantities) drifts < 1e-6 over two steps.
+  * Noh -n 300 (config 3, 14.1M particles in the sphere; lattice substitute for the glass block, SURVEY F6;
+    `noh_init.hpp:46-152` field values): no error flag, no non-converged h, every nc inside the h-iteration window
+    [ng0/4, ngmax+1] (stored lists never beyond ngmax), total energy drift < 1e-6 over two steps (the AV converts
+    kinetic into internal energy, the sum is conserved to the integrator's order).
+  * Evrard -n 300 with self-gravity (config 5 on one GPU, `evrard_init.hpp:50-190` field values): no error flag, the
+    potential energy is the Barnes-Hut potential of the state (finite, negative, within 1 % of the analytic
+    -3/(2(5-n)) G M^2 / R = -2/3 of the initial 1/r sphere), and total energy including egrav conserved over two
+    steps to 1e-5 (the tree's opening-angle error enters the potential as a near-constant offset, not as drift).
 """
 import numpy as np
 import pytest
 
 import sphexa_amd as sx
+from sphexa_amd import ic
 
 pytestmark = pytest.mark.gpu
 
-SIDE = 400
 
-
-def test_sedov_n400_two_steps_one_gpu():
-    n = SIDE ** 3
+def _sedov(side):
+    n = side ** 3
     ctx = sx.Context(0)
     box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
     sim = sx.Sim(ctx, n, box)
     try:
-        sim.init_sedov(SIDE)
+        sim.init_sedov(side)
         e0 = sim.conserved()
         sim.step()
         st = sim.stats()
@@ -39,6 +47,74 @@ def test_sedov_n400_two_steps_one_gpu():
         assert np.array_equal(ids, np.arange(n, dtype=np.uint64))
         h = sim.get(["h"])["h"]
         assert np.all(np.isfinite(h)) and np.all(h > 0)
+    finally:
+        sim.close()
+        ctx.close()
+
+
+def test_sedov_n400_two_steps_one_gpu():
+    _sedov(400)
+
+
+def test_sedov_n200_two_steps_one_gpu():
+    _sedov(200)
+
+
+def _from_ic(init, side, g=0.0):
+    arrays, lim, bnd, dt0 = getattr(ic, init)(side)
+    n = arrays["x"].size
+    ctx = sx.Context(0)
+    sim = sx.Sim(ctx, n, sx.make_box(lim, bnd), params=sx.default_params(g=g))
+    sim.set_state(arrays, dt0, dt0)
+    return ctx, sim, n
+
+
+def _check_counts(sim, n):
+    st = sim.stats()
+    assert st["numFailed"] == 0, st
+    nc = sim.get(["nc"])["nc"].astype(np.int64)
+    assert nc.size == n
+    assert nc.min() >= 100 // 4 and nc.max() <= 151, (nc.min(), nc.max())
+    assert st["maxNeighbors"] <= 150
+    return st
+
+
+def test_noh_n300_two_steps_one_gpu():
+    ctx, sim, n = _from_ic("noh", 300)
+    try:
+        assert 14_000_000 < n < 14_200_000
+        e0 = sim.conserved()
+        sim.step()
+        _check_counts(sim, n)
+        sim.step()
+        _check_counts(sim, n)
+        e2 = sim.conserved()
+        assert abs(e2["etot"] / e0["etot"] - 1) < 1e-6, (e0, e2)
+        ids = np.sort(sim.get(["id"])["id"])
+        assert np.array_equal(ids, np.arange(n, dtype=np.uint64))
+        f = sim.get(["h", "temp"])
+        assert np.all(np.isfinite(f["h"])) and np.all(f["h"] > 0) and np.all(np.isfinite(f["temp"]))
+    finally:
+        sim.close()
+        ctx.close()
+
+
+def test_evrard_n300_gravity_two_steps_one_gpu():
+    ctx, sim, n = _from_ic("evrard", 300, g=1.0)
+    try:
+        sim.step()
+        _check_counts(sim, n)
+        e1 = sim.conserved()
+        # M = 1, R = 1, rho ~ 1/r: W = -G M^2 / R * 3 / (2 (5 - 1)) ... for a density power law rho ~ r^-a the
+        # potential energy is -(3 - a)/(5 - 2a) G M^2 / R = -2/3 for a = 1
+        assert np.isfinite(e1["egrav"]) and abs(e1["egrav"] / (-2.0 / 3.0) - 1) < 0.01, e1
+        sim.step()
+        sim.step()
+        _check_counts(sim, n)
+        e3 = sim.conserved()
+        assert abs(e3["etot"] / e1["etot"] - 1) < 1e-5, (e1, e3)
+        ids = np.sort(sim.get(["id"])["id"])
+        assert np.array_equal(ids, np.arange(n, dtype=np.uint64))
     finally:
         sim.close()
         ctx.close()
