@@ -17,6 +17,11 @@ domain.hpp:196-244) and the halo exchanges of HydroVeProp (main/src/propagator/v
   6. the five halo exchanges between the kernels (xm | v,prho,c,kx | c_ij,divv | alpha), global dt = min over
      ranks, positions + h update on the locals.
 
+With overlap=True each exchange is overlapped as sx_sim.cpp does it (classifyClustersKernel + the comm-stream
+exchanges): clusters of 256 SFC-consecutive locals whose neighbor union holds no halo are "interior" and are
+computed BEFORE the exchange, with the halo copies of the exchanged fields poisoned (NaN); the "boundary" clusters
+after it.  A wrong classification lets a NaN into an interior result, so overlap == serial bitwise is the check.
+
 The per-particle kernels are the plain-C oracle (sph_oracle.c) on [first, last) of the rank's arrays.
 """
 import math
@@ -69,9 +74,12 @@ def _fold(d, box, k):
 class DistOracle:
     """one rank of the decomposed oracle; `local` is a po.HostState with this rank's particles"""
 
-    def __init__(self, ora, box, local, bucket=64):
+    CLUSTER = 256  # targets sharing one neighbor union (sx_device.hpp kCluster)
+
+    def __init__(self, ora, box, local, bucket=64, overlap=False):
         dist = _dist()
-        self.ora, self.box, self.bucket = ora, box, bucket
+        self.ora, self.box, self.bucket, self.overlap = ora, box, bucket, overlap
+        self.cluster_counts = [0, 0]  # interior, boundary clusters of the last step
         self.rank, self.size = dist.get_rank(), dist.get_world_size()
         self.local = local
         self.p = ora.params()
@@ -181,6 +189,42 @@ class DistOracle:
                     a[o:o + c] = recv[pos:pos + c]
                 pos += c
 
+    def _classify(self, nbr, nc, f, l):
+        """interior / boundary clusters as (c0, c1) target ranges (classifyClustersKernel, sx_sim.cpp)"""
+        ng = self.p.ngmax
+        inner, bound = [], []
+        for c0 in range(f, l, self.CLUSTER):
+            c1 = min(l, c0 + self.CLUSTER)
+            halo = False
+            for i in range(c0, c1):
+                cnt = min(int(nc[i - f]) - 1, ng)
+                row = nbr[(i - f) * ng:(i - f) * ng + cnt]
+                if cnt and (row.min() < f or row.max() >= l):
+                    halo = True
+                    break
+            (bound if halo else inner).append((c0, c1))
+        self.cluster_counts = [len(inner), len(bound)]
+        return inner, bound
+
+    def _phase(self, fields, kern, nbr, f, l):
+        """exchange `fields`, then run kern(nbr rows, first, last) on the locals; with overlap: interior clusters
+        first against poisoned halo copies, then the exchange, then the boundary clusters"""
+        if not self.overlap:
+            if fields:
+                self.halo_exchange(fields)
+            kern(nbr, f, l)
+            return
+        full, ng = self.full, self.p.ngmax
+        for name in fields:
+            full.arrays[name][:f] = np.nan
+            full.arrays[name][l:] = np.nan
+        for c0, c1 in self.interior:
+            kern(nbr[(c0 - f) * ng:], c0, c1)
+        if fields:
+            self.halo_exchange(fields)
+        for c0, c1 in self.boundary:
+            kern(nbr[(c0 - f) * ng:], c0, c1)
+
     # ---- one VE step (ve_hydro.hpp:132-218) ---------------------------------------------------------------------
     def step(self):
         import torch
@@ -208,17 +252,24 @@ class DistOracle:
             self.halo_retries += 1
         else:
             raise RuntimeError("halo discovery did not converge")
+        if self.overlap:
+            self.interior, self.boundary = self._classify(nbr, nc, f, l)
         ora.xmass(full, box, nbr, f, l)
-        self.halo_exchange(["xm"])
-        ora.ve_def_gradh(full, box, nbr, f, l)
+        self._phase(["xm"], lambda nb, a, b: ora.ve_def_gradh(full, box, nb, a, b), nbr, f, l)
         ora.eos(full, f, l)
-        self.halo_exchange(["vx", "vy", "vz", "prho", "c", "kx"])
-        ora.iad_divv_curlv(full, box, nbr, f, l)
+        self._phase(["vx", "vy", "vz", "prho", "c", "kx"], lambda nb, a, b: ora.iad_divv_curlv(full, box, nb, a, b),
+                    nbr, f, l)
         max_divv = float(np.max(full.divv[f:l])) if l > f else -math.inf
-        self.halo_exchange(["c11", "c12", "c13", "c22", "c23", "c33", "divv"])
-        ora.av_switches(full, box, nbr, f, l)
-        self.halo_exchange(["alpha"])
-        ora.momentum_energy(full, box, nbr, f, l)
+        self._phase(["c11", "c12", "c13", "c22", "c23", "c33", "divv"],
+                    lambda nb, a, b: ora.av_switches(full, box, nb, a, b), nbr, f, l)
+        courant = []
+
+        def momentum(nb, a, b):
+            ora.momentum_energy(full, box, nb, a, b)
+            courant.append(full.minDtCourant)
+
+        self._phase(["alpha"], momentum, nbr, f, l)
+        full.minDtCourant = min(courant) if courant else math.inf
         # rhoTimestep + computeTimestep (ts_global.hpp:72-112) with the MPI_Allreduce(min) as a gloo all-reduce
         dt_rho = p.Krho / abs(max_divv) if max_divv != 0 else math.inf  # C: division by zero -> inf
         dt_loc = min(full.minDtCourant, dt_rho, p.maxDtIncrease * full.minDt)

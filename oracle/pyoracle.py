@@ -499,9 +499,10 @@ def conserved_quantities(st, first=0, last=None, mui=np.float32(10.0), gamma=5.0
 
 
 # ---- block time-step rung bookkeeping (numpy restatement of sph/include/sph/ts_rungs.hpp) -----------------------
-# ts_rungs.hpp includes <mpi.h>, which this image lacks, so oracle/_ref cannot compile it: this restatement is pinned
-# by the reference text (cited per line) and by hand-checked cases in tests/test_rungs_oracle.py, not by the
-# reference binary.
+# Only findRungRanges<false> of ts_rungs.hpp is host code: oracle/_ref compiles it (with the image's MPICH for the
+# header's <mpi.h>) and tests/test_rungs_oracle.py pins find_rung_ranges to it.  sortGroupDt / computeMinTimestep /
+# rungTimestep / minimumGroupDt call GPU-only primitives (cstone::sortByKeyGpu, sequenceGpu, memcpyD2H from the
+# reference's CUDA sources): their restatement is pinned by the reference text (cited per line) and hand cases.
 MAX_NUM_RUNGS = 4  # sph::Timestep::maxNumRungs (sph/timestep.h:42)
 
 

@@ -22,8 +22,11 @@
  *       float du_m1 storage as a double.  The mock dataset below gives `du` a by-value element access, so
  *       `Tdu` becomes `double` and the reference loop runs unmodified but correct (GPU semantics,
  *       positions_gpu.cu:160-163).
- *   MPI: computeTimestep (ts_global.hpp:97-112) and rhoTimestep (:72-94) live in a header that includes
- *       <mpi.h>; the single-rank arithmetic of both is restated in ref_step (no MPI library is linked).
+ *   MPI: computeTimestep (ts_global.hpp:97-112) and rhoTimestep (:72-94) live in a header that includes <mpi.h>.
+ *       The parity build (SX_REF_MPI, oracle/Makefile) compiles that header against the image's MPICH
+ *       (/opt/conda/include, single-rank MPI_Init) and ref_step calls both as they are; the timing build
+ *       (libsphexa_ref_fast.so, bench.py's cpu_baseline on the GPU box) restates their single-rank arithmetic, so
+ *       it loads without an MPI runtime.  ref_rho_timestep / ref_compute_timestep expose them to the tests.
  *   Domain::sync (single rank) is restated as: Hilbert keys -> sort_by_key -> reorder -> fully converged
  *       cornerstone tree (bucket 64) -> buildOctreeCpu -> nodeFpCenters -> layout. The reference's focus tree
  *       converges incrementally over steps; neighbor *sets* do not depend on the tree, only their order.
@@ -57,6 +60,11 @@
 #include "sph/positions.hpp"
 #include "sph/sph_kernel_tables.hpp"
 #include "sph/update_h.hpp"
+#ifdef SX_REF_MPI
+#include "cstone/primitives/mpi_wrappers.hpp" // MpiType, used unqualified by ts_global.hpp
+#include "sph/ts_global.hpp"
+#include "sph/ts_rungs.hpp" // findRungRanges<false> is host code; the rest of the file needs GPU primitives
+#endif
 
 #include "ryoanji/nbody/traversal_cpu.hpp"
 #include "ryoanji/nbody/upsweep_cpu.hpp"
@@ -115,6 +123,7 @@ struct MockData
     double   K{0};
     double   minDt{1e-6}, minDt_m1{1e-6}, minDtCourant{INFINITY}, minDtRho{INFINITY};
     double   Kcour{0.2}, Krho{0.06}, gamma{5.0 / 3.0}, sincIndex{6.0};
+    double   ttot{0}, g{0}, maxDtIncrease{1.1}, etaAcc{0.2}, eps{0.005}; // computeTimestep (ts_global.hpp:97-112)
     float    muiConst{10.0};
     T        alphamin{0.05}, alphamax{1.0}, decay_constant{0.2};
     T        Atmin{0.1}, Atmax{0.2}, ramp{1.0 / (0.2 - 0.1)};
@@ -138,6 +147,16 @@ cstone::Box<double> makeBox(const ox_box* b)
 }
 
 std::vector<float> g_wh, g_whd;
+
+#ifdef SX_REF_MPI
+//! single-rank MPI for the reference's global time-step (MPICH singleton init)
+void refMpiInit()
+{
+    int on = 0;
+    MPI_Initialized(&on);
+    if (!on) MPI_Init(nullptr, nullptr);
+}
+#endif
 double             g_K = 0;
 
 void ensureTables()
@@ -591,6 +610,9 @@ extern "C"
             sph::computeVeDefGradhImpl(0, n, d, box);
             sph::computeEOS_Impl(0, n, d);
             sph::computeIadDivvCurlvImpl(0, n, d, box);
+#ifdef SX_REF_MPI
+            d.minDtRho = sph::rhoTimestep(0, n, d);
+#else
             {   // rhoTimestep (ts_global.hpp:72-94), single rank
                 float maxDivv = -INFINITY;
 #pragma omp parallel for reduction(max : maxDivv)
@@ -598,6 +620,7 @@ extern "C"
                     maxDivv = std::max(s->divv[i], maxDivv);
                 d.minDtRho = d.Krho / std::abs(maxDivv);
             }
+#endif
             sph::computeAVswitchesImpl(0, n, d, box);
             if (p->avClean) sph::computeMomentumEnergyImpl<true>(0, n, d, box);
             else sph::computeMomentumEnergyImpl<false>(0, n, d, box);
@@ -607,6 +630,18 @@ extern "C"
         {
             // mHolder_.upsweep + traverse (ve_hydro.hpp:193-202), accelerationTimestep (ts_global.hpp:47-67)
             s->egrav = gravityOnTree(s, p, box, t, 0, unsigned(n), nullptr, nullptr, 0);
+        }
+#ifdef SX_REF_MPI
+        refMpiInit();
+        d.g      = p->g;
+        d.etaAcc = p->etaAcc;
+        d.eps    = p->eps;
+        d.ttot   = s->ttot;
+        sph::computeTimestep(0, n, d);
+        s->ttot = d.ttot;
+#else
+        if (p->g != 0.0)
+        {
             double maxAccSq = 0.0;
             for (size_t i = 0; i < n; ++i)
             {
@@ -621,6 +656,7 @@ extern "C"
         s->ttot += minDtLoc;
         d.minDt_m1 = d.minDt;
         d.minDt    = minDtLoc;
+#endif
         sph::updatePositionsHost(0, n, d, box);
         sph::updateTempHost(0, n, d);
         sph::updateSmoothingLengthCpu(0, n, d.ng0, s->nc, s->h);
@@ -730,4 +766,38 @@ extern "C"
                                   wh.data(), whd.data());
     }
 
+#ifdef SX_REF_MPI
+    /*! sph::rhoTimestep (ts_global.hpp:72-94) on n divv values: Krho / |max divv| */
+    double ref_rho_timestep(const float* divv, size_t n, double Krho)
+    {
+        MockData<float> d;
+        d.divv = PtrVec<float>{const_cast<float*>(divv), n};
+        d.Krho = Krho;
+        return sph::rhoTimestep(0, n, d);
+    }
+
+    /*! sph::computeTimestep (ts_global.hpp:97-112, MPI_Allreduce over one rank) with accelerationTimestep
+     *  (:47-67) when g != 0.  io[0..6] = minDt, minDt_m1, ttot, minDtCourant, minDtRho, g, maxDtIncrease (in),
+     *  minDt, minDt_m1, ttot updated in place */
+    void ref_compute_timestep(double* io, const float* ax, const float* ay, const float* az, size_t n, double etaAcc,
+                              double eps)
+    {
+        refMpiInit();
+        MockData<float> d;
+        d.ax = PtrVec<float>{const_cast<float*>(ax), n};
+        d.ay = PtrVec<float>{const_cast<float*>(ay), n};
+        d.az = PtrVec<float>{const_cast<float*>(az), n};
+        d.minDt = io[0], d.minDt_m1 = io[1], d.ttot = io[2], d.minDtCourant = io[3], d.minDtRho = io[4];
+        d.g = io[5], d.maxDtIncrease = io[6], d.etaAcc = etaAcc, d.eps = eps;
+        sph::computeTimestep(0, n, d);
+        io[0] = d.minDt, io[1] = d.minDt_m1, io[2] = d.ttot;
+    }
+    /*! sph::findRungRanges<false> (ts_rungs.hpp:116-130) on ascending groupDt: out[0..maxNumRungs] */
+    void ref_find_rung_ranges(float minDt, const float* groupDt, uint32_t numGroups, int numRungs, uint32_t* out)
+    {
+        auto r = sph::findRungRanges<false>(minDt, groupDt, numGroups, numRungs);
+        for (size_t k = 0; k < r.size(); ++k)
+            out[k] = r[k];
+    }
+#endif
 } // extern "C"

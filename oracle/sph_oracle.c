@@ -1973,6 +1973,42 @@ double ox_acc_timestep(const ox_state* s, const ox_params* p, unsigned first, un
     return p->etaAcc * sqrt(p->eps / sqrt(maxAccSq));
 }
 
+/* rhoTimestep (ts_global.hpp:72-94): Krho / |max divv| over n values (float max, double quotient) */
+double ox_rho_timestep(const float* divv, size_t n, double Krho)
+{
+    float maxDivv = -INFINITY;
+#pragma omp parallel for reduction(max : maxDivv)
+    for (size_t i = 0; i < n; ++i)
+        maxDivv = divv[i] > maxDivv ? divv[i] : maxDivv;
+    return Krho / fabs((double)maxDivv);
+}
+
+/* computeTimestep (ts_global.hpp:97-112), one rank: min of the acceleration (g != 0), Courant, rho and growth
+ * limits; io[0..6] = minDt, minDt_m1, ttot, minDtCourant, minDtRho, g, maxDtIncrease, the first three updated */
+void ox_compute_timestep(double* io, const float* ax, const float* ay, const float* az, size_t n, double etaAcc,
+                         double eps)
+{
+    double minDtAcc = INFINITY;
+    if (io[5] != 0.0)
+    {
+        double maxAccSq = 0.0;
+        for (size_t i = 0; i < n; ++i)
+        {
+            double x = ax[i], y = ay[i], z = az[i];
+            double a2 = x * x + (y * y + z * z);
+            maxAccSq  = a2 > maxAccSq ? a2 : maxAccSq;
+        }
+        minDtAcc = etaAcc * sqrt(eps / sqrt(maxAccSq));
+    }
+    double minDtLoc = INFINITY;
+    double cand[4]  = {minDtAcc, io[3], io[4], io[6] * io[0]};
+    for (int k = 0; k < 4; ++k)
+        minDtLoc = cand[k] < minDtLoc ? cand[k] : minDtLoc;
+    io[2] += minDtLoc;
+    io[1] = io[0];
+    io[0] = minDtLoc;
+}
+
 typedef struct
 {
     uint64_t key;
@@ -2050,34 +2086,23 @@ int ox_step(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket)
         ox_ve_def_gradh(s, p, b, nbr, 0, (unsigned)n);
         ox_eos(s, p, 0, (unsigned)n);
         ox_iad_divv_curlv(s, p, b, nbr, 0, (unsigned)n);
-        float maxDivv = -INFINITY;
-#pragma omp parallel for reduction(max : maxDivv)
-        for (size_t i = 0; i < n; ++i)
-            maxDivv = s->divv[i] > maxDivv ? s->divv[i] : maxDivv;
-        s->minDtRho = p->Krho / fabs((double)maxDivv);
+        s->minDtRho = ox_rho_timestep(s->divv, n, p->Krho);
         ox_av_switches(s, p, b, nbr, 0, (unsigned)n);
         ox_momentum_energy(s, p, b, nbr, 0, (unsigned)n);
     }
-    double minDtAcc = INFINITY;
     if (p->g != 0.0)
     {
-        /* mHolder_.upsweep + traverse (ve_hydro.hpp:193-202) on the same tree, then accelerationTimestep */
+        /* mHolder_.upsweep + traverse (ve_hydro.hpp:193-202) on the same tree; accelerationTimestep below */
         double* c4 = (double*)calloc(4 * (size_t)t.nTot, sizeof(double));
         float*  mp = (float*)calloc(8 * (size_t)t.nTot, sizeof(float));
         grav_upsweep(s, &t, 1.0f / p->theta, c4, mp);
         s->egrav = grav_traverse(s, &t, c4, mp, (float)p->g, 0, (unsigned)n);
         free(c4);
         free(mp);
-        minDtAcc = ox_acc_timestep(s, p, 0, (unsigned)n);
     }
-
-    double minDtLoc = INFINITY;
-    double cand[4]  = {minDtAcc, s->minDtCourant, s->minDtRho, p->maxDtIncrease * s->minDt};
-    for (int k = 0; k < 4; ++k)
-        minDtLoc = cand[k] < minDtLoc ? cand[k] : minDtLoc;
-    s->ttot += minDtLoc;
-    s->minDt_m1 = s->minDt;
-    s->minDt    = minDtLoc;
+    double io[7] = {s->minDt, s->minDt_m1, s->ttot, s->minDtCourant, s->minDtRho, p->g, p->maxDtIncrease};
+    ox_compute_timestep(io, s->ax, s->ay, s->az, n, p->etaAcc, p->eps);
+    s->minDt = io[0], s->minDt_m1 = io[1], s->ttot = io[2];
     ox_positions(s, p, b, 0, (unsigned)n);
     ox_update_h_range(s, p->ng0, 0, (unsigned)n);
 

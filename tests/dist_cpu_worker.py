@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--side", type=int, default=16)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--gravity", action="store_true", help="only the multi-rank gravity of the IC (G = 1)")
+    ap.add_argument("--overlap", action="store_true", help="interior clusters before each halo exchange")
     args = ap.parse_args()
     import torch.distributed as dist
 
@@ -40,7 +41,7 @@ def main():
     for k in po.CONSERVED:
         local.arrays[k][:] = st.arrays[k][f:l]
     local.minDt, local.minDt_m1 = st.minDt, st.minDt_m1
-    d = do.DistOracle(po.load_oracle(), box, local)
+    d = do.DistOracle(po.load_oracle(), box, local, overlap=args.overlap)
     out = {}
     if args.gravity:
         full = d._discover(d._exchange_particles(d._sort(d.local)), do.HALO_MARGIN)
@@ -58,6 +59,7 @@ def main():
         out[f"s{s}_scalars"] = np.array([loc.minDt, loc.minDt_m1, loc.ttot])
         out[f"s{s}_layout"] = np.array([d.first, d.last, d.total, d.halo_retries])
         out[f"s{s}_split"] = d.split.astype(np.uint64)
+        out[f"s{s}_clusters"] = np.array(d.cluster_counts)
     np.savez(os.path.join(args.out, f"rank{args.rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()

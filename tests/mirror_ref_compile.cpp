@@ -7,7 +7,34 @@
  *  the reference's propagators pass (ve_hydro.hpp, ve_hydro_bdt.hpp, std_hydro.hpp).  Built by
  *  tests/test_mirror_compile.py with g++ -I<reference include dirs>; never run (no GPU is touched). */
 #include <cstdint>
+#include <memory>
 #include <vector>
+
+// GroupData<GpuTag>::data is a thrust::device_vector (traversal/groups.hpp:31-39).  Thrust is not in this image, so a
+// TEST-ONLY stand-in with the members the mirror touches (data().get(), size(), resize) takes its place; defining
+// THRUST_MAJOR_VERSION keeps cuda_stubs.h:59-66 from forward-declaring the real one.  It lets the mirror's
+// thrust branch of rawPtr (data().get()) compile against the seam's real GroupData<GpuTag> type.
+#define THRUST_MAJOR_VERSION 0
+namespace thrust
+{
+template<class T>
+struct device_ptr
+{
+    T* p;
+    T* get() const { return p; }
+};
+template<class T, class Alloc = std::allocator<T>>
+class device_vector
+{
+public:
+    device_ptr<T> data() { return {v_.data()}; }
+    size_t        size() const { return v_.size(); }
+    void          resize(size_t n) { v_.resize(n); }
+
+private:
+    std::vector<T, Alloc> v_;
+};
+} // namespace thrust
 
 #include "cstone/sfc/box.hpp"
 #include "cstone/traversal/groups.hpp"
@@ -41,10 +68,12 @@ struct Dataset
 };
 
 void instantiate(Dataset& d, const cstone::Box<double>& box, const cstone::GroupView& grp,
-                 cstone::GroupData<cstone::CpuTag>& groups, float* groupDt)
+                 cstone::GroupData<cstone::CpuTag>& groups, cstone::GroupData<cstone::GpuTag>& groupsGpu,
+                 float* groupDt)
 {
     auto& dv = d.devData;
     sph::computeSpatialGroups(0, 100, d, box, groups);
+    sph::computeSpatialGroups(0, 100, d, box, groupsGpu); // the seam's own type (sph_gpu.hpp:17)
     sph::cuda::computeXMass(grp, d, box);
     sph::cuda::computeDensity(grp, d, box);
     sph::cuda::computeVeDefGradh(grp, d, box);
@@ -82,8 +111,9 @@ int main(int argc, char**)
         cstone::Box<double>               box(0, 1, cstone::BoundaryType::periodic);
         cstone::GroupView                 grp{0, 100, 2, nullptr, nullptr};
         cstone::GroupData<cstone::CpuTag> groups;
+        cstone::GroupData<cstone::GpuTag> groupsGpu;
         float                             groupDt[2];
-        instantiate(d, box, grp, groups, groupDt);
+        instantiate(d, box, grp, groups, groupsGpu, groupDt);
     }
     return 0;
 }

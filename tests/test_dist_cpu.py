@@ -135,3 +135,22 @@ def test_decomposed_gravity_matches_direct_sum(tmp_path, nproc):
     for d in ranks:
         halos, far_cells, remote_cells = d["stats"]
         assert 0 < far_cells < remote_cells and halos > 0, d["stats"]
+
+
+@pytest.mark.parametrize("ic,side", [("sedov", 40), ("noh", 44)])
+def test_overlapped_exchanges_classification(tmp_path, ic, side):
+    """the interior/boundary cluster classification of the overlapped halo exchanges (sx_sim.cpp
+    classifyClustersKernel, exchange on a comm stream while interior clusters compute): restated on the CPU over gloo
+    (oracle/dist_oracle.py, overlap=True) with the halo copies of every exchanged field poisoned with NaN while the
+    interior clusters run.  Two ranks, two steps: bitwise equal to the serial exchanges, both classes non-empty."""
+    a = run_ranks(tmp_path / "serial", 2, side, 2, ic) if (tmp_path / "serial").mkdir() is None else None
+    b = run_ranks(tmp_path / "ovl", 2, side, 2, ic, ("--overlap",)) if (tmp_path / "ovl").mkdir() is None else None
+    for s in range(2):
+        for q in range(2):
+            inner, bound = b[q][f"s{s}_clusters"]
+            assert inner > 0 and bound > 0, (s, q, inner, bound)
+            for k in ["id", "nc", "h"] + FIELDS:
+                x, y = a[q][f"s{s}_{k}"], b[q][f"s{s}_{k}"]
+                assert np.array_equal(x, y), (s, q, k)
+                assert not np.any(np.isnan(y.astype(np.float64)))
+            assert np.array_equal(a[q][f"s{s}_scalars"], b[q][f"s{s}_scalars"])

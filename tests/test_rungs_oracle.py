@@ -1,8 +1,11 @@
 """The oracle's numpy restatement of the block time-step rung bookkeeping (sph/include/sph/ts_rungs.hpp:67-157,
-sph/groups.hpp:31-48) on hand-checked cases.  ts_rungs.hpp includes <mpi.h>, which this image lacks, so the
-reference cannot be compiled here (parity of this restatement is pinned by the reference text, cited per line in
-oracle/pyoracle.py, and by these cases)."""
+sph/groups.hpp:31-48) on hand-checked cases, and its findRungRanges against the reference's own (compiled into
+oracle/_ref).  The rest of ts_rungs.hpp (sortGroupDt, computeMinTimestep, rungTimestep, minimumGroupDt) runs only
+on the GPU in the reference: it calls cstone::sortByKeyGpu / sequenceGpu / memcpyD2H, defined in the reference's
+CUDA sources, and its host-vector branch leaves minGroupDt unset, so those parts are pinned by the reference text
+(cited per line in oracle/pyoracle.py) and by these cases."""
 import numpy as np
+import pytest
 
 import pyoracle as po
 
@@ -51,3 +54,28 @@ def test_extract_groups():
     ge = np.array([10, 20, 30, 35], np.uint32)
     s, e = po.extract_groups(gs, ge, np.array([3, 0, 2, 1], np.uint32), 1, 3)
     assert list(s) == [0, 20] and list(e) == [10, 30]
+
+
+@pytest.mark.ref
+@pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("seed", range(8))
+def test_find_rung_ranges_vs_reference(seed):
+    """findRungRanges<false> (ts_rungs.hpp:116-130) is host code: compiled from /root/reference into oracle/_ref (with
+    the image's MPICH for the header's <mpi.h>) and compared with the restatement on sorted random group time-steps,
+    including ties at the 2^r minDt boundaries"""
+    import ctypes as C
+
+    ref = C.CDLL(po.REF_SO)
+    f = ref.ref_find_rung_ranges
+    f.restype = None
+    f.argtypes = [C.c_float, C.POINTER(C.c_float), C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 3000))
+    dt = np.sort((10.0 ** rng.uniform(-6, -3, n)).astype(np.float32))
+    if seed % 2:  # exact multiples of minDt at the rung boundaries
+        dt[rng.integers(0, n, n // 4)] = dt[0] * np.float32(2 ** rng.integers(1, 4))
+        dt = np.sort(dt)
+    for num_rungs in range(1, po.MAX_NUM_RUNGS + 1):
+        out = np.zeros(po.MAX_NUM_RUNGS + 1, np.uint32)
+        f(float(dt[0]), dt.ctypes.data_as(C.POINTER(C.c_float)), n, num_rungs, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+        assert out.tolist() == po.find_rung_ranges(dt[0], dt, n, num_rungs)
