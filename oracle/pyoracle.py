@@ -372,7 +372,13 @@ class Lib:
         s = st.struct()
         f = getattr(self.lib, name)
         ptr = nbr.ctypes.data_as(C.POINTER(C.c_uint32))
+        errs = getattr(self.lib, "ox_list_errors", None)
+        if errs is not None:
+            errs.restype = C.c_ulonglong
+            self.lib.ox_clear_list_errors()
         r = f(C.byref(s), C.byref(p), C.byref(box), ptr, first, last)
+        if errs is not None and errs():
+            raise AssertionError(f"{name}: {errs()} neighbor-list entries outside [0, {st.n}) (list under test is bad)")
         st.pull(s)
         return r
 

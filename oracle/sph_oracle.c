@@ -788,6 +788,30 @@ static inline unsigned nc_capped(const uint32_t* nc, size_t i, unsigned ngmax)
     return v < ngmax ? v : ngmax;
 }
 
+/* Neighbor-list consumers check every index they are about to read against the state size first: a list exported
+ * from the GPU path under test is INPUT to this checker, so a bad index must fail the test (ox_list_errors() > 0,
+ * raised by pyoracle), not crash the process.  A kernel given a bad list computes nothing. */
+static unsigned long long g_listErrors = 0;
+
+unsigned long long ox_list_errors(void) { return g_listErrors; }
+void               ox_clear_list_errors(void) { g_listErrors = 0; }
+
+static int lists_ok(const ox_state* s, const uint32_t* neighbors, unsigned first, unsigned last, unsigned ngmax)
+{
+    unsigned long long bad = 0;
+#pragma omp parallel for reduction(+ : bad)
+    for (size_t i = first; i < last; ++i)
+    {
+        const unsigned  cnt = nc_capped(s->nc, i, ngmax);
+        const uint32_t* row = neighbors + (size_t)ngmax * (i - first);
+        for (unsigned k = 0; k < cnt; ++k)
+            bad += row[k] >= s->n ? 1 : 0;
+    }
+    if (s->n && last > s->n) bad += 1;
+    g_listErrors += bad;
+    return bad == 0;
+}
+
 /* Error scales of the neighbor sums (tests only): when registered by ox_set_scales, the J-loops also accumulate,
  * per particle, the magnitude of the terms their float sums are made of -- the scale of the rounding error of a
  * float sum in any order (SURVEY.md 8(c) tier 1).  a: L1 over the three components; dv: divv, curlv and dV;
@@ -822,6 +846,7 @@ static float xmassJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* n
 void ox_xmass(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
               unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; i++)
@@ -882,6 +907,7 @@ static void veDefGradhJLoop(uint32_t i, double K, const ox_box* b, const uint32_
 void ox_ve_def_gradh(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
                      unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; i++)
@@ -1028,6 +1054,7 @@ static void divVcurlVJLoop(uint32_t i, double K, const ox_box* b, const uint32_t
 void ox_iad_divv_curlv(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
                        unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; ++i)
@@ -1110,6 +1137,7 @@ static float AVswitchesJLoop(uint32_t i, double K, const ox_box* b, const uint32
 void ox_av_switches(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
                     unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; ++i)
@@ -1289,6 +1317,7 @@ static inline float tsKCourant(float maxvsignal, float h, float c, float Kcour)
 double ox_momentum_energy(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors,
                           unsigned first, unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return 0.0;
     ensure_tables();
     float minDt = INFINITY;
 #pragma omp parallel for schedule(static) reduction(min : minDt)
@@ -1313,6 +1342,7 @@ double ox_momentum_energy(ox_state* s, const ox_params* p, const ox_box* b, cons
 void ox_density(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
                 unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; i++)
@@ -1339,6 +1369,7 @@ void ox_eos_std(ox_state* s, const ox_params* p, unsigned first, unsigned last)
 void ox_iad_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors, unsigned first,
                 unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return;
     ensure_tables();
 #pragma omp parallel for
     for (size_t i = first; i < last; ++i)
@@ -1441,6 +1472,7 @@ static void momentumStdJLoop(uint32_t i, double K, const ox_box* b, const uint32
 double ox_momentum_energy_std(ox_state* s, const ox_params* p, const ox_box* b, const uint32_t* neighbors,
                               unsigned first, unsigned last)
 {
+    if (!lists_ok(s, neighbors, first, last, p->ngmax)) return 0.0;
     ensure_tables();
     float minDt = INFINITY;
 #pragma omp parallel for schedule(static) reduction(min : minDt)

@@ -82,6 +82,21 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+#ifdef SX_NS_PROBE_ON
+#define SX_NS_PROBE(k)                                                                                                \
+    do                                                                                                                \
+    {                                                                                                                 \
+        const uint64_t t_ = __builtin_readcyclecounter();                                                             \
+        prb[k] += t_ - tprev;                                                                                         \
+        tprev = t_;                                                                                                   \
+    } while (0)
+#else
+#define SX_NS_PROBE(k)                                                                                                \
+    do                                                                                                                \
+    {                                                                                                                 \
+    } while (0)
+#endif
+
 #ifndef SX_NS_WAVES_PER_EU
 #define SX_NS_WAVES_PER_EU 3
 #endif
@@ -101,12 +116,23 @@ union NsStreamLds
     double4   reg[2 * kMaxRegions];
 };
 
-//! next cluster of this workgroup: the XCD range of blockIdx % 8 first, then the other ranges (work stealing);
-//! numClusters when every range is done
-__device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClusters)
+//! clusters [lo, hi) of XCD range x
+__device__ __forceinline__ uint32_t rangeLo(uint32_t numClusters, uint32_t x)
+{
+    return (uint32_t)((uint64_t)numClusters * x / 8);
+}
+
+//! next cluster of this workgroup: the XCD range of blockIdx % 8 from the ticket `own` already drawn there (or a
+//! new one when own == ~0u), then the other ranges (work stealing); numClusters when every range is done
+__device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClusters, uint32_t own = ~0u)
 {
     const uint32_t x0 = blockIdx.x & 7;
-    for (uint32_t t = 0; t < 8; ++t)
+    if (own != ~0u)
+    {
+        const uint32_t lo = rangeLo(numClusters, x0), hi = rangeLo(numClusters, x0 + 1);
+        if (lo + own < hi) return lo + own;
+    }
+    for (uint32_t t = own != ~0u ? 1u : 0u; t < 8; ++t)
     {
         const uint32_t x  = (x0 + t) & 7;
         const uint32_t lo = (uint32_t)((uint64_t)numClusters * x / 8), hi = (uint32_t)((uint64_t)numClusters * (x + 1) / 8);
@@ -147,10 +173,16 @@ findNeighborsKernel(NsArgs a)
     if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters);
     __syncthreads();
     uint32_t c = s_next;
+#ifdef SX_NS_PROBE_ON
+    uint64_t prb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_readcyclecounter();
+#endif
     while (c < numClusters)
     {
     __syncthreads(); // every thread has read s_next
-    if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters); // in flight while this cluster is searched
+    // the next ticket of this workgroup's XCD range is drawn now and read at the end of the cluster, so the atomic's
+    // round trip overlaps the search instead of stalling wave 0 before its first barrier
+    uint32_t ticket = 0;
+    if (threadIdx.x == 0) ticket = atomicAdd(&a.work[blockIdx.x & 7], 1u);
     const uint32_t g     = c * kClusterWaves + wave;
     const uint32_t c0    = a.first + c * kCluster;
     const uint32_t i     = c0 + threadIdx.x;
@@ -192,13 +224,17 @@ findNeighborsKernel(NsArgs a)
         // the mask stores of this wave precede their loads; the translated tables have landed
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
+        // the next mask is loaded unconditionally (row 0 when there is none, then discarded by hn): a load under a
+        // divergent condition makes the compiler copy its result at the branch merge, i.e. wait for it at once
         uint32_t nz = nzq;
         int      q  = nz ? __builtin_ctz(nz) : 0;
         nz &= nz - 1u;
-        uint64_t m  = nzq ? __builtin_nontemporal_load(maskRow + (size_t)q * kWave) : 0ull;
-        int      qn = nz ? __builtin_ctz(nz) : 0;
-        uint64_t mn = nz ? __builtin_nontemporal_load(maskRow + (size_t)qn * kWave) : 0ull;
+        uint64_t m  = __builtin_nontemporal_load(maskRow + (size_t)q * kWave);
+        bool     hn = nz != 0u;
+        int      qn = hn ? __builtin_ctz(nz) : 0;
+        uint64_t mn = __builtin_nontemporal_load(maskRow + (size_t)qn * kWave);
         nz &= nz - 1u;
+        if (!nzq) m = 0ull;
         while (m)
         {
             const uint16_t* tq = wl.tab[q];
@@ -210,14 +246,19 @@ findNeighborsKernel(NsArgs a)
             // one store site: odd parity completes the pending word, even parity writes a fresh pair
             const bool     odd = stored & 1u;
             const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
+#ifdef SX_EXP_NOSTORE
+            if ((odd || two) && w == 0xdeadbeefu) ll[(size_t)(stored >> 1) * kWave] = w; // timing experiment only
+#else
             if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
+#endif
             pend = odd ? e2 : e1;
             stored += two ? 2u : 1u;
             if (!m)
             {
-                m  = mn, q = qn;
-                qn = nz ? __builtin_ctz(nz) : 0;
-                mn = nz ? __builtin_nontemporal_load(maskRow + (size_t)qn * kWave) : 0ull;
+                m  = hn ? mn : 0ull, q = qn;
+                hn = nz != 0u;
+                qn = hn ? __builtin_ctz(nz) : 0;
+                mn = __builtin_nontemporal_load(maskRow + (size_t)qn * kWave);
                 nz &= nz - 1u;
             }
         }
@@ -289,6 +330,7 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads();
+        SX_NS_PROBE(0);
         const int nreg = min(s_nreg, kMaxRegions);
         // waves whose regions reach node (bit w)
         auto reachMask = [&](int node, bool any) -> unsigned {
@@ -348,6 +390,7 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads();
+        SX_NS_PROBE(1);
         numCand = s_numCand;
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
@@ -363,6 +406,7 @@ findNeighborsKernel(NsArgs a)
                 s_bits[w] = 0;
         }
         __syncthreads(); // the regions (aliasing the stream LDS) are no longer read
+        SX_NS_PROBE(2);
 
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f    = 4.0f * hi * hi;
@@ -665,6 +709,7 @@ findNeighborsKernel(NsArgs a)
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
 
+        SX_NS_PROBE(3);
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -686,6 +731,7 @@ findNeighborsKernel(NsArgs a)
         const bool waveAgain = __ballot(again) != 0; // full-wave ballot, then one lane publishes it
         if (lane == 0) s_again[wave] = waveAgain;
         __syncthreads(); // also: every wave's bitmap updates are complete
+        SX_NS_PROBE(4);
         int any = 0;
         for (int w = 0; w < kClusterWaves; ++w)
             any |= s_again[w];
@@ -754,6 +800,7 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads(); // s_pre complete
+        SX_NS_PROBE(5);
         // the last batch: union positions straight into the lists
         if (nq > 0) expandBatch(true);
         if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
@@ -784,6 +831,7 @@ findNeighborsKernel(NsArgs a)
         }
         if (threadIdx.x == 0) a.ucount[c] = ucnt;
     }
+    SX_NS_PROBE(6);
 
     if (valid)
     {
@@ -801,6 +849,7 @@ findNeighborsKernel(NsArgs a)
         if (nfail) atomicAdd(&a.stats[1], nfail); // failures only: rare
         s_cst[wave] = make_uint4(maxCnt, (uint32_t)nstore, (uint32_t)tested, 0u);
     }
+    if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters, ticket);
     __syncthreads();
     if (threadIdx.x == 0)
     {
@@ -814,8 +863,14 @@ findNeighborsKernel(NsArgs a)
         a.clStats[c] = t;
     }
     __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
+    SX_NS_PROBE(7);
     c = s_next;
     }
+#ifdef SX_NS_PROBE_ON
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k)
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 12 + 2 * k), (unsigned long long)prb[k]);
+#endif
 }
 
 //! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]

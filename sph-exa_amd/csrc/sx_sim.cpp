@@ -352,16 +352,27 @@ __global__ __launch_bounds__(256) void markHalosKernel(const ReqBox* boxes, int 
     }
 }
 
-__global__ void maskFlagKernel(const unsigned long long* mark, size_t n, int q, uint32_t* flag)
+//! send flags of every peer at once: segment q of (n + 1) entries holds bit q of each particle's mark (0 for q == r
+//! and for the segment's closing entry), so one exclusive scan numbers the send lists of all peers in peer order
+__global__ void maskFlagsKernel(const unsigned long long* mark, size_t n, int P, int r, uint32_t* flag)
 {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i <= n) flag[i] = (i < n) ? (uint32_t)((mark[i] >> q) & 1ull) : 0u;
+    const size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (k >= (size_t)P * (n + 1)) return;
+    const size_t q = k / (n + 1), i = k - q * (n + 1);
+    flag[k]        = (i < n && (int)q != r) ? (uint32_t)((mark[i] >> q) & 1ull) : 0u;
 }
 
-__global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, size_t n, uint32_t* out)
+__global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, size_t n, int P, uint32_t* out)
 {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i < n && flag[i]) out[scan[i]] = (uint32_t)i;
+    const size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (k < (size_t)P * (n + 1) && flag[k]) out[scan[k]] = (uint32_t)(k % (n + 1));
+}
+
+//! start of every peer's send list in the scan (P entries) and the total (entry P)
+__global__ void segStartsKernel(const uint32_t* scan, size_t n, int P, uint32_t* out)
+{
+    const int q = threadIdx.x;
+    if (q <= P) out[q] = scan[q < P ? (size_t)q * (n + 1) : (size_t)P * (n + 1) - 1];
 }
 
 static inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
@@ -515,6 +526,8 @@ struct sx_sim
     NbLists   nb;
     uint32_t* stats;
     uint32_t* statsHost;
+    int       sortBits{30};          // key bits the local sort orders first (sortLocals)
+    uint64_t  sortStats[3]{0, 0, 0}; // sorts requested, done (not the identity), redone on all bits
     Scalars*  sc;
     Scalars*  scHost;
 
@@ -717,9 +730,45 @@ double quantMargin(const DevBox& b)
     } while (0)
 
 //! sort the local particles [0,nl) of the primary arrays by key (keys[0..nl) computed) via the spare buffers
+/*! SFC order of the locals, identical to the reference's stable sort of the full keys (Domain::sync):
+ *  - keys already ascending (no descent): the stable sort is the identity, nothing moves;
+ *  - else a stable radix sort of the top sortBits key bits, accepted when the result is ascending in the full keys
+ *    (then keys equal in the sorted bits kept their input order AND that order is ascending in the lower bits, which
+ *    is what the full stable sort gives); otherwise the full sort, and more bits from the next step on.
+ *  Lattice-like states separate every particle within the top 10 levels (30 bits), so 4 of the 8 radix passes. */
 int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
 {
-    SIM_HIP(sortKeys(s->work, s->keys, s->order, nl, st));
+    uint32_t* cnt  = s->work.get<uint32_t>("sort.desc", 1);
+    uint32_t* cntH = s->work.pinned<uint32_t>("sort.desch", 1);
+    auto descents = [&](const uint64_t* k, uint32_t& out) -> int {
+        SIM_HIP(hipMemsetAsync(cnt, 0, 4, st));
+        SIM_HIP(countDescents(k, nl, cnt, st));
+        SIM_HIP(hipMemcpyAsync(cntH, cnt, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        out = *cntH;
+        return SX_OK;
+    };
+    uint32_t d = 0;
+    if (int e = descents(s->keys, d)) return e;
+    s->sortStats[0]++;
+    if (d == 0) return SX_OK;
+    hipError_t he   = hipSuccess;
+    const int  bits = std::clamp(s->sortBits, 1, 63);
+    uint64_t*  kOut = sortKeysBits(s->work, s->keys, s->order, nl, 63 - bits, st, he);
+    SIM_HIP(he);
+    if (bits < 63)
+    {
+        if (int e = descents(kOut, d)) return e;
+        if (d)
+        {
+            kOut = sortKeysBits(s->work, s->keys, s->order, nl, 0, st, he);
+            SIM_HIP(he);
+            s->sortBits = std::min(63, bits + 9);
+            s->sortStats[2]++;
+        }
+    }
+    s->sortStats[1]++;
+    SIM_HIP(hipMemcpyAsync(s->keys, kOut, nl * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     GatherSet set{};
     for (auto& sp : s->spares)
     {
@@ -859,6 +908,12 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     SIM_HIP(hipStreamSynchronize(st));
     std::vector<uint64_t> split(P + 1, 0);
     if (int e = sx_domain_splitters(hb.data(), kHistBits, P, split.data())) return e;
+    // every rank's particle count after the exchange: the histogram bins of its range (splitters are bin
+    // boundaries), so the request-box counts of step 4 need no exchange
+    std::vector<uint64_t> nlOf(P, 0);
+    for (int q = 0; q < P; ++q)
+        for (uint64_t b = split[q] >> (63 - kHistBits); b < (split[q + 1] >> (63 - kHistBits)) && b < nb; ++b)
+            nlOf[q] += hb[b];
 
     // --- 3. particle exchange
     uint64_t* dsplit = s->work.get<uint64_t>("dom.split", P + 1);
@@ -905,12 +960,14 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     }
 
     // --- 4. halo discovery: request boxes, exchange, mark, send lists
+    if (nl != nlOf[r]) return SX_ERR_ARG; // the exchange must deliver exactly this rank's bins
     const size_t nChunks = (nl + kChunk - 1) / kChunk;
     ReqBox*      myBoxes = s->work.get<ReqBox>("dom.mybox", nChunks);
     if (nChunks) chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
-    std::vector<uint64_t> boxCnt(P, nChunks), boxRecv;
+    std::vector<uint64_t> boxCnt(P, nChunks), boxRecv(P);
     boxCnt[r] = 0;
-    SIM_COMM(T->exchangeCounts(boxCnt, boxRecv, st, s->cntBuf));
+    for (int q = 0; q < P; ++q)
+        boxRecv[q] = q == r ? 0 : (nlOf[q] + kChunk - 1) / kChunk;
     uint64_t nRemote = 0;
     for (int q = 0; q < P; ++q)
         nRemote += boxRecv[q];
@@ -936,35 +993,33 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         markHalosKernel<<<grid(nRemote, 4), 256, 0, st>>>(
             remote, (int)nRemote, s->localTree.childOffsets, s->localTree.internalToLeaf, s->localTree.layout,
             s->localTree.centers, s->localTree.sizes, s->x, s->y, s->z, s->dbox, qm, mark, err);
-    uint32_t* flag = s->work.get<uint32_t>("dom.flag", nl + 1);
-    uint32_t* scan = s->work.get<uint32_t>("dom.scan", nl + 1);
+    // send lists of all peers from one flag array and one scan (peer order), one host read of the P + 1 offsets
+    const size_t nf   = (size_t)P * (nl + 1);
+    uint32_t*    flag = s->work.get<uint32_t>("dom.flag", nf);
+    uint32_t*    scan = s->work.get<uint32_t>("dom.scan", nf);
+    uint32_t*    segs = s->work.get<uint32_t>("dom.segs", P + 1);
+    uint32_t*    hseg = s->work.pinned<uint32_t>("dom.hseg", P + 1);
     s->haloSend.assign(P, 0);
     s->haloSendOff.assign(P, 0);
-    std::vector<uint64_t> counts(P, 0);
-    // count per peer, then compact in rank order
-    s->sendIdx      = s->work.get<uint32_t>("dom.sendIdx", std::max<size_t>(1, nl) * std::min(P - 1, 8));
-    uint64_t offset = 0;
-    size_t   tmpB   = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nl + 1, st);
-    void*    tmp    = s->work.get<char>("dom.scantmp", tmpB);
-    uint32_t* hcnt  = s->work.pinned<uint32_t>("dom.hcnt", 2);
+    const size_t sendCap = std::max<size_t>(1, nl) * std::min(P - 1, 8);
+    s->sendIdx           = s->work.get<uint32_t>("dom.sendIdx", sendCap);
+    if (!flag || !scan || !s->sendIdx) return SX_ERR_NOMEM;
+    size_t tmpB = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nf, st);
+    void* tmp = s->work.get<char>("dom.scantmp", tmpB);
+    maskFlagsKernel<<<grid(nf), 256, 0, st>>>(mark, nl, P, r, flag);
+    SIM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nf, st));
+    segStartsKernel<<<1, 128, 0, st>>>(scan, nl, P, segs);
+    SIM_HIP(hipMemcpyAsync(hseg, segs, 4 * (P + 1), hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    if (hseg[P] > sendCap) return SX_ERR_NOMEM; // more than 8 full copies of the locals: give up loudly
+    scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, s->sendIdx);
     for (int q = 0; q < P; ++q)
     {
-        if (q == r || nl == 0) continue;
-        maskFlagKernel<<<grid(nl + 1), 256, 0, st>>>(mark, nl, q, flag);
-        hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nl + 1, st);
-        SIM_HIP(hipMemcpyAsync(hcnt, scan + nl, 4, hipMemcpyDeviceToHost, st));
-        SIM_HIP(hipStreamSynchronize(st));
-        uint64_t cq = hcnt[0];
-        if (offset + cq > std::max<size_t>(1, nl) * std::min(P - 1, 8))
-            s->sendIdx = nullptr; // capacity exceeded (more than 8 full copies): give up loudly
-        if (!s->sendIdx) return SX_ERR_NOMEM;
-        scatterIdxKernel<<<grid(nl), 256, 0, st>>>(flag, scan, nl, s->sendIdx + offset);
-        s->haloSend[q]    = cq;
-        s->haloSendOff[q] = offset;
-        offset += cq;
+        s->haloSendOff[q] = hseg[q];
+        s->haloSend[q]    = (q < P - 1 ? hseg[q + 1] : hseg[P]) - hseg[q];
     }
-    s->numSend = offset;
+    s->numSend = hseg[P];
     SIM_COMM(T->exchangeCounts(s->haloSend, s->haloRecv, st, s->cntBuf));
     s->haloRecv[r] = 0;
     uint64_t nLow = 0, nHigh = 0;
@@ -1795,6 +1850,15 @@ extern "C"
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         s->lastStats.build         = s->nsPolicy.lastBuild;
+#ifdef SX_NS_PROBE_ON
+        {
+            const uint64_t* pr  = reinterpret_cast<const uint64_t*>(s->statsHost + 12);
+            const double    nwv = (double)((s->last - s->first + 63) / 64);
+            fprintf(stderr, "nsprobe kcycles/wave: regions %.1f walk+scan %.1f reach %.1f stream %.1f iterwait %.1f union %.1f "
+                            "expand %.1f tail %.1f\n", pr[0] / nwv / 1e3, pr[1] / nwv / 1e3, pr[2] / nwv / 1e3,
+                    pr[3] / nwv / 1e3, pr[4] / nwv / 1e3, pr[5] / nwv / 1e3, pr[6] / nwv / 1e3, pr[7] / nwv / 1e3);
+        }
+#endif
         if (s->statsHost[0] & 1u)
         {
             fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 queue/candidate leaves, "

@@ -19,7 +19,10 @@ constexpr int kQCap = 512;  //!< internal-node ring per wave (power of 2)
 /*! Collect every leaf node passing `overlaps` (whose ancestors all pass) into cand[0..return), at most CCap leaves.
  *  Sets `overflow` if the queue or the candidate list ran out of space (the caller reports an error).  The capacity
  *  is a template parameter: the search builds (sx_neighbors.hip) and the halo discovery (sx_sim.cpp) size it
- *  differently, each in its own translation unit. */
+ *  differently, each in its own translation unit.
+ *  The queue holds the FIRST CHILD of every passing internal node (childOffsets[node], loaded with the node's own
+ *  leaf test), so a step's chain of dependent global loads is one deep: the children's boxes and child offsets.
+ *  Leaves come out in the order of the level-by-level expansion (deterministic). */
 template<int CCap, class Overlaps>
 __device__ __forceinline__ int waveCollectLeaves(const int32_t* __restrict__ childOffsets, Overlaps&& overlaps,
                                                  int* queue, int* cand, int lane, bool& overflow)
@@ -29,29 +32,43 @@ __device__ __forceinline__ int waveCollectLeaves(const int32_t* __restrict__ chi
     overflow               = false;
     if (overlaps(0))
     {
-        if (childOffsets[0] == 0) { numCand = 1, cand[0] = 0; }
-        else { queue[0] = 0, qt = 1; }
+        const int c0 = childOffsets[0];
+        if (c0 == 0) { numCand = 1, cand[0] = 0; }
+        else { queue[0] = c0, qt = 1; }
     }
     __builtin_amdgcn_wave_barrier();
+    // up to 16 queued nodes per step, two children per lane (queue items qh..qh+7 in the first half, qh+8..qh+15 in
+    // the second): both halves' loads are in flight together.  Items produced by this step are appended behind every
+    // item already queued, so the FIFO order -- and the order of the collected leaves -- is that of 8-node steps.
     while (qh < qt)
     {
-        const int  take  = min(8, qt - qh);
+        const int  take  = min(16, qt - qh);
         const int  slot  = lane >> 3, oct = lane & 7;
-        const bool ok    = slot < take;
-        const int  node  = ok ? queue[(qh + slot) & (kQCap - 1)] : 0;
-        const int  child = ok ? childOffsets[node] + oct : 0;
-        const bool pass  = ok && overlaps(child);
-        const bool leaf  = pass && childOffsets[child] == 0;
-        const bool inner = pass && !leaf;
-        const uint64_t bl = __ballot(leaf), bi = __ballot(inner);
-        if (leaf)
+        const bool okA   = slot < take, okB = slot + 8 < take;
+        const int  cA    = okA ? queue[(qh + slot) & (kQCap - 1)] + oct : 0;
+        const int  cB    = okB ? queue[(qh + slot + 8) & (kQCap - 1)] + oct : 0;
+        const int  gA    = childOffsets[cA]; // issued with the box loads of overlaps(): independent of them
+        const int  gB    = childOffsets[cB];
+        const bool pA    = okA && overlaps(cA);
+        const bool pB    = okB && overlaps(cB);
+        const bool leafA = pA && gA == 0, innerA = pA && gA != 0;
+        const bool leafB = pB && gB == 0, innerB = pB && gB != 0;
+        const uint64_t blA = __ballot(leafA), biA = __ballot(innerA);
+        const uint64_t blB = __ballot(leafB), biB = __ballot(innerB);
+        if (leafA)
         {
-            int pos = numCand + __popcll(bl & ltMask);
-            if (pos < CCap) cand[pos] = child;
+            const int pos = numCand + __popcll(blA & ltMask);
+            if (pos < CCap) cand[pos] = cA;
         }
-        if (inner) { queue[(qt + __popcll(bi & ltMask)) & (kQCap - 1)] = child; }
-        numCand += __popcll(bl);
-        qt += __popcll(bi);
+        if (leafB)
+        {
+            const int pos = numCand + __popcll(blA) + __popcll(blB & ltMask);
+            if (pos < CCap) cand[pos] = cB;
+        }
+        if (innerA) queue[(qt + __popcll(biA & ltMask)) & (kQCap - 1)] = gA;
+        if (innerB) queue[(qt + __popcll(biA) + __popcll(biB & ltMask)) & (kQCap - 1)] = gB;
+        numCand += __popcll(blA) + __popcll(blB);
+        qt += __popcll(biA) + __popcll(biB);
         qh += take;
         if (qt - qh > kQCap) overflow = true;
         __builtin_amdgcn_wave_barrier();

@@ -359,6 +359,44 @@ hipError_t launchSfcKeys(const double* x, const double* y, const double* z, uint
     return hipGetLastError();
 }
 
+//! number of descents keys[i] > keys[i+1] (added to *out)
+__global__ __launch_bounds__(256) void descentsKernel(const uint64_t* __restrict__ keys, size_t n, uint32_t* out)
+{
+    uint32_t cnt = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + 1 < n; i += (size_t)gridDim.x * blockDim.x)
+        cnt += keys[i] > keys[i + 1] ? 1u : 0u;
+    cnt = waveSum(cnt);
+    __shared__ uint32_t s_c[4];
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        const uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        if (t) atomicAdd(out, t);
+    }
+}
+
+hipError_t countDescents(const uint64_t* keys, size_t n, uint32_t* out, hipStream_t s)
+{
+    if (n < 2) return hipSuccess;
+    descentsKernel<<<(unsigned)std::min<size_t>(2048, (n + 255) / 256), 256, 0, s>>>(keys, n, out);
+    return hipGetLastError();
+}
+
+uint64_t* sortKeysBits(Arena& arena, const uint64_t* keys, uint32_t* order, size_t n, int beginBit, hipStream_t s,
+                       hipError_t& e)
+{
+    uint64_t* kOut = arena.get<uint64_t>("sort.kout", n);
+    uint32_t* vIn  = arena.get<uint32_t>("sort.vin", n);
+    iotaKernel<<<grid(n), 256, 0, s>>>(vIn, n);
+    size_t tmpBytes = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmpBytes, keys, kOut, vIn, order, (int)n, beginBit, 63, s);
+    if (e) return nullptr;
+    void* tmp = arena.get<char>("sort.tmp", tmpBytes);
+    e         = hipcub::DeviceRadixSort::SortPairs(tmp, tmpBytes, keys, kOut, vIn, order, (int)n, beginBit, 63, s);
+    return kOut;
+}
+
 hipError_t sortKeys(Arena& arena, uint64_t* keys, uint32_t* order, size_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;

@@ -147,10 +147,10 @@ struct NbLists
     }
 };
 
-constexpr int kStatsWords = 26; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
+constexpr int kStatsWords = 28; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
                                 //!< neighbors, [6] candidates tested, [8] union entries, [10] compact-build
                                 //!< overflow redone by the large build, [11] the compact build ran first,
-                                //!< [12..23] profile build
+                                //!< [12..27] phase probes of a profiling build
 
 //! which search build runs: the compact one (four workgroups per CU) with a device-side fallback to the large one,
 //! or the large one directly.  Host state of one caller (context or sim), fed with the stats of each finished
@@ -245,6 +245,10 @@ struct NsArgs
 hipError_t launchSfcKeys(const double* x, const double* y, const double* z, uint64_t* keys, size_t n,
                          const DevBox& b, hipStream_t s);
 hipError_t sortKeys(Arena& arena, uint64_t* keys, uint32_t* order, size_t n, hipStream_t s);
+//! stable radix sort of keys on bits [beginBit, 63) into the arena's "sort.kout" (returned) with the permutation
+hipError_t countDescents(const uint64_t* keys, size_t n, uint32_t* out, hipStream_t s);
+uint64_t*  sortKeysBits(Arena& arena, const uint64_t* keys, uint32_t* order, size_t n, int beginBit, hipStream_t s,
+                        hipError_t& e);
 hipError_t gather(const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes, hipStream_t s);
 //! up to kMaxGatherFields fields of 4 or 8 bytes reordered by one kernel (the index is read once per particle)
 constexpr int kMaxGatherFields = 16;

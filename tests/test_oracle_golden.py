@@ -82,3 +82,25 @@ def test_tree_and_neighbors_bitwise(ora):
     nbr, nc = ora.find_neighbors(st, box, bucket=16, iterate_h=True)
     assert np.array_equal(nc, d["nc_iter"]) and np.array_equal(nbr, d["nbr_iter"])
     assert np.array_equal(st.h, d["h_iter"])
+
+
+def test_oracle_rejects_out_of_range_neighbor_indices():
+    """a neighbor list exported from the path under test is input to the checker: an index beyond the state fails as
+    an assertion (sph_oracle.c lists_ok), it does not crash the process"""
+    import pytest
+
+    ora = po.load_oracle()
+    st, box = po.sedov_state(8)
+    po.converge_h(ora, st, box)
+    keys = ora.sfc_keys(st, box).copy()
+    o = np.argsort(keys, kind="stable")
+    for k in st.arrays:
+        st.arrays[k][:] = st.arrays[k][o]
+    st.keys[:] = keys[o]
+    nbr, nc = ora.find_neighbors(st, box)
+    st.nc[:] = nc
+    ora.xmass(st, box, nbr)  # a good list passes
+    bad = nbr.copy()
+    bad[5 * 150 + 3] = st.n + 1000
+    with pytest.raises(AssertionError, match="outside"):
+        ora.xmass(st, box, bad)
