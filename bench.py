@@ -92,6 +92,32 @@ def pmc_slot(pmc, slot):
     return tot if hit else None
 
 
+CALIB_FILE = os.path.join(ROOT, "profiles", "r3_fetch_calib.json")
+
+
+def step_traffic(pmc):
+    """HBM bytes of one whole step from the PMC summary: every kernel's (FETCH_SIZE x2 + WRITE_SIZE) x its launches
+    per step"""
+    if pmc is None:
+        return None
+    tot = 0.0
+    for k, v in pmc.items():
+        if k == "_meta":
+            continue
+        tot += (v.get("hbm_read_bytes_est", 0.0) + v.get("hbm_write_bytes_est", 0.0)) * v.get("calls_per_step", 1.0)
+    return tot
+
+
+def calibration():
+    """FETCH_SIZE / WRITE_SIZE factors measured on this library's access shapes (scripts/fetch_calib.hip)"""
+    try:
+        with open(CALIB_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {k: round(v["factor"], 3) for k, v in d.items() if v.get("factor")}
+
+
 def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
     """roofline entry of one kernel-time slot: HBM counter bytes / measured time vs the 8 TB/s peak, VALU issue and
     LDS conflict shares from the same counters, edge-model effective bandwidth"""
@@ -299,13 +325,24 @@ def main():
                             if (dom.get("frac") or 0) < 0.5 else "hbm"),
                 "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) if pmc else None,
                 "definition": "achieved = rocprofv3 PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, same "
-                              "workload) / avg launch time measured live with HIP events; frac = achieved / 8 TB/s; "
+                              "workload; the x2 is measured for coalesced 4/8/16-B, leaf-run and random 16-B/4-B "
+                              "gathers alike, profiles/r3_fetch_calib.json) / avg launch time measured live with HIP "
+                              "events; frac = achieved / 8 TB/s; "
                               "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); lds_conflict_frac = "
                               "SQ_LDS_BANK_CONFLICT / 256 CUs / (time x 2.4 GHz); effective_gbs = SURVEY 8(d) edge "
                               "model (neighbor records served from LDS/L2, not a roofline)",
                 **{k: dom[k] for k in ("valu_issue_frac", "lds_conflict_frac", "effective_gbs",
                                        "algorithmic_bytes_per_launch", "algorithmic_frac") if k in dom},
                 "per_kernel": per_kernel}
+    st_bytes = step_traffic(pmc)
+    if st_bytes:
+        roofline["step_traffic"] = st_bytes
+        roofline["step_hbm_gbs"] = st_bytes / (ms_step * 1e-3) / 1e9
+        roofline["step_hbm_frac"] = roofline["step_hbm_gbs"] / HBM_PEAK_GBS
+    cal = calibration()
+    if cal:
+        roofline["counter_calibration"] = {"source": os.path.relpath(CALIB_FILE, ROOT),
+                                           "known_bytes_per_counter_byte": cal}
     mom = per_kernel.get("momentumEnergy")
     if mom and not std_prop:
         roofline["momentum_valu"] = {"flop_per_pair": MOM_FLOP_PER_PAIR,

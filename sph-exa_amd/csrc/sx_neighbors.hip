@@ -116,6 +116,28 @@ union NsStreamLds
     double4   reg[2 * kMaxRegions];
 };
 
+//! the cluster's candidate space and union bitmap: dead once the final list expansion starts, whose hit masks then
+//! take the same bytes (kMaskSlots nonzero-chunk masks per thread, thread-interleaved)
+struct NsCandLds
+{
+    int      queue[kQCap];
+    int      cand[kCCap];
+    uint32_t cOff[kCCap + 1];
+    uint32_t p0[kCCap];    // first particle of candidate leaf cc
+    uint8_t  reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
+    uint32_t bits[kCandWords];
+    uint32_t pre[kCandWords];
+};
+constexpr int kMaskSlots = (int)(sizeof(NsCandLds) / (sizeof(uint64_t) * kCluster));
+union NsCandOrMasks
+{
+    NsCandLds c;
+    uint64_t  mk[kMaskSlots][kCluster];
+};
+//! masks per thread in the final expansion: the candidate-space bytes plus the two of each wave's staging records
+constexpr int kMaskLds = kMaskSlots + 2;
+static_assert(sizeof(float4) * kWave >= 2 * sizeof(uint64_t) * kWave, "two mask slots per lane in the records");
+
 //! clusters [lo, hi) of XCD range x
 __device__ __forceinline__ uint32_t rangeLo(uint32_t numClusters, uint32_t x)
 {
@@ -146,13 +168,14 @@ __device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClus
 __global__ __launch_bounds__(kCluster) __attribute__((amdgpu_waves_per_eu(SX_NS_WAVES_PER_EU))) void
 findNeighborsKernel(NsArgs a)
 {
-    __shared__ int         s_queue[kQCap];
-    __shared__ int         s_cand[kCCap];
-    __shared__ uint32_t    s_cOff[kCCap + 1];
-    __shared__ uint32_t    s_p0[kCCap];    // first particle of candidate leaf cc
-    __shared__ uint8_t     s_reach[kCCap]; // bit w: some lane of wave w may reach leaf cc
-    __shared__ uint32_t    s_bits[kCandWords];
-    __shared__ uint32_t    s_pre[kCandWords];
+    __shared__ NsCandOrMasks s_cm;
+    int* const               s_queue = s_cm.c.queue;
+    int* const               s_cand  = s_cm.c.cand;
+    uint32_t* const          s_cOff  = s_cm.c.cOff;
+    uint32_t* const          s_p0    = s_cm.c.p0;
+    uint8_t* const           s_reach = s_cm.c.reach;
+    uint32_t* const          s_bits  = s_cm.c.bits;
+    uint32_t* const          s_pre   = s_cm.c.pre;
     __shared__ int         s_nreg;
     __shared__ int         s_again[kClusterWaves];
     __shared__ uint32_t    s_wsum[kClusterWaves];
@@ -212,15 +235,6 @@ findNeighborsKernel(NsArgs a)
     // union positions (final: the chunk tables translated first).  Per lane, its nonzero chunks in order, two hits
     // per iteration; the next nonzero chunk's mask is loaded while the current one is expanded.
     auto expandBatch = [&](bool final) {
-        if (final)
-        {
-            for (int q = 0; q < nq; ++q)
-            {
-                // slots nobody hit hold stale indices: bounded into the candidate space, never referenced
-                const uint32_t ci = wl.tab[q][lane] & (kCandSpace - 1);
-                wl.tab[q][lane]   = (uint16_t)bitRank(s_bits, s_pre, ci);
-            }
-        }
         // the mask stores of this wave precede their loads; the translated tables have landed
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
@@ -266,6 +280,67 @@ findNeighborsKernel(NsArgs a)
         nq  = 0;
         nzq = 0;
         __builtin_amdgcn_wave_barrier(); // table reads precede the next chunk's staging writes
+    };
+
+    /*! the final expansion with the masks in LDS: every thread's nonzero-chunk masks are loaded in one burst (all
+     *  loads in flight together) and parked in the candidate-space bytes and its wave's record slots (kMaskLds per
+     *  thread), so the per-lane cursor below reads only LDS: no load latency, and no wait on the list stores it
+     *  issues (vmcnt counts stores too, in order).  A thread with more nonzero chunks than slots (rare) reads the
+     *  rest from the scratch rows.  Called by every thread of the workgroup after the union and the early-entry
+     *  rewrite, when the candidate space is dead. */
+    auto expandFinal = [&]() {
+        uint64_t* const slotsRec = reinterpret_cast<uint64_t*>(wl.rec); // [2][64] of this wave
+        auto slotAddr = [&](int k) -> uint64_t* {
+            return k < kMaskSlots ? &s_cm.mk[k][threadIdx.x] : slotsRec + (k - kMaskSlots) * kWave + lane;
+        };
+        {
+            // groups of 8 chunks: 8 loads in flight, then parked (16 VGPRs, not 2 kBatch)
+            int k = 0;
+            for (int q0 = 0; q0 < nq; q0 += 8)
+            {
+                uint64_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    v[u] = q0 + u < nq ? __builtin_nontemporal_load(maskRow + (size_t)(q0 + u) * kWave) : 0ull;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if ((nzq >> (q0 + u)) & 1u)
+                    {
+                        if (k < kMaskLds) *slotAddr(k) = v[u];
+                        ++k;
+                    }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): this thread's slots have landed (only it reads them)
+        uint32_t nz = nzq;
+        int      q  = nz ? __builtin_ctz(nz) : 0;
+        nz &= nz - 1u;
+        int      k  = 0;
+        uint64_t m  = nzq ? *slotAddr(0) : 0ull;
+        while (m)
+        {
+            const uint16_t* tq = wl.tab[q];
+            const uint32_t  e1 = tq[__builtin_ctzll(m)];
+            m &= m - 1ull;
+            const bool     two = m != 0ull;
+            const uint32_t e2  = two ? tq[__builtin_ctzll(m)] : 0u;
+            if (two) m &= m - 1ull;
+            // one store site: odd parity completes the pending word, even parity writes a fresh pair
+            const bool     odd = stored & 1u;
+            const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
+            if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
+            pend = odd ? e2 : e1;
+            stored += two ? 2u : 1u;
+            if (!m && nz)
+            {
+                q = __builtin_ctz(nz);
+                nz &= nz - 1u;
+                ++k;
+                m = k < kMaskLds ? *slotAddr(k) : __builtin_nontemporal_load(maskRow + (size_t)q * kWave);
+            }
+        }
+        nq  = 0;
+        nzq = 0;
     };
 
     int numCand = 0;
@@ -801,14 +876,20 @@ findNeighborsKernel(NsArgs a)
         }
         __syncthreads(); // s_pre complete
         SX_NS_PROBE(5);
-        // the last batch: union positions straight into the lists
-        if (nq > 0) expandBatch(true);
-        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
+        // the last batch's chunk tables -> union positions
+        for (int q = 0; q < nq; ++q)
+        {
+            // slots nobody hit hold stale indices: bounded into the candidate space, never referenced
+            const uint32_t ci = wl.tab[q][lane] & (kCandSpace - 1);
+            wl.tab[q][lane]   = (uint16_t)bitRank(s_bits, s_pre, ci);
+        }
         // entries written early as candidate indices -> union positions (ascending either way); batches of 8 list
         // words, the 8 loads issued together (one L2 round trip per batch)
         if (__ballot(nEarly > 0))
         {
-            const uint32_t nwl = (nEarly + 1) >> 1;
+            // complete words only: with nEarly odd the last early entry is still the pending half (translated below)
+            __builtin_amdgcn_s_waitcnt(0); // the early expansion's stores precede these loads
+            const uint32_t nwl = nEarly >> 1;
             constexpr int  kRB = 8;
             for (uint32_t k0 = 0; k0 < nwl; k0 += kRB)
             {
@@ -823,13 +904,18 @@ findNeighborsKernel(NsArgs a)
                     if (k < nwl)
                     {
                         const uint32_t lo = bitRank(s_bits, s_pre, v[u] & 0xffffu);
-                        const uint32_t hp = (2 * k + 1 < nEarly) ? bitRank(s_bits, s_pre, v[u] >> 16) : (v[u] >> 16);
+                        const uint32_t hp = bitRank(s_bits, s_pre, v[u] >> 16);
                         ll[(size_t)k * kWave] = lo | (hp << 16);
                     }
                 }
             }
+            if (nEarly & 1u) pend = bitRank(s_bits, s_pre, pend);
         }
         if (threadIdx.x == 0) a.ucount[c] = ucnt;
+        __syncthreads(); // the candidate space and the union bitmap are dead: the masks take their bytes
+        // the last batch: union positions straight into the lists (the early entries' last pending half included)
+        expandFinal();
+        if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
     }
     SX_NS_PROBE(6);
 
