@@ -332,7 +332,9 @@ int sx_gravity_upsweep(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, flo
                        float* multipoles);
 /*! Barnes-Hut traversal for targets [g->firstBody, g->lastBody) (computeGravity, traversal_cpu.hpp:166-230: groups
  *  of 16, vector MAC, quadrupole M2P, P2P softened by h_i + h_j): adds G * acc to f->ax, ay, az and returns the
- *  potential energy 0.5 sum G m phi in *egrav.  Open boxes only (no Ewald replicas). */
+ *  potential energy 0.5 sum G m phi in *egrav.  With explicit groups (g->groupStart, e.g. the active rungs of
+ *  ve-bdt, MultipoleHolder::traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285) only the targets of those groups are
+ *  traversed (the others keep their acceleration) and egrav sums over them.  Open boxes only (no Ewald replicas). */
 int sx_gravity_traverse(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
                         const double* centers, const float* multipoles, float G, double* egrav);
 

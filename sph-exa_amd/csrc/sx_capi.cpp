@@ -1140,9 +1140,13 @@ extern "C"
             return fail(c, SX_ERR_ARG, "sx_gravity_traverse: bad arguments");
         if (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)
             return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic gravity (Ewald replicas) is not provided");
+        // explicit groups (mHolder_.traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285): only their targets
+        sx_groups tmp;
+        if (int rc = resolveView(c, g, tmp, f->n, false)) return rc;
         GravArgs a   = gravArgs(c, f, tree);
         a.first      = g->firstBody;
         a.last       = g->lastBody;
+        a.active     = c->viewActive;
         a.centers4   = const_cast<double*>(centers);
         a.multipoles = const_cast<float*>(multipoles);
         a.G          = G;

@@ -265,10 +265,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         uint32_t*       err;
         uint32_t        first, last;
         float           G;
+        const uint8_t*  active;
     } const a{args.x, args.y, args.z, args.centers4, args.m, args.h, args.multipoles, args.childOffsets,
               args.internalToLeaf, args.layout, args.ax, args.ay, args.az, args.egrav, args.waveE, args.err, args.first,
               args.last,
-              args.G};
+              args.G, args.active};
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
     __shared__ int  s_p2p[4][kGList];
@@ -284,7 +285,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     const uint32_t i0   = a.first + g * kWave;
     if (i0 >= a.last) return; // whole wave
     const uint32_t i     = i0 + lane;
-    const bool     valid = i < a.last;
+    // a group view's targets (the ve-bdt active rungs): the others are not traversed and keep their acceleration
+    const bool     valid = i < a.last && (!a.active || a.active[i]);
+    if (__ballot(valid) == 0ull)
+    {
+        if (lane == 0 && a.waveE) a.waveE[g] = 0.0;
+        return;
+    }
     const uint32_t iS    = valid ? i : i0;
     const double   xi = a.x[iS], yi = a.y[iS], zi = a.z[iS];
     const float    hi = a.h[iS];

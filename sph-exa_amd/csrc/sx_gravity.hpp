@@ -32,6 +32,7 @@ struct GravArgs
                           // into *egrav by one small kernel (one atomic per launch instead of one per wave)
     uint32_t* err;        // bit 0: traversal stack exhausted
     int       fast;       // 1: M2P/P2P in float with rsqrt (displacements formed in double, sums in double)
+    const uint8_t* active; // nullable: targets with active[i] == 0 (outside the group view) get no gravity
 };
 
 //! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi

@@ -165,6 +165,74 @@ __device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClus
     return numClusters;
 }
 
+/*! Every leaf passing `overlaps` (all ancestors passing) into cand[0..return), by all four waves of the workgroup
+ *  (called by every thread).  FIFO breadth-first expansion as waveCollectLeaves (sx_traverse.hpp; the queue holds
+ *  first-child indices), 32 queued nodes per step, 8 per wave: wave w takes items qh+8w..qh+8w+7, and the
+ *  passing leaves and inner nodes of a step are appended in wave order, then lane order -- the order a single wave
+ *  taking 8 items per step produces, so the collected leaves are the same list.  Two barriers per step. */
+template<class Overlaps>
+__device__ __forceinline__ int clusterCollectLeaves(const int32_t* __restrict__ childOffsets, Overlaps&& overlaps,
+                                                    int* queue, int* cand, uint2* s_cnt, int wave, int lane,
+                                                    bool& overflow)
+{
+    const uint64_t ltMask  = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int            numCand = 0, qh = 0, qt = 0;
+    overflow               = false;
+    if (overlaps(0))
+    {
+        const int c0 = childOffsets[0];
+        if (c0 == 0) numCand = 1;
+        else qt = 1;
+        if (threadIdx.x == 0)
+        {
+            if (c0 == 0) cand[0] = 0;
+            else queue[0] = c0;
+        }
+    }
+    __syncthreads();
+    while (qh < qt)
+    {
+        const int  base  = qh + 8 * wave;
+        const int  take  = min(8, qt - base); // <= 0: this wave has no item this step
+        const int  slot  = lane >> 3, oct = lane & 7;
+        const bool ok    = slot < take;
+        const int  child = ok ? queue[(base + slot) & (kQCap - 1)] + oct : 0;
+        const int  gc    = childOffsets[child]; // issued with the box loads of overlaps(): independent of them
+        const bool pass  = ok && overlaps(child);
+        const bool leaf  = pass && gc == 0;
+        const bool inner = pass && !leaf;
+        const uint64_t bl = __ballot(leaf), bi = __ballot(inner);
+        if (lane == 0) s_cnt[wave] = make_uint2(__popcll(bl), __popcll(bi));
+        __syncthreads();
+        uint32_t offL = 0, offI = 0, totL = 0, totI = 0;
+#pragma unroll
+        for (int w = 0; w < kClusterWaves; ++w)
+        {
+            const uint2 cw = s_cnt[w];
+            if (w < wave) offL += cw.x, offI += cw.y;
+            totL += cw.x, totI += cw.y;
+        }
+        if (leaf)
+        {
+            const int pos = numCand + (int)offL + __popcll(bl & ltMask);
+            if (pos < kCCap) cand[pos] = child;
+        }
+        if (inner) queue[(qt + (int)offI + __popcll(bi & ltMask)) & (kQCap - 1)] = gc;
+        const int consumed = min(8 * kClusterWaves, qt - qh);
+        numCand += (int)totL;
+        qt += (int)totI;
+        qh += consumed;
+        if (qt - qh > kQCap) overflow = true;
+        __syncthreads(); // the queue and cand writes are visible; s_cnt is rewritten by the next step
+    }
+    if (numCand > kCCap)
+    {
+        overflow = true;
+        numCand  = kCCap;
+    }
+    return numCand;
+}
+
 __global__ __launch_bounds__(kCluster) __attribute__((amdgpu_waves_per_eu(SX_NS_WAVES_PER_EU))) void
 findNeighborsKernel(NsArgs a)
 {
@@ -183,6 +251,7 @@ findNeighborsKernel(NsArgs a)
     __shared__ int         s_numCand;
     __shared__ uint4       s_cst[kClusterWaves]; // per-wave statistics
     __shared__ uint32_t    s_next;               // the cluster this workgroup takes next
+    __shared__ uint2       s_bfsCnt[kClusterWaves];
     double4* const s_reg = s_str.reg;            // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}
 
     // the fallback launch (a.gate) exits at once unless the compact build overflowed
@@ -423,12 +492,12 @@ findNeighborsKernel(NsArgs a)
             }
             return bits;
         };
+        bool      overflow = false;
+        const int nCand    = clusterCollectLeaves(
+            a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, s_bfsCnt, wave,
+            lane, overflow);
         if (wave == 0)
         {
-            bool      overflow = false;
-            const int nCand    = waveCollectLeaves<kCCap>(
-                a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, lane,
-                overflow);
             if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short
             // exclusive scan of the candidate leaf sizes
             uint32_t run = 0;

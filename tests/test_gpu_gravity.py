@@ -132,3 +132,46 @@ def test_sim_steps_with_gravity(ctx, ora, side, steps):
 
     gutil.shadow_steps(ctx, ora, sim, obox, steps, ora.params(g=1.0, theta=0.5), FLOATS, on_step=egrav)
     sim.close()
+
+
+def test_traverse_group_view(ctx):
+    """explicit groups (the ve-bdt active rungs: mHolder_.traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285): the
+    targets of the view's groups get the full traversal's accelerations bitwise (the same wave, the same lists), every
+    other target keeps its acceleration, egrav sums over the view"""
+    st, obox = po.evrard_state(14)
+    keys = po.load_oracle().sfc_keys(st, obox).copy()
+    o = np.argsort(keys, kind="stable")
+    for k in st.arrays:
+        st.arrays[k][:] = st.arrays[k][o]
+    st.keys[:] = keys[o]
+    full = gpu_gravity(ctx, st, obox, exact=False)
+    # a view of every third 64-particle group (the reference extracts such group slices, sph/groups.hpp:31-48)
+    n = st.n
+    starts = np.arange(0, n, 64, dtype=np.uint32)
+    sel = starts[::3]
+    gs = ctx.alloc(len(sel), np.uint32)
+    ge = ctx.alloc(len(sel), np.uint32)
+    gs.set(sel)
+    ge.set(np.minimum(sel + 64, n).astype(np.uint32))
+    box = gutil.box_to_sx(obox)
+    ds = sx.DeviceState(ctx, gutil.host_dict(st))
+    inview = np.zeros(n, bool)
+    for s0 in sel:
+        inview[s0:min(s0 + 64, n)] = True
+    marker = np.float32(123.5)
+    for k in ("ax", "ay", "az"):
+        ds.set(k, np.where(inview, np.float32(0), marker).astype(np.float32))
+    tree, host = gutil.device_tree(ctx, ds.dev["keys"], n, 64, box)
+    nn = tree.numNodes
+    cen = ctx.alloc(4 * nn, np.float64)
+    mp = ctx.alloc(8 * nn, np.float32)
+    ctx.check(ctx.L.sx_gravity_upsweep(ctx.h, C.byref(ds.fields), C.byref(tree), 0.5, cen.ptr, mp.ptr), "upsweep")
+    g = sx.SxGroups(firstBody=0, lastBody=0, numGroups=len(sel), groupStart=gs.ptr, groupEnd=ge.ptr)
+    eg = C.c_double()
+    ctx.check(ctx.L.sx_gravity_traverse(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(tree), C.byref(box), cen.ptr,
+                                        mp.ptr, 1.0, C.byref(eg)), "traverse view")
+    for k in ("ax", "ay", "az"):
+        got = ds.get(k)
+        assert np.all(got[~inview] == marker), k
+        assert np.array_equal(got[inview], full[k][inview]), k
+    assert 0 > eg.value > full["egrav"]  # part of the sum, same sign
