@@ -98,7 +98,9 @@ typedef struct sx_params
     float    theta;   /* gravity opening parameter (sphexa.cpp:127: 0.5 with gravity) */
     double   g;       /* gravitational constant (ParticlesData::g); sx_sim adds self-gravity when != 0 */
     double   eps, etaAcc; /* accelerationTimestep (ts_global.hpp:47-67): 0.005, 0.2 */
-    int32_t  propagator;  /* sx_sim only: 0 = ve (HydroVeProp), 1 = std (HydroProp, std_hydro.hpp; factory.hpp:50-84) */
+    int32_t  propagator;  /* sx_sim only: 0 = ve (HydroVeProp), 1 = std (HydroProp, std_hydro.hpp), 2 = ve-bdt
+                             (HydroVeBdtProp, ve_hydro_bdt.hpp: block time-steps, one substep per sx_sim_step);
+                             factory.hpp:50-84 */
 } sx_params;
 
 /*! Device pointers in sphexa::ParticlesData field order (particles_data.hpp:247-251); NULL where unused.
@@ -370,7 +372,8 @@ int sx_rung_timestep(sx_ctx* ctx, float* groupDt, uint32_t* groupIndices, uint32
                      sx_comm* comm, sx_timestep* out);
 /*! minimumGroupDt (ts_rungs.hpp:147-157) for the numGroups active groups of substep ts->substep: sorts them as
  *  above, groupIndices[numGroups, ts->rungRanges[SX_MAX_RUNGS]) = the identity; *dt = min(dtMin, (totDt -
- *  elapsedDt) / substeps left), rungRanges over all SX_MAX_RUNGS rungs.  Synchronises the context stream. */
+ *  elapsedDt) / substeps left), rungRanges over all SX_MAX_RUNGS rungs.  numGroups may be 0 (a rank without active
+ *  groups on a substep: it contributes nothing to the min over the ranks).  Synchronises the context stream. */
 int sx_minimum_group_dt(sx_ctx* ctx, const sx_timestep* ts, float* groupDt, uint32_t* groupIndices, uint32_t numGroups,
                         sx_comm* comm, float* dt, uint32_t* rungRanges);
 /*! extractGroupGpu (groups.hpp:31-48): group k of the output = group indices[first + k] of grp, k < last - first
@@ -435,6 +438,11 @@ int    sx_sim_conserved(sx_sim* sim, double out[13]);
 /*! device time (ms) of each hot kernel alone in the last step (HIP events on the launch stream, bracketing just the
  *  launch): findNeighbors, xmass, veDefGradh, iadDivvCurlv, avSwitches, momentumEnergy */
 int    sx_sim_kernel_times(sx_sim* sim, float* ms, int cap, const char** names);
+/*! propagator 2 (ve-bdt): the Timestep after the last substep (sph::Timestep, timestep_ of HydroVeBdtProp,
+ *  ve_hydro_bdt.hpp:380).  A substep with activeRung(substep, numRungs) == 0 starts a new hierarchy (full sync,
+ *  every particle active); the others drift the inactive rungs and compute the active ones (partial sync: halo
+ *  x,y,z,h refreshed, order, tree and halo lists kept).  SX_ERR_ARG for the other propagators. */
+int    sx_sim_timestep(sx_sim* sim, sx_timestep* ts);
 
 #ifdef __cplusplus
 }

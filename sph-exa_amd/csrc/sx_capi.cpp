@@ -970,7 +970,14 @@ extern "C"
         SX_HIP(c, sortGroupDt(groupDt, groupIndices, numGroups, numGroupsTot, sc, c->stream));
         const float    fastFraction = 0.4f;
         const uint32_t kFast        = (uint32_t)(fastFraction * (float)numGroups);
-        SX_HIP(c, pickDt(groupDt, kFast, d, c->stream));
+        if (numGroups) SX_HIP(c, pickDt(groupDt, kFast, d, c->stream));
+        else
+        {
+            // a rank without active groups (possible on a substep of a multi-rank hierarchy) still joins the
+            // reduction, with nothing to contribute
+            const double inf[2] = {INFINITY, INFINITY};
+            SX_HIP(c, hipMemcpyAsync(d, inf, sizeof(inf), hipMemcpyHostToDevice, c->stream));
+        }
         if (sx::Transport* t = sx_comm_transport_internal(comm); t && t->size() > 1)
             if (!t->allreduceMinF64(d, 2, c->stream)) return fail(c, SX_ERR_HIP, "rung time-step: allreduce failed");
         double h[2];
@@ -1016,8 +1023,7 @@ extern "C"
     int sx_minimum_group_dt(sx_ctx* c, const sx_timestep* ts, float* groupDt, uint32_t* groupIndices,
                             uint32_t numGroups, sx_comm* comm, float* dt, uint32_t* ranges)
     {
-        if (!ts || !groupDt || !groupIndices || !dt || !ranges || numGroups == 0 ||
-            numGroups > ts->rungRanges[kMaxNumRungs])
+        if (!ts || !groupDt || !groupIndices || !dt || !ranges || numGroups > ts->rungRanges[kMaxNumRungs])
             return fail(c, SX_ERR_ARG, "sx_minimum_group_dt: bad arguments");
         float mins[2];
         if (int e = computeMinTimestep(c, groupDt, groupIndices, numGroups, ts->rungRanges[kMaxNumRungs], comm, mins))

@@ -37,10 +37,12 @@
 #include "sx_gravity.hpp"
 #include "sx_hydro.hpp"
 #include "sx_observables.hpp"
+#include "sx_sim.hpp"
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
 using namespace sx;
+using namespace sx::sim;
 
 extern "C" void*          sx_ctx_stream_internal(sx_ctx* c);
 extern "C" int            sx_ctx_exact_internal(sx_ctx* c);
@@ -53,7 +55,6 @@ namespace
 
 constexpr int      kHistBits   = 18;    // global key histogram resolution (level 6)
 constexpr uint32_t kChunk      = 2048;  // particles per halo request box
-constexpr double   kHaloMargin = 1.05;  // request radius = 2 * hmax(chunk) * margin (+ quantisation margin)
 
 DevBox toDevBox(const sx_box* b)
 {
@@ -70,18 +71,6 @@ DevBox toDevBox(const sx_box* b)
     }
     return d;
 }
-
-//! device scalars of one rank: ParticlesData time-step members
-struct Scalars
-{
-    double   minDt, minDt_m1, ttot, minDtCourant, minDtRho;
-    double   dtCand;   // rank-local candidate, globally min-reduced
-    float    courant;  // atomic-min target of the momentum kernel
-    unsigned maxDivvU; // order-preserving image of max divv
-    double   egrav;    // gravitational potential energy (ParticlesData::egrav)
-    unsigned long long maxAccSqBits; // max |a|^2 of the locals (bit image of a non-negative double)
-    unsigned gravErr;
-};
 
 //! max |a|^2 over [first, last) for accelerationTimestep (ts_global.hpp:47-67)
 __global__ void maxAccSqKernel(const float* ax, const float* ay, const float* az, size_t first, size_t last,
@@ -215,19 +204,14 @@ __global__ void lowerBoundsKernel(const uint64_t* keys, size_t n, const uint64_t
     out[q] = lo;
 }
 
-struct Fields
-{
-    double *  x, *y, *z, *temp;
-    float *   h, *m, *vx, *vy, *vz, *xm1, *ym1, *zm1, *dum1, *alpha;
-    uint64_t* id;
-};
-
 __global__ void packPRecKernel(Fields f, size_t n, PRec* out)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
+    // ve-bdt: the rung rides in the top byte of the id slot (particle ids < 2^56)
+    const uint64_t id = f.rung ? (f.id[i] | (uint64_t)f.rung[i] << 56) : f.id[i];
     out[i] = PRec{f.x[i],   f.y[i],   f.z[i],   f.temp[i], f.h[i],    f.m[i],     f.vx[i], f.vy[i],
-                  f.vz[i],  f.xm1[i], f.ym1[i], f.zm1[i],  f.dum1[i], f.alpha[i], f.id[i]};
+                  f.vz[i],  f.xm1[i], f.ym1[i], f.zm1[i],  f.dum1[i], f.alpha[i], id};
 }
 
 __global__ void unpackPRecKernel(const PRec* in, size_t n, Fields f)
@@ -249,7 +233,8 @@ __global__ void unpackPRecKernel(const PRec* in, size_t n, Fields f)
     f.zm1[i]  = r.zm1;
     f.dum1[i] = r.dum1;
     f.alpha[i] = r.alpha;
-    f.id[i]   = r.id;
+    f.id[i]   = f.rung ? r.id & ((1ull << 56) - 1) : r.id;
+    if (f.rung) f.rung[i] = (uint8_t)(r.id >> 56);
 }
 
 //! request box of every kChunk SFC-consecutive local particles: AABB grown by 2*hmax*margin + quantisation margin
@@ -310,6 +295,21 @@ __global__ void chunkCheckKernel(const float* h, size_t n, const ReqBox* boxes, 
     if (i >= n) return;
     const ReqBox& b = boxes[i / kChunk];
     if ((double)h[i] > b.hmax * margin) atomicOr(flag, 1u);
+}
+
+/*! 1 if some local's search sphere (2h around its current position) leaves its chunk's request box (minimum image):
+ *  the peers sent every particle inside that box, so a sphere inside it sees all of them.  Unlike chunkCheckKernel
+ *  this also covers the drift of the locals inside a ve-bdt hierarchy. */
+__global__ void chunkCoverKernel(const double* x, const double* y, const double* z, const float* h, size_t n,
+                                 const ReqBox* boxes, DevBox box, double qmargin, unsigned* flag)
+{
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ReqBox& b = boxes[i / kChunk];
+    const double  r = 2.0 * (double)h[i] * (1.0 + 1e-6) + qmargin;
+    const bool    out = fabs(foldPbc(x[i] - b.c[0], box, 0)) + r > b.s[0] || fabs(foldPbc(y[i] - b.c[1], box, 1)) + r > b.s[1] ||
+                     fabs(foldPbc(z[i] - b.c[2], box, 2)) + r > b.s[2];
+    if (out) atomicOr(flag, 1u);
 }
 
 /*! one wave per peer request box: traverse the local tree, mark local particles inside the box (minimum image)
@@ -381,11 +381,13 @@ static inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 
 
 constexpr int kCellShift = 63 - kHistBits; // level-6 cell of a key: the global histogram bins, one owner each
 
-//! source record of a gravity halo: coordinates, mass and smoothing length
-struct __attribute__((aligned(16))) GPart
+//! source record of a gravity halo: coordinates, mass, smoothing length and the SFC key of the owner's last sync
+//! (inside a ve-bdt hierarchy the particles drift while the key order of the sync stays the tree's order)
+struct __attribute__((aligned(8))) GPart
 {
-    double x, y, z;
-    float  m, h;
+    double   x, y, z;
+    float    m, h;
+    uint64_t key;
 };
 
 __global__ void farKeysKernel(uint64_t* keys, size_t n)
@@ -463,7 +465,7 @@ __global__ void reqLookupKernel(const uint32_t* req, size_t nReq, const uint32_t
 //! one wave per request: the cell's particles into the send buffer at its scanned offset
 __global__ void gatherCellsKernel(const uint32_t* beg, const uint32_t* size, const uint32_t* off, size_t nReq,
                                   const double* x, const double* y, const double* z, const float* m, const float* h,
-                                  GPart* out)
+                                  const uint64_t* keys, GPart* out)
 {
     const size_t k    = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
     const int    lane = threadIdx.x & 63;
@@ -472,106 +474,22 @@ __global__ void gatherCellsKernel(const uint32_t* beg, const uint32_t* size, con
     for (uint32_t t = lane; t < c; t += 64)
     {
         const uint32_t i = b + t;
-        out[o + t]       = GPart{x[i], y[i], z[i], m[i], h[i]};
+        out[o + t]       = GPart{x[i], y[i], z[i], m[i], h[i], keys[i]};
     }
 }
 
-__global__ void unpackGPartKernel(const GPart* in, size_t n, double* x, double* y, double* z, float* m, float* h)
+__global__ void unpackGPartKernel(const GPart* in, size_t n, double* x, double* y, double* z, float* m, float* h,
+                                  uint64_t* keys)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const GPart p = in[i];
-    x[i] = p.x, y[i] = p.y, z[i] = p.z, m[i] = p.m, h[i] = p.h;
+    x[i] = p.x, y[i] = p.y, z[i] = p.z, m[i] = p.m, h[i] = p.h, keys[i] = p.key;
 }
 
 } // namespace
 
-// ---------------------------------------------------------------------------------------------------------------
-
-struct sx_sim
-{
-    sx_ctx*        ctx;
-    NsPolicy       nsPolicy;       // neighbor search: compact or large build (sx_tree.hpp)
-    sx::Transport* comm{nullptr};
-    sx_params      p;
-    sx_box         box;
-    DevBox         dbox;
-    uint32_t       bucket;
-    size_t         cap{0}, n{0}, first{0}, last{0};
-    Arena          mem;
-    Arena          work;
-    DevTree        tree;
-    DevTree        localTree;
-    // multi-rank gravity: uniform level-6 far tree (built once, own arena) and the per-step near tree over the
-    // locals + gravity halos (own arena, so neither clobbers the SPH tree's "dt.*" buffers)
-    Arena          farMem;
-    Arena          gravWork;
-    DevTree        farTree;
-    DevTree        nearTree;
-
-    double *  x, *y, *z, *temp;
-    float *   h, *m, *vx, *vy, *vz, *xm1, *ym1, *zm1, *dum1, *alpha;
-    uint64_t* id;
-    uint64_t* keys;
-    uint32_t *order, *nc;
-    float *   xm, *kx, *gradh, *prho, *c, *divv, *curlv, *c11, *c12, *c13, *c22, *c23, *c33, *ax, *ay, *az;
-    double*   du;
-    float*    dV[6]{}; // dV11, dV12, dV13, dV22, dV23, dV33 (avClean only)
-    float *   rho{nullptr}, *pres{nullptr}; // std propagator only (HydroProp DependentFields rho, p)
-    RecX*     rx;
-    RecV*     rv;
-    RecT*     rt;
-    RecS*     rs; // std: {rho, p} records, aliasing rt (the std step has no xm/kx/prho/alpha)
-    RecC*     rc;
-    NbLists   nb;
-    uint32_t* stats;
-    uint32_t* statsHost;
-    int       sortBits{30};          // key bits the local sort orders first (sortLocals)
-    uint64_t  sortStats[3]{0, 0, 0}; // sorts requested, done (not the identity), redone on all bits
-    Scalars*  sc;
-    Scalars*  scHost;
-
-    struct Spare
-    {
-        void** field;
-        void*  alt;
-        int    elemBytes;
-    };
-    std::vector<Spare> spares; // double buffers of the conserved fields
-
-    // halo bookkeeping of the current step
-    std::vector<uint64_t> haloSend, haloSendOff, haloRecv, haloRecvOff;
-    uint32_t*             sendIdx{nullptr};
-    uint64_t              numSend{0};
-    uint64_t              numHalos{0};
-    uint64_t*             cntBuf{nullptr};
-
-    // overlap of the halo exchanges with the pair kernels of the interior clusters (no halo in their union):
-    // exchanges run on commStream, joined by events; cluster index lists built after each search
-    bool        overlap{true};
-    hipStream_t commStream{nullptr};
-    hipEvent_t  evProd{nullptr}, evComm{nullptr};
-    uint32_t*   clsList{nullptr}; // [interior | boundary] cluster indices (2 x numClusters)
-    uint32_t*   clsCount{nullptr};
-    uint32_t*   clsHost{nullptr}; // pinned copy of clsCount
-    uint32_t    nInterior{0}, nBoundary{0};
-
-    std::vector<hipEvent_t>  ev;
-    std::vector<std::string> stageNames;
-    std::vector<hipEvent_t>  kev; // begin/end pairs around the hot kernels alone
-    std::vector<std::string> kernelNames;
-    std::vector<float>       kernelMs;
-    std::vector<float>       stageMs;
-    sx_nbstats               lastStats{};
-    int                      haloRetries{0};
-    uint64_t                 gravHalos{0};    // gravity halos of the last multi-rank step
-    uint64_t                 gravFarCells{0}; // remote level-6 cells taken as far-field multipoles
-    uint64_t                 gravRemoteCells{0};
-
-    Fields fields() const { return Fields{x, y, z, temp, h, m, vx, vy, vz, xm1, ym1, zm1, dum1, alpha, id}; }
-};
-
-namespace
+namespace sx::sim
 {
 
 void allocFields(sx_sim* s, size_t cap)
@@ -652,6 +570,11 @@ void allocFields(sx_sim* s, size_t cap)
     spare(s->dum1, "du_m1");
     spare(s->alpha, "alpha");
     spare(s->id, "id");
+    if (s->p.propagator == 2)
+    {
+        s->rung = a.get<uint8_t>("rung", cap);
+        spare(s->rung, "rung");
+    }
     s->nb.reserve(a, 0, (uint32_t)cap, s->p.ngmax, true);
     s->stats      = a.get<uint32_t>("stats", kStatsWords);
     s->statsHost  = a.pinned<uint32_t>("statsHost", kStatsWords);
@@ -1069,7 +992,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
  *  Each source is counted once (locals and near cells in the near tree, far cells in the far tree); every far-cell
  *  multipole is accepted by the same MAC the reference applies, so the result matches the single-rank
  *  Barnes-Hut field within its opening-angle error. */
-int distributedGravity(sx_sim* s, hipStream_t st)
+int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
 {
     sx::Transport* T  = s->comm;
     const int      P  = T->size(), r = T->rank();
@@ -1193,7 +1116,8 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     GPart*       psend = W.get<GPart>("g.psend", nSend);
     if (nReq)
         gatherCellsKernel<<<grid(nReq * 64), 256, 0, st>>>(rbeg, rsize, roff, nReq, s->x + s->first, s->y + s->first,
-                                                           s->z + s->first, s->m + s->first, s->h + s->first, psend);
+                                                           s->z + s->first, s->m + s->first, s->h + s->first,
+                                                           s->keys + s->first, psend);
     SIM_COMM(T->exchangeCounts(pCnt, pRecv, st, s->cntBuf));
     uint64_t nLow = 0, nHigh = 0;
     for (int q = 0; q < P; ++q)
@@ -1219,16 +1143,18 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     float*    gm = W.get<float>("g.m", nG);
     float*    gh = W.get<float>("g.h", nG);
     uint64_t* gk = W.get<uint64_t>("g.keys", nG);
-    if (nLow) unpackGPartKernel<<<grid(nLow), 256, 0, st>>>(precv, nLow, gx, gy, gz, gm, gh);
+    if (nLow) unpackGPartKernel<<<grid(nLow), 256, 0, st>>>(precv, nLow, gx, gy, gz, gm, gh, gk);
     if (nHigh)
         unpackGPartKernel<<<grid(nHigh), 256, 0, st>>>(precv + nLow, nHigh, gx + nLow + nl, gy + nLow + nl,
-                                                       gz + nLow + nl, gm + nLow + nl, gh + nLow + nl);
+                                                       gz + nLow + nl, gm + nLow + nl, gh + nLow + nl, gk + nLow + nl);
     SIM_HIP(hipMemcpyAsync(gx + nLow, s->x + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
     SIM_HIP(hipMemcpyAsync(gy + nLow, s->y + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
     SIM_HIP(hipMemcpyAsync(gz + nLow, s->z + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
     SIM_HIP(hipMemcpyAsync(gm + nLow, s->m + s->first, 4 * nl, hipMemcpyDeviceToDevice, st));
     SIM_HIP(hipMemcpyAsync(gh + nLow, s->h + s->first, 4 * nl, hipMemcpyDeviceToDevice, st));
-    SIM_HIP(launchSfcKeys(gx, gy, gz, gk, nG, s->dbox, st));
+    // the keys of the last sync, not of the current positions: the sources stay in the sync's key order (inside a
+    // ve-bdt hierarchy particles drift out of their cells, as in the reference's fixed focus tree)
+    SIM_HIP(hipMemcpyAsync(gk + nLow, s->keys + s->first, 8 * nl, hipMemcpyDeviceToDevice, st));
     SIM_HIP(buildTree(W, gk, nG, s->bucket, s->dbox, s->nearTree, st));
 
     GravArgs ga{};
@@ -1252,6 +1178,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     ga.ax    = s->ax + shift;
     ga.ay    = s->ay + shift;
     ga.az    = s->az + shift;
+    ga.active = active ? active + shift : nullptr;
     ga.egrav = &s->sc->egrav;
     ga.err   = &s->sc->gravErr;
     ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
@@ -1277,6 +1204,7 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     fa.G          = (float)s->p.g;
     fa.invTheta   = invTheta;
     fa.ax = s->ax, fa.ay = s->ay, fa.az = s->az;
+    fa.active = active;
     fa.egrav = &s->sc->egrav;
     fa.err   = &s->sc->gravErr;
     fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
@@ -1287,6 +1215,32 @@ int distributedGravity(sx_sim* s, hipStream_t st)
     s->gravRemoteCells = nAll;
     s->gravFarCells    = nAll - (reqOff.empty() ? 0 : hwReq);
     return SX_OK;
+}
+
+int halosOutgrown(sx_sim* s, hipStream_t st, unsigned& hf)
+{
+    const size_t nl  = s->last - s->first;
+    auto*        flg = s->work.get<unsigned>("dom.hflag", 1);
+    SIM_HIP(hipMemsetAsync(flg, 0, 4, st));
+    if (nl)
+        chunkCoverKernel<<<grid(nl), 256, 0, st>>>(s->x + s->first, s->y + s->first, s->z + s->first, s->h + s->first,
+                                                 nl, s->work.get<ReqBox>("dom.mybox", 1), s->dbox,
+                                                 quantMargin(s->dbox), flg);
+    // the retry decision must be global: a rank redoing the sync alone would deadlock the collectives
+    SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
+    unsigned* hflg = s->work.pinned<unsigned>("dom.hflagh", 1);
+    SIM_HIP(hipMemcpyAsync(hflg, flg, 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    hf = *hflg;
+    return SX_OK;
+}
+
+void maxAccSq(sx_sim* s, hipStream_t st)
+{
+    const size_t nl = s->last - s->first;
+    if (nl)
+        maxAccSqKernel<<<std::min<unsigned>(grid(nl), 2048), 256, 0, st>>>(s->ax, s->ay, s->az, s->first, s->last,
+                                                                          &s->sc->maxAccSqBits);
 }
 
 int localSync(sx_sim* s, hipStream_t st)
@@ -1300,7 +1254,7 @@ int localSync(sx_sim* s, hipStream_t st)
     return SX_OK;
 }
 
-} // namespace
+} // namespace sx::sim
 
 extern "C"
 {
@@ -1308,6 +1262,7 @@ extern "C"
     int sx_sim_create(sx_sim** out, sx_ctx* ctx, size_t capacity, const sx_params* p, const sx_box* box,
                       uint32_t bucketSize)
     {
+        if (p->propagator < 0 || p->propagator > 2) return SX_ERR_ARG;
         auto* s   = new sx_sim;
         s->ctx    = ctx;
         s->p      = *p;
@@ -1316,6 +1271,7 @@ extern "C"
         s->bucket = bucketSize;
         s->cap    = capacity;
         allocFields(s, capacity);
+        if (s->p.propagator == 2) allocBdt(s);
         if (s->mem.failed())
         {
             delete s;
@@ -1360,7 +1316,8 @@ extern "C"
 
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
-        s->comm = sx_comm_transport_internal(c);
+        s->comm       = sx_comm_transport_internal(c);
+        s->commHandle = c;
         return SX_OK;
     }
 
@@ -1384,7 +1341,7 @@ extern "C"
         out[0] = s->first;
         out[1] = s->last;
         out[2] = s->n;
-        out[3] = s->haloRetries;
+        out[3] = s->haloRetries + s->bdt.haloShort;
         return SX_OK;
     }
 
@@ -1407,6 +1364,8 @@ extern "C"
             sedovInitKernel<<<grid(n), 256, 0, st>>>(side, f, n, s->x, s->y, s->z, s->h, s->m, s->temp, s->vx, s->vy,
                                                      s->vz, s->xm1, s->ym1, s->zm1, s->dum1, s->alpha, s->id,
                                                      (float)hInit, (float)(1.0 / N), ener0, width * width, 1e-8, cv);
+        if (s->rung && n) SIM_HIP(hipMemsetAsync(s->rung, 0, n, st));
+        s->bdt.started = false;
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         SIM_HIP(hipMemcpyAsync(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice, st));
         SIM_HIP(hipStreamSynchronize(st));
@@ -1440,6 +1399,8 @@ extern "C"
         SIM_HIP(cp(s->dum1, du_m1, 4));
         SIM_HIP(cp(s->alpha, alpha, 4));
         SIM_HIP(cp(s->id, id, 8));
+        if (s->rung) SIM_HIP(hipMemset(s->rung, 0, n));
+        s->bdt.started = false;
         Scalars init{minDt, minDt_m1, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0};
         SIM_HIP(hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice));
         return SX_OK;
@@ -1486,6 +1447,12 @@ extern "C"
         f->gradh = s->gradh + o;
         f->keys  = s->keys + o;
         f->nc    = s->nc + o;
+        f->rung  = s->rung ? s->rung + o : nullptr;
+        if (s->dV[0])
+        {
+            f->dV11 = s->dV[0] + o, f->dV12 = s->dV[1] + o, f->dV13 = s->dV[2] + o;
+            f->dV22 = s->dV[3] + o, f->dV23 = s->dV[4] + o, f->dV33 = s->dV[5] + o;
+        }
         if (id) *id = s->id + o;
         return SX_OK;
     }
@@ -1524,6 +1491,7 @@ extern "C"
 
     int sx_sim_step(sx_sim* s)
     {
+        if (s->p.propagator == 2) return stepBdt(s);
         hipStream_t        st  = (hipStream_t)sx_ctx_stream_internal(s->ctx);
         const HydroLaunch& H   = sx_ctx_exact_internal(s->ctx) ? hydro_exact() : hydro_fast();
         const bool         dist = s->comm && s->comm->size() > 1;
@@ -1771,7 +1739,7 @@ extern "C"
         {
             if (dist)
             {
-                if (int e = distributedGravity(s, st)) return e;
+                if (int e = distributedGravity(s, st, nullptr)) return e;
             }
             else
             {
@@ -1799,10 +1767,7 @@ extern "C"
             ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
             SIM_HIP(gravityTraverse(ga, st));
             }
-            const size_t nl = s->last - s->first;
-            if (nl)
-                maxAccSqKernel<<<std::min<unsigned>(grid(nl), 2048), 256, 0, st>>>(s->ax, s->ay, s->az, s->first,
-                                                                                  s->last, &s->sc->maxAccSqBits);
+            maxAccSq(s, st);
         }
         SIM_HIP(hipEventRecord(s->kev[13], st));
         SIM_HIP(hipEventRecord(s->ev[ev++], st));

@@ -433,7 +433,8 @@ __global__ void gatherManyKernel(const uint32_t* __restrict__ order, size_t n, G
     for (int f = 0; f < set.count; ++f) // uniform: every lane walks the same field list
     {
         if (set.bytes[f] == 8) static_cast<uint64_t*>(set.dst[f])[i] = static_cast<const uint64_t*>(set.src[f])[o];
-        else static_cast<uint32_t*>(set.dst[f])[i] = static_cast<const uint32_t*>(set.src[f])[o];
+        else if (set.bytes[f] == 4) static_cast<uint32_t*>(set.dst[f])[i] = static_cast<const uint32_t*>(set.src[f])[o];
+        else static_cast<uint8_t*>(set.dst[f])[i] = static_cast<const uint8_t*>(set.src[f])[o];
     }
 }
 
@@ -441,7 +442,7 @@ hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hip
 {
     if (!n || !set.count) return hipSuccess;
     for (int f = 0; f < set.count; ++f)
-        if (set.bytes[f] != 4 && set.bytes[f] != 8) return hipErrorInvalidValue;
+        if (set.bytes[f] != 1 && set.bytes[f] != 4 && set.bytes[f] != 8) return hipErrorInvalidValue;
     gatherManyKernel<<<grid(n), 256, 0, s>>>(order, n, set);
     return hipGetLastError();
 }

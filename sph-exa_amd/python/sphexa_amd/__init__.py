@@ -196,6 +196,7 @@ def lib():
         "sx_sim_layout": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_sim_set_overlap": (C.c_int, [vp, C.c_int]),
         "sx_sim_overlap_stats": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
+        "sx_sim_timestep": (C.c_int, [vp, C.POINTER(SxTimestep)]),
         "sx_comm_unique_id": (C.c_int, [vp]),
         "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
@@ -237,16 +238,19 @@ def halo_layout(recv_counts, rank, num_local):
     return off, tuple(int(v) for v in out)
 
 
-def default_params(K=None, ngmax=150, ng0=100, av_clean=False, g=0.0, theta=0.5, std=False):
-    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> and std the std
-    propagator (HydroProp) in sx_sim."""
+def default_params(K=None, ngmax=150, ng0=100, av_clean=False, g=0.0, theta=0.5, std=False, bdt=False):
+    """ParticlesData defaults (particles_data.hpp:86-138); av_clean selects HydroVeProp<true> (with bdt:
+    HydroVeBdtProp<true>), std the std propagator (HydroProp) and bdt the block time-step VE propagator
+    (HydroVeBdtProp, one substep per step) in sx_sim."""
+    if std and bdt:
+        raise ValueError("std and bdt are different propagators")
     if K is None:
         K = lib().sx_kernel_constant()
     return SxParams(K=K, ng0=ng0, ngmax=ngmax, Kcour=0.2, Krho=0.06, gamma=5.0 / 3.0, muiConst=10.0, alphamin=0.05,
                     alphamax=1.0, decay_constant=0.2, Atmin=0.1, Atmax=0.2,
                     ramp=float(np.float32(1.0) / (np.float32(0.2) - np.float32(0.1))), maxDtIncrease=1.1,
                     avClean=1 if av_clean else 0, theta=theta, g=g, eps=0.005, etaAcc=0.2,
-                    propagator=1 if std else 0)
+                    propagator=1 if std else (2 if bdt else 0))
 
 
 def make_box(lim, bnd):
@@ -590,6 +594,14 @@ class Sim:
         names = ["ecin", "eint", "egrav", "etot", "linmom", "angmom", "totalNeighbors", "px", "py", "pz", "Lx", "Ly",
                  "Lz"]
         return dict(zip(names, list(out)))
+
+    def timestep(self):
+        """ve-bdt: the Timestep after the last substep (sx_sim_timestep)"""
+        ts = SxTimestep()
+        self.ctx.check(self.L.sx_sim_timestep(self.h, C.byref(ts)), "timestep")
+        return dict(nextDt=ts.nextDt, elapsedDt=ts.elapsedDt, totDt=ts.totDt, numRungs=ts.numRungs,
+                    substep=ts.substep, rungRanges=list(ts.rungRanges), dt_m1=list(ts.dt_m1),
+                    dt_drift=list(ts.dt_drift))
 
     def gravity_stats(self):
         out = (C.c_uint64 * 3)()

@@ -1,12 +1,13 @@
 """HydroVeBdtProp on one GPU: the VE propagator with block time-steps, driven through the C-ABI seam.
 
-Mirror of `main/src/propagator/ve_hydro_bdt.hpp:51-378` (avClean = false, one rank, no gravity): the reference's
+Mirror of `main/src/propagator/ve_hydro_bdt.hpp:51-378` on one rank (avClean and self-gravity included): the reference's
 host control flow -- full/partial syncs, the rung hierarchy, the substep drift/kick cycle -- calling the HIP
 kernels of libsphexa_hip.so through the same seam functions the reference's propagator calls (`sph_gpu.hpp`):
 
   computeForces  (:222-290)  sync; computeXMass(activeRungs) [search + h-nc iteration on the view]; VeDefGradh;
                              computeEOS(first, last); IAD+divv/curlv; groupDivvTimestep; AV switches;
-                             momentum/energy (Courant per view group into groupDt); groupAccTimestep
+                             momentum/energy (Courant per view group into groupDt); self-gravity (upsweep + traversal of
+                             gravGroup: every target on a new hierarchy, else the active view); groupAccTimestep
   computeRungs   (:292-331)  rungTimestep on a new hierarchy, minimumGroupDt on a substep; extractGroupGpu
   integrate      (:333-378)  per rung: drift, or drift back + computePositions + storeRung; updateSmoothingLength
 
@@ -16,7 +17,9 @@ cornerstone tree + linked octree + node geometry, then computeSpatialGroups (`gr
 keeps order and tree and grows `searchExtFactor` by 1.012 (:196-211).  Everything stays on the device; the host
 sees the group count, the rung ranges and the time-step scalars, as in the reference.
 
-The product path is the HIP library: nothing here computes particle data on the CPU.
+The product path is the HIP library: nothing here computes particle data on the CPU.  The production driver is the
+native one (sx_sim with propagator 2, sph-exa_amd/csrc/sx_bdt.cpp); this one stays as its bit-for-bit reference
+(tests/test_gpu_ve_bdt_native.py) and as the seam-level mirror the CPU oracle is checked against.
 """
 import ctypes as C
 
@@ -32,6 +35,7 @@ CONSERVED = ["x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "x_m1", "y_m1", 
              "id"]
 DEPENDENT = ["ax", "ay", "az", "prho", "c", "du", "c11", "c12", "c13", "c22", "c23", "c33", "xm", "kx", "nc", "divv",
              "curlv", "gradh", "keys"]
+GRAD_V = ["dV11", "dV12", "dV13", "dV22", "dV23", "dV33"]  # GradVFields of HydroVeBdtProp<avClean = true>
 DT = dict(DTYPES, id=np.uint64)
 
 
@@ -75,14 +79,16 @@ class HydroVeBdtProp:
         """host: dict of numpy arrays with the conserved fields (rung optional, zeros); box: SxBox"""
         self.ctx, self.L, self.h = ctx, ctx.L, ctx.h
         self.p = params or default_params()
-        if self.p.avClean or self.p.g != 0.0 or self.p.propagator != 0:
-            raise SxError("HydroVeBdtProp here is the VE propagator without AV cleaning and gravity")
+        if self.p.propagator not in (0, 2):
+            raise SxError("HydroVeBdtProp is the VE propagator")
+        if self.p.g != 0.0 and any(box.bnd[k] == 1 for k in range(3)):
+            raise SxError("self-gravity needs an open box (no Ewald replicas)")
         self.box, self.bucket = box, bucket
         n = len(host["x"])
         self.n = n
         self.dev, self.fields = {}, SxFields()
         self.fields.n = n
-        for name in CONSERVED + DEPENDENT:
+        for name in CONSERVED + DEPENDENT + (GRAD_V if self.p.avClean else []):
             dt = DT[name]
             d = ctx.alloc(n, dt)
             if name in host:
@@ -110,6 +116,7 @@ class HydroVeBdtProp:
         self.rungs = [None] * MAX_RUNGS
         self.active = None
         self.tree = None
+        self.egrav = 0.0
         self.on_search = None  # test hook: called after the search of computeForces with the active view
         self.log = []
 
@@ -206,10 +213,29 @@ class HydroVeBdtProp:
         # groupDivvTimestep: groupDivvTimestepGpu(d.Krho, ...) (ts_rungs.hpp:48-54)
         self._ck(L.sx_group_divv_timestep(h, np.float32(p.Krho), C.byref(v), f.divv, gdt), "group divv dt")
         self._ck(L.sx_av_switches(h, C.byref(v), C.byref(f), C.byref(p), C.byref(box), self.min_dt), "AV switches")
-        self._ck(L.sx_momentum_energy(h, C.byref(v), gdt, C.byref(f), C.byref(p), C.byref(box), None), "momentum")
+        me = L.sx_momentum_energy_avclean if p.avClean else L.sx_momentum_energy
+        self._ck(me(h, C.byref(v), gdt, C.byref(f), C.byref(p), C.byref(box), None), "momentum")
+        if p.g != 0.0:
+            self._gravity(self.is_synced())
         # groupAccTimestep: etaAcc * sqrt(eps) (ts_rungs.hpp:58-65)
         eta = np.float32(np.float64(p.etaAcc) * np.sqrt(np.float64(p.eps)))
         self._ck(L.sx_group_acc_timestep(h, eta, C.byref(v), f.ax, f.ay, f.az, gdt), "group acc dt")
+
+    def _gravity(self, new_hierarchy):
+        """mHolder_.upsweep + traverse(gravGroup) (:272-286): gravGroup is every target on a new hierarchy
+        (computeSpatialGroups of the MultipoleHolder), else the active rungs"""
+        L, h, t = self.L, self.h, self.tree
+        nn = t.numNodes
+        if getattr(self, "_gcap", 0) < nn:
+            self._gcap = nn
+            self._gc, self._gm = self.ctx.alloc(4 * nn, np.float64), self.ctx.alloc(8 * nn, np.float32)
+        self._ck(L.sx_gravity_upsweep(h, C.byref(self.fields), C.byref(t), self.p.theta, self._gc.ptr, self._gm.ptr),
+                 "upsweep")
+        g = SxGroups(firstBody=0, lastBody=self.n) if new_hierarchy else self.active
+        e = C.c_double()
+        self._ck(L.sx_gravity_traverse(h, C.byref(g), C.byref(self.fields), C.byref(t), C.byref(self.box),
+                                       self._gc.ptr, self._gm.ptr, np.float32(self.p.g), C.byref(e)), "gravity")
+        self.egrav = e.value
 
     # ---- computeRungs (:292-331) ---------------------------------------------------------------------------
     def compute_rungs(self):

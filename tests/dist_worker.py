@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--std", action="store_true", help="std propagator (HydroProp)")
     ap.add_argument("--no-overlap", action="store_true", help="serial halo exchanges (no interior/boundary split)")
     ap.add_argument("--av-clean", action="store_true", help="avClean momentum (dV halos)")
+    ap.add_argument("--g", type=float, default=None, help="gravitational constant (default: 1 for evrard, else 0)")
+    ap.add_argument("--bdt", action="store_true", help="ve-bdt propagator: one block time-step substep per step")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -44,10 +46,12 @@ def main():
     comm = sx.Comm(args.backend)
     ic = {"evrard": po.evrard_state, "noh": po.noh_state}.get(args.ic, po.sedov_state)
     st, obox = ic(args.side)
-    if args.ic == "evrard":
-        po.converge_h(po.load_oracle(), st, obox)  # the lattice-contracted IC's h iterate in the first search
+    if args.ic in ("evrard", "noh"):
+        po.converge_h(po.load_oracle(), st, obox)  # these ICs' h would iterate (and may not converge) in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
-    params = sx.default_params(g=1.0 if args.ic == "evrard" else 0.0, std=args.std, av_clean=args.av_clean)
+    g = args.g if args.g is not None else (1.0 if args.ic == "evrard" else 0.0)
+    params = sx.default_params(g=g, std=args.std, av_clean=args.av_clean,
+                               bdt=args.bdt)
     sim = sx.Sim(ctx, 2 * st.n // size + 4096, box, params=params)
     sim.set_comm(comm)
     sim.set_overlap(not args.no_overlap)
@@ -59,7 +63,8 @@ def main():
     out = {}
     for s in range(args.steps):
         sim.step()
-        got = sim.get(["id", "nc", "h"] + FIELDS + (["rho", "p"] if args.std else []))
+        got = sim.get(["id", "nc", "h", "m"] + FIELDS + (["rho", "p"] if args.std else []) +
+                      (["rung"] if args.bdt else []))
         for k, v in got.items():
             out[f"s{s}_{k}"] = v
         sc = sim.scalars()
@@ -68,6 +73,9 @@ def main():
         out[f"s{s}_conserved"] = np.array([cq[k] for k in ("ecin", "eint", "egrav", "etot", "totalNeighbors")])
         gs = sim.gravity_stats()
         out[f"s{s}_gravity"] = np.array([gs["halos"], gs["far_cells"], gs["remote_cells"]])
+        if args.bdt:
+            ts = sim.timestep()
+            out[f"s{s}_ts"] = np.array([ts["numRungs"], ts["substep"], ts["nextDt"]])
         lay = sim.layout()
         out[f"s{s}_layout"] = np.array([lay["first"], lay["last"], lay["n"], lay["haloRetries"]])
         ov = sim.overlap_stats()

@@ -102,7 +102,7 @@ def ftz_floor(ref):
     return norm * cmax * 3.0 * ref["nc"].astype(np.float64) * FLT_MIN * 2.0
 
 
-def check(name, got, ref, sc):
+def check_all(name, got, ref, sc):
     a = got.astype(np.float64)
     b = ref[name].astype(np.float64)
     s = scale_of(name, ref, sc)
@@ -118,8 +118,10 @@ def check(name, got, ref, sc):
     return float(np.max(err / (s + 1e-300)))
 
 
-def run_cluster_kernels(ctx, st, box_sx, inputs, ref, sc, params, minDt, av_clean):
-    """GPU: own search (cluster lists) with the reference h, then each kernel in isolation on reference inputs"""
+def run_cluster_kernels(ctx, st, box_sx, inputs, ref, sc, params, minDt, av_clean, view=None):
+    """GPU: own search (cluster lists) with the reference h, then each kernel in isolation on reference inputs.
+    view = (groupStart, groupEnd, active mask): the kernels run on that explicit-group view (a ve-bdt partial
+    substep); inside it the reference's values, outside it the previous device values untouched"""
     n = st.n
     host = gutil.host_dict(st)
     for k in ("h", "nc"):
@@ -133,12 +135,28 @@ def run_cluster_kernels(ctx, st, box_sx, inputs, ref, sc, params, minDt, av_clea
                                   C.byref(stats)), "search")
     assert np.array_equal(ds.get("nc"), inputs["nc"])  # same neighbor sets as the reference
     g = sx.SxGroups(firstBody=0, lastBody=n, numGroups=(n + 63) // 64)
+    act = np.ones(n, bool)
+    if view is not None:
+        gs, ge, act = view
+        gsd, ged = ctx.upload(gs), ctx.upload(ge)
+        g = sx.SxGroups(firstBody=0, lastBody=0, numGroups=gs.size, groupStart=gsd.ptr, groupEnd=ged.ptr)
     f = ds.fields
     worst = {}
+    before = {}
 
     def setf(names, src):
         for k in names:
             ds.set(k, src[k])
+        for k in names:
+            before[k] = src[k]
+
+    def check(name, got, ref, sc):
+        """inside the view against the oracle; outside it the value the device held before the kernel"""
+        if view is None:
+            return check_all(name, got, ref, sc)
+        prev = before[name] if name in before else host.get(name, np.zeros(n, got.dtype))
+        assert np.array_equal(got[~act], np.asarray(prev)[~act].astype(got.dtype)), ("outside the view", name)
+        return check_all(name, np.where(act, got, ref[name].astype(got.dtype)), ref, sc)
 
     ctx.check(L.sx_xmass_only(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box_sx)), "xmass")
     worst["xm"] = check("xm", ds.get("xm"), ref, sc)
@@ -148,8 +166,8 @@ def run_cluster_kernels(ctx, st, box_sx, inputs, ref, sc, params, minDt, av_clea
         worst[k] = check(k, ds.get(k), ref, sc)
     setf(["kx", "gradh"], ref)
     ctx.check(L.sx_eos(h, 0, n, 10.0, 5.0 / 3.0, f.temp, f.m, f.kx, f.xm, f.gradh, f.prho, f.c, None, None), "eos")
-    for k in ("prho", "c"):
-        worst[k] = check(k, ds.get(k), ref, sc)
+    for k in ("prho", "c"):  # computeEOS(first, last): every target, view or not
+        worst[k] = check_all(k, ds.get(k), ref, sc)
     setf(["prho", "c"], ref)
     ctx.check(L.sx_iad_divv_curlv(h, C.byref(g), C.byref(f), C.byref(p), C.byref(box_sx)), "iad")
     for k in ["c11", "c12", "c13", "c22", "c23", "c33", "divv", "curlv"] + (GRADV if av_clean else []):
@@ -163,7 +181,8 @@ def run_cluster_kernels(ctx, st, box_sx, inputs, ref, sc, params, minDt, av_clea
     ctx.check(me(h, C.byref(g), None, C.byref(f), C.byref(p), C.byref(box_sx), C.byref(mdt)), "momentum")
     for k in ("du", "ax", "ay", "az"):
         worst[k] = check(k, ds.get(k), ref, sc)
-    assert mdt.value == pytest.approx(float(ref["minDtCourant"][0]), rel=1e-5)
+    if view is None:
+        assert mdt.value == pytest.approx(float(ref["minDtCourant"][0]), rel=1e-5)
     ctx.free_all()
     return worst
 
@@ -205,6 +224,23 @@ def test_cluster_kernels_vs_oracle(ctx, ora, ic, side, steps, av_clean):
     inputs = {"h": st.h.copy(), "nc": st.nc.copy()}
     worst = run_cluster_kernels(ctx, st, gutil.box_to_sx(box), inputs, ref, sc, params, st.minDt, av_clean)
     print(ic, side, {k: f"{v:.2e}" for k, v in worst.items()})
+
+
+@pytest.mark.parametrize("ic,side,steps,seed,av_clean", [("sedov", 24, 2, 1, False), ("noh", 20, 3, 2, True)])
+def test_cluster_kernels_view_vs_oracle(ctx, ora, ic, side, steps, seed, av_clean):
+    """the production kernels on a ve-bdt partial-substep view (a shuffled third of random-size explicit groups, as
+    the rung-sorted activeRungs_ slices are): the view's targets within the per-kernel tolerance of the oracle, every
+    other target untouched"""
+    from test_gpu_group_views import make_view
+
+    params = ora.params(av_clean=av_clean)
+    st, box, nbr = advanced_state(ora, ic, side, steps, params)
+    chk = st.copy()
+    ref, sc = reference_chain(ora, chk, box, nbr, params, st.minDt)
+    inputs = {"h": st.h.copy(), "nc": st.nc.copy()}
+    view = make_view(st.n, seed)
+    assert 0 < view[2].sum() < st.n
+    run_cluster_kernels(ctx, st, gutil.box_to_sx(box), inputs, ref, sc, params, st.minDt, av_clean, view=view)
 
 
 STD_OUT = ["rho", "p", "c", "c11", "c12", "c13", "c22", "c23", "c33", "du", "ax", "ay", "az"]
