@@ -15,7 +15,8 @@
  *   4. halo discovery: each rank publishes request boxes = AABB of every 2048-particle SFC chunk grown by
  *      2*hmax(chunk)*margin; every rank marks (wave-cooperative tree traversal of its own tree) the particles
  *      inside each peer's boxes -> send lists; halos land in place, [halos of lower ranks | local | higher];
- *   5. the combined array is key-sorted by construction -> one tree over locals + halos.
+ *   5. the combined array is key-sorted by construction -> one tree over locals + halos, built from the halos' keys
+ *      (sent first, 8 B each) while their coordinates, h and m are exchanged on the communication stream.
  *   After the h iteration the request margin is checked; if some particle outgrew it, discovery is redone.
  * Halo exchanges carry exactly the reference's fields (ve_hydro.hpp:150-186): x,y,z,h,m at setup, then xm,
  * then vx,vy,vz,prho,c,kx, then c11..c33,divv, then alpha.
@@ -969,9 +970,21 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     s->first = nLow;
     s->last  = nLow + nl;
     s->n     = nLow + nl + nHigh;
-    if (int e = haloExchange(s, {{s->x, 8}, {s->y, 8}, {s->z, 8}, {s->h, 4}, {s->m, 4}}, st)) return e;
-    SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, s->n, s->dbox, st));
+    // the halos' keys come from their owners (8 B each; the owners computed them from the same coordinates), so the
+    // combined tree is built while x,y,z,h,m (28 B per halo) are still in flight on the communication stream
+    SIM_HIP(launchSfcKeys(s->x + s->first, s->y + s->first, s->z + s->first, s->keys + s->first, nl, s->dbox, st));
+    if (int e = haloExchange(s, {{s->keys, 8}}, st)) return e;
+    const bool ovl = s->overlap && s->commStream;
+    hipStream_t cs = ovl ? s->commStream : st;
+    if (ovl)
+    {
+        SIM_HIP(hipEventRecord(s->evProd, st));
+        SIM_HIP(hipStreamWaitEvent(cs, s->evProd, 0));
+    }
+    if (int e = haloExchange(s, {{s->x, 8}, {s->y, 8}, {s->z, 8}, {s->h, 4}, {s->m, 4}}, cs)) return e;
+    if (ovl) SIM_HIP(hipEventRecord(s->evComm, cs));
     SIM_HIP(buildTree(s->work, s->keys, s->n, s->bucket, s->dbox, s->tree, st));
+    if (ovl) SIM_HIP(hipStreamWaitEvent(st, s->evComm, 0));
     unsigned errH = 0;
     SIM_HIP(hipMemcpy(&errH, err, 4, hipMemcpyDeviceToHost));
     if (errH) return SX_ERR_TRAVERSAL;
