@@ -240,12 +240,6 @@ struct __attribute__((aligned(16))) GSrc
     float  m, h;
 };
 
-#ifndef SX_GRAV_MERGE_LEAVES
-#define SX_GRAV_MERGE_LEAVES 1 // fast P2P: contiguous same-mask leaves share a chunk
-#endif
-#ifndef SX_GRAV_PAIR_P2P
-#define SX_GRAV_PAIR_P2P 1 // fast P2P: two sources per lane per iteration in packed FP32
-#endif
 #ifndef SX_GRAV_WPE
 #define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
 #endif
@@ -411,9 +405,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const bool     mine = (em >> qq) & 1u;
                     const uint64_t W    = __ballot(mine);
                     const int      cnt  = __popcll(W);
-#ifdef SX_GRAV_NOM2P
-                    continue;
-#endif
                     if (cnt == 0) continue;
                     SX_LOAD_QUARTER(qq)
                     __builtin_amdgcn_wave_barrier(); // the previous quarter's reads of s_idx are done
@@ -470,7 +461,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     jm = (unsigned)(e & 15);
                     ec0 += kWave;
                     if (s0 + ec0 >= s1) ++ek, ec0 = 0;
-#if SX_GRAV_MERGE_LEAVES
                     // following list leaves with the same quarter mask whose particles continue this range (siblings
                     // of one node, appended together in SFC order) join the chunk up to 64 sources
                     while (ec0 == 0 && jn < (uint32_t)kWave && ek < nP)
@@ -484,7 +474,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                         if (take == r1 - r0) ++ek;
                         else ec0 = take;
                     }
-#endif
                     return true;
                 }
                 ++ek, ec0 = 0;
@@ -509,7 +498,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             const uint32_t cn = jn;
             const unsigned cm = jm;
             __builtin_amdgcn_wave_barrier();
-#if SX_GRAV_PAIR_P2P
             {
                 // source l goes to pair P = 4 (l / 8) + l % 4 as half (l / 4) % 2: the lane of sub s evaluates sources
                 // s + 8j and s + 8j + 4 together; lanes [cn, roundup8(cn)) write massless far-away padding
@@ -524,9 +512,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     s_hF[wave][buf][P * 2 + hf] = in ? ph : 0.0f;
                 }
             }
-#else
-            if ((uint32_t)lane < cn) s_srcF[wave][buf][lane] = pv, s_hF[wave][buf][lane] = ph;
-#endif
             have = nextChunk();
             if (have) loadRegs();
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the staged chunk has landed
@@ -535,11 +520,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             for (int qq = 0; qq < 4; ++qq)
             {
                 if (!((cm >> qq) & 1u)) continue;
-#ifdef SX_GRAV_NOP2P
-                continue;
-#endif
                 SX_LOAD_QUARTER(qq)
-#if SX_GRAV_PAIR_P2P
                 if (qok)
                 {
                     // two sources per iteration in packed FP32 (v_pk_add/mul/fma_f32), the padding adds exact zeros
@@ -567,22 +548,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     for (int c_ = 0; c_ < 4; ++c_)
                         fq[c_] += f2[c_].x + f2[c_].y;
                 }
-#else
-                if (qok)
-                    for (uint32_t s = sub; s < cn; s += 4)
-                    {
-                        const float4 src = s_srcF[wave][buf][s];
-                        const float  dx = src.x - qx, dy = src.y - qy, dz = src.z - qz;
-                        const float  R2   = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                        const float  h_ij = qh + s_hF[wave][buf][s];
-                        const float  invR = __builtin_amdgcn_rsqf(fmaxf(R2, h_ij * h_ij)); // >= h^2: no denormals
-                        const float  invR3m = src.w * invR * invR * invR;
-                        fq[0] = fmaf(-invR3m, R2, fq[0]);
-                        fq[1] = fmaf(dx, invR3m, fq[1]);
-                        fq[2] = fmaf(dy, invR3m, fq[2]);
-                        fq[3] = fmaf(dz, invR3m, fq[3]);
-                    }
-#endif
                 SX_FOLD_QUARTER(qq)
             }
             buf ^= 1;

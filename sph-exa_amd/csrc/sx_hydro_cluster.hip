@@ -169,30 +169,14 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
 
     if (cu.U <= (uint32_t)CH)
     {
-#ifdef SX_PAIR_PROFILE
-        const uint64_t tp0 = __builtin_readcyclecounter();
-#endif
         if (!resident)
         {
             fill(0, cu.U);
             __syncthreads();
             resident = true;
         }
-#ifdef SX_PAIR_PROFILE
-        const uint64_t tp1 = __builtin_readcyclecounter();
-#endif
         const uint32_t wBeg = cu.wBeg, wEnd = cu.wEnd;
-#ifdef SX_PAIR_PROFILE
-        auto profOut = [&]() {
-            const uint64_t t2 = __builtin_readcyclecounter();
-            if (threadIdx.x == 0 && (blockIdx.x % 20000) == 7)
-                printf("pairprof CH %d SPLIT %d U %u fill %llu loop %llu\n", CH, SPLIT, cu.U,
-                       (unsigned long long)(tp1 - tp0), (unsigned long long)(t2 - tp1));
-        };
-        if (wBeg >= wEnd) return profOut();
-#else
         if (wBeg >= wEnd) return;
-#endif
         const uint32_t* nl = cu.nl;
         // PF: list words beyond the share read the share's last word again (always in bounds) and every prefetch
         // below is unconditional, so the LDS reads of the next pair are issued on one path and the wait before a
@@ -235,9 +219,6 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             const uint32_t t = q0;
             q0 = q2, q2 = q1, q1 = t;
         }
-#ifdef SX_PAIR_PROFILE
-        profOut();
-#endif
     }
     else
     {
@@ -1014,11 +995,7 @@ void veDefGradh(const PairArgs& a, hipStream_t s)
 }
 void iadDivvCurlv(const PairArgs& a, hipStream_t s)
 {
-#ifdef SX_IAD_TWO_PASS
-    if (a.numGroups && clusters(a)) iadDivvCurlvKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
-#else
     if (a.numGroups && clusters(a)) iadDivvCurlvFusedKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
-#endif
 }
 void avSwitches(const PairArgs& a, hipStream_t s)
 {

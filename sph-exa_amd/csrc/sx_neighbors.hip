@@ -82,20 +82,6 @@ __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-#ifdef SX_NS_PROBE_ON
-#define SX_NS_PROBE(k)                                                                                                \
-    do                                                                                                                \
-    {                                                                                                                 \
-        const uint64_t t_ = __builtin_readcyclecounter();                                                             \
-        prb[k] += t_ - tprev;                                                                                         \
-        tprev = t_;                                                                                                   \
-    } while (0)
-#else
-#define SX_NS_PROBE(k)                                                                                                \
-    do                                                                                                                \
-    {                                                                                                                 \
-    } while (0)
-#endif
 
 #ifndef SX_NS_WAVES_PER_EU
 #define SX_NS_WAVES_PER_EU 3
@@ -265,9 +251,6 @@ findNeighborsKernel(NsArgs a)
     if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters);
     __syncthreads();
     uint32_t c = s_next;
-#ifdef SX_NS_PROBE_ON
-    uint64_t prb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = __builtin_readcyclecounter();
-#endif
     while (c < numClusters)
     {
     __syncthreads(); // every thread has read s_next
@@ -329,11 +312,7 @@ findNeighborsKernel(NsArgs a)
             // one store site: odd parity completes the pending word, even parity writes a fresh pair
             const bool     odd = stored & 1u;
             const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
-#ifdef SX_EXP_NOSTORE
-            if ((odd || two) && w == 0xdeadbeefu) ll[(size_t)(stored >> 1) * kWave] = w; // timing experiment only
-#else
             if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
-#endif
             pend = odd ? e2 : e1;
             stored += two ? 2u : 1u;
             if (!m)
@@ -474,7 +453,6 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads();
-        SX_NS_PROBE(0);
         const int nreg = min(s_nreg, kMaxRegions);
         // waves whose regions reach node (bit w)
         auto reachMask = [&](int node, bool any) -> unsigned {
@@ -534,7 +512,6 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads();
-        SX_NS_PROBE(1);
         numCand = s_numCand;
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
@@ -550,7 +527,6 @@ findNeighborsKernel(NsArgs a)
                 s_bits[w] = 0;
         }
         __syncthreads(); // the regions (aliasing the stream LDS) are no longer read
-        SX_NS_PROBE(2);
 
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f    = 4.0f * hi * hi;
@@ -727,11 +703,7 @@ findNeighborsKernel(NsArgs a)
                 // the chunk joins the batch: this lane's mask row (coalesced 512-B store per wave)
                 maskRow[(size_t)nq * kWave] = hm;
                 nzq |= (hm != 0ull ? 1u : 0u) << nq;
-#ifdef SX_NS_NO_EARLY
-                if (++nq == kBatch) { atomicOr(&a.stats[0], 1u | 4u); nq = 0; nzq = 0; }
-#else
                 if (++nq == kBatch) expandBatch(false);
-#endif
             }
             else
             {
@@ -853,7 +825,6 @@ findNeighborsKernel(NsArgs a)
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
 
-        SX_NS_PROBE(3);
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -875,7 +846,6 @@ findNeighborsKernel(NsArgs a)
         const bool waveAgain = __ballot(again) != 0; // full-wave ballot, then one lane publishes it
         if (lane == 0) s_again[wave] = waveAgain;
         __syncthreads(); // also: every wave's bitmap updates are complete
-        SX_NS_PROBE(4);
         int any = 0;
         for (int w = 0; w < kClusterWaves; ++w)
             any |= s_again[w];
@@ -944,7 +914,6 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads(); // s_pre complete
-        SX_NS_PROBE(5);
         // the last batch's chunk tables -> union positions
         for (int q = 0; q < nq; ++q)
         {
@@ -986,7 +955,6 @@ findNeighborsKernel(NsArgs a)
         expandFinal();
         if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
     }
-    SX_NS_PROBE(6);
 
     if (valid)
     {
@@ -1018,14 +986,8 @@ findNeighborsKernel(NsArgs a)
         a.clStats[c] = t;
     }
     __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
-    SX_NS_PROBE(7);
     c = s_next;
     }
-#ifdef SX_NS_PROBE_ON
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k)
-            atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + 12 + 2 * k), (unsigned long long)prb[k]);
-#endif
 }
 
 //! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]
@@ -1073,9 +1035,6 @@ unsigned searchGrid()
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, findNeighborsKernel, kCluster, 0);
         grid = (unsigned)std::max(1, cus) * (unsigned)std::max(1, perCu);
-#ifdef SX_NS_GRIDMUL
-        grid *= SX_NS_GRIDMUL;
-#endif
         if (getenv("SX_NS_DEBUG_GRID")) fprintf(stderr, "search grid %u (%d per CU)\n", grid, perCu);
     }
     return grid;

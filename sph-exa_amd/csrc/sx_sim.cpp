@@ -1828,15 +1828,6 @@ extern "C"
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         s->lastStats.build         = s->nsPolicy.lastBuild;
-#ifdef SX_NS_PROBE_ON
-        {
-            const uint64_t* pr  = reinterpret_cast<const uint64_t*>(s->statsHost + 12);
-            const double    nwv = (double)((s->last - s->first + 63) / 64);
-            fprintf(stderr, "nsprobe kcycles/wave: regions %.1f walk+scan %.1f reach %.1f stream %.1f iterwait %.1f union %.1f "
-                            "expand %.1f tail %.1f\n", pr[0] / nwv / 1e3, pr[1] / nwv / 1e3, pr[2] / nwv / 1e3,
-                    pr[3] / nwv / 1e3, pr[4] / nwv / 1e3, pr[5] / nwv / 1e3, pr[6] / nwv / 1e3, pr[7] / nwv / 1e3);
-        }
-#endif
         if (s->statsHost[0] & 1u)
         {
             fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 queue/candidate leaves, "
