@@ -7,10 +7,10 @@
  *
  * Per cluster (workgroup):
  *   1. search regions in registers (wave / 16-particle sub-group boxes, particle spheres where the SFC range jumps);
- *   2. wave 0 collects every leaf whose geometric box comes within 2*h*ext of some region (waveCollectLeaves,
- *      sx_traverse.hpp; minimum image on periodic axes, inflated by the key-quantisation margin) and numbers the
- *      particles of those leaves consecutively: the cluster's CANDIDATE SPACE (leaf cc's particles start at
- *      s_cOff[cc]);
+ *   2. the four waves together collect every leaf whose geometric box comes within 2*h*ext of some region
+ *      (clusterCollectLeaves: one breadth-first walk per cluster, each wave testing 8 nodes x 8 octants per step;
+ *      minimum image on periodic axes, inflated by the key-quantisation margin) and number the particles of those
+ *      leaves consecutively: the cluster's CANDIDATE SPACE (leaf cc's particles start at s_cOff[cc]);
  *   3. each wave streams the candidate leaves one of its lanes can reach in blocks of 64 particles, culls them
  *      against the wave box grown by 2 hmax and stages the survivors into 64-slot CHUNKS (records in LDS, the
  *      slot's candidate index in the wave's chunk table); every lane tests a chunk against its own particle with a

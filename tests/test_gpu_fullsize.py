@@ -118,3 +118,30 @@ def test_evrard_n300_gravity_two_steps_one_gpu():
     finally:
         sim.close()
         ctx.close()
+
+
+def test_sedov_n200_ve_bdt_substeps_one_gpu():
+    """the native ve-bdt propagator (sx_sim propagator 2) on config 2's 8M particles: a hierarchy with several rungs
+    forms after the first full sync, partial substeps run, energy is conserved, ids stay a permutation"""
+    side = 200
+    n = side ** 3
+    ctx = sx.Context(0)
+    box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
+    sim = sx.Sim(ctx, n, box, params=sx.default_params(bdt=True))
+    try:
+        sim.init_sedov(side)
+        e0 = sim.conserved()
+        partial, rungs = 0, 1
+        for _ in range(6):
+            sim.step()
+            ts = sim.timestep()
+            rungs = max(rungs, ts["numRungs"])
+            partial += ts["substep"] > 1
+        e = sim.conserved()
+        assert rungs >= 2 and partial > 0, (rungs, partial)
+        assert abs(e["etot"] / e0["etot"] - 1) < 1e-6, (e0, e)
+        ids = np.sort(sim.get(["id"])["id"])
+        assert np.array_equal(ids, np.arange(n, dtype=np.uint64))
+    finally:
+        sim.close()
+        ctx.close()
