@@ -32,6 +32,10 @@ namespace cluster
 
 constexpr int kB = kCluster; // threads per workgroup
 
+#ifndef SX_ME_LEAN
+#define SX_ME_LEAN true // momentum: one record in flight (see neighborLoop)
+#endif
+
 //! per-workgroup cluster bookkeeping
 struct Clu
 {
@@ -145,7 +149,7 @@ __device__ __forceinline__ void combineShares(const Clu& cu, float (&v)[NV], flo
  *  of particle j.  `resident` carries "the whole union is already in LDS" from a previous pass over the same records.
  *  With the union resident the loop is software-pipelined: the LDS records of the next two neighbors (one list
  *  word) are read while the current two are computed, and list words are prefetched four ahead. */
-template<int CH, int SPLIT, bool PF = true, class Stage, class Load, class Compute>
+template<int CH, int SPLIT, bool PF = true, bool LEAN = false, class Stage, class Load, class Compute>
 __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&& load, Compute&& compute,
                                              bool& resident)
 {
@@ -178,12 +182,36 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
         const uint32_t wBeg = cu.wBeg, wEnd = cu.wEnd;
         if (wBeg >= wEnd) return;
         const uint32_t* nl = cu.nl;
+        if constexpr (LEAN)
+        {
+            // one record in flight while the other is computed: the LDS read latency (~100 cycles) is far below a
+            // heavy pair's compute, and half the record registers let one more wave per SIMD in (momentum 152 -> 128
+            // VGPRs).  List words beyond the share re-read its last word; their records are read, never computed.
+            const uint32_t wLast = wEnd - 1;
+            auto           ld    = [&](uint32_t w) { return nl[(size_t)min(w, wLast) * kWave]; };
+            uint32_t       q0 = ld(wBeg + 1), q1 = ld(wBeg + 2);
+            uint32_t       wd = nl[(size_t)wBeg * kWave];
+            auto           ra = load(wd & 0xffffu);
+            for (uint32_t w = wBeg;;)
+            {
+                const auto rb = load(wd >> 16);
+                compute(ra);
+                const bool odd = 2 * w + 1 < cu.cnt;
+                wd             = q0;
+                q0             = q1;
+                q1             = ld(w + 3);
+                ra             = load(wd & 0xffffu);
+                if (odd) compute(rb);
+                if (++w >= wEnd) break;
+            }
+            return;
+        }
         // PF: list words beyond the share read the share's last word again (always in bounds) and every prefetch
         // below is unconditional, so the LDS reads of the next pair are issued on one path and the wait before a
         // computation covers only the records it consumes (a masked prefetch leaves a path on which the previous
         // pair's reads may still be outstanding, and the merged wait then also waits for the new reads).  Measured
         // (Sedov 64M): IAD -0.4 ms, AV -0.3 ms; momentum +0.3..0.7 ms (its records are 80 B: the extra registers of
-        // the unmasked form cost more than the wait), so momentum keeps the masked form.
+        // the unmasked form cost more than the wait), so momentum takes the LEAN form above (22.5 -> 21.5 ms).
         const uint32_t  wLast = wEnd - 1;
         auto            ld    = [&](uint32_t w) {
             if constexpr (PF) return nl[(size_t)min(w, wLast) * kWave];
@@ -713,7 +741,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
         gradV_i[3] = a.dV22[q], gradV_i[4] = a.dV23[q], gradV_i[5] = a.dV33[q];
         eta_crit   = avEtaCrit(cu.cnt);
     }
-    neighborLoop<CH, SPLIT, false>(
+    neighborLoop<CH, SPLIT, false, SX_ME_LEAN>(
         cu,
         [&](uint32_t j, uint32_t slot) {
             const RecX r   = a.rx[j];
@@ -966,7 +994,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #define SX_SPLIT_AV 2
 #endif
 #ifndef SX_SPLIT_ME
-#define SX_SPLIT_ME 3 // 12 waves on the CU's one momentum workgroup (152 VGPRs fit three waves per SIMD)
+#define SX_SPLIT_ME 4 // 16 waves on the CU's one momentum workgroup (104 VGPRs with one record in flight: four per SIMD)
 #endif
 #ifndef SX_SPLIT_ME_AVC
 #define SX_SPLIT_ME_AVC 2 // the avClean variant needs 190 VGPRs: two waves per SIMD
