@@ -32,6 +32,9 @@ namespace cluster
 
 constexpr int kB = kCluster; // threads per workgroup
 
+#ifndef SX_LEAN_DEPTH
+#define SX_LEAN_DEPTH 2
+#endif
 #ifndef SX_ME_LEAN
 #define SX_ME_LEAN true // momentum: one record in flight (see neighborLoop)
 #endif
@@ -189,7 +192,13 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             // VGPRs).  List words beyond the share re-read its last word; their records are read, never computed.
             const uint32_t wLast = wEnd - 1;
             auto           ld    = [&](uint32_t w) { return nl[(size_t)min(w, wLast) * kWave]; };
-            uint32_t       q0 = ld(wBeg + 1), q1 = ld(wBeg + 2);
+            // list words prefetched SX_LEAN_DEPTH ahead (the list streams from HBM: a load's latency under load
+            // spans several heavy pairs)
+            constexpr int  D = SX_LEAN_DEPTH;
+            uint32_t       q[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                q[d] = ld(wBeg + 1 + d);
             uint32_t       wd = nl[(size_t)wBeg * kWave];
             auto           ra = load(wd & 0xffffu);
             for (uint32_t w = wBeg;;)
@@ -197,9 +206,11 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
                 const auto rb = load(wd >> 16);
                 compute(ra);
                 const bool odd = 2 * w + 1 < cu.cnt;
-                wd             = q0;
-                q0             = q1;
-                q1             = ld(w + 3);
+                wd             = q[0];
+#pragma unroll
+                for (int d = 0; d + 1 < D; ++d)
+                    q[d] = q[d + 1];
+                q[D - 1] = ld(w + 1 + D);
                 ra             = load(wd & 0xffffu);
                 if (odd) compute(rb);
                 if (++w >= wEnd) break;
@@ -702,8 +713,66 @@ struct RecM
     float2 g2;
 };
 
+//! c11 .. c33 of a RecC without its divv and pad (two loads, 24 of its 32 bytes)
+struct MeC
+{
+    float4 a; // c11, c12, c13, c22
+    float2 b; // c23, c33
+};
+__device__ __forceinline__ MeC meLoadC(const RecC* rc, uint32_t j)
+{
+    const float* p = reinterpret_cast<const float*>(rc + j);
+    return MeC{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float2*>(p + 4)};
+}
+//! a cluster's data the momentum kernel prefetches one cluster ahead: its union size and indices, each thread's own
+//! target (list count, view flag, packed records) and, issued after the previous cluster's neighbor loop, the raw
+//! records of the union entries this thread stages
 template<int CH, int SPLIT, bool AVC>
-__global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
+struct MePre
+{
+    static constexpr int NT = kB * SPLIT, S = (CH + NT - 1) / NT;
+    static constexpr int SP = S < 2 ? S : 2; // slots whose records are prefetched (registers); the rest load at staging
+    uint32_t c, U;
+    uint32_t nc;
+    uint8_t  act;
+    RecX     o; // the cluster origin (its first particle)
+    RecX     ri;
+    RecV     vi;
+    RecT     ti;
+    MeC      ci;
+    float    gi[AVC ? 6 : 1];
+    uint32_t js[S];
+};
+template<bool AVC>
+struct MeRaw
+{
+    RecX  x;
+    RecV  v;
+    RecT  t;
+    MeC   c;
+    float g[AVC ? 6 : 1];
+};
+template<bool AVC>
+__device__ __forceinline__ MeRaw<AVC> meLoadRaw(const PairArgs& a, uint32_t j)
+{
+    MeRaw<AVC> r;
+    r.x = a.rx[j], r.v = a.rv[j], r.t = a.rt[j], r.c = meLoadC(a.rc, j);
+    if constexpr (AVC)
+    {
+        r.g[0] = a.dV11[j], r.g[1] = a.dV12[j], r.g[2] = a.dV13[j];
+        r.g[3] = a.dV22[j], r.g[4] = a.dV23[j], r.g[5] = a.dV33[j];
+    }
+    return r;
+}
+
+/*! momentum + energy as a persistent kernel: the momentum records (80 B, 104 with avClean) fill the CU's LDS with one
+ *  workgroup, so nothing overlaps a cluster's dependent load chain (targets -> union indices -> union records ->
+ *  staging) but the loads of the next cluster: each workgroup walks its XCD's clusters and issues the next cluster's
+ *  setup and union-index loads before the neighbor loop and its union records after it, so they land during the
+ *  loop and the share combination.  Measured before this form (Sedov 64M): the kernel without its neighbor loop took
+ *  7.9 of 21.4 ms. */
+template<int CH, int SPLIT, bool AVC>
+__global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, uint32_t numClusters)
 {
     __shared__ float4 sP[CH]; // x, y, z, 1/h
     __shared__ float4 sV[CH]; // vx, vy, vz, c
@@ -712,148 +781,269 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a)
     __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
     __shared__ float4 sG[AVC ? CH : 1];  // dV11, dV12, dV13, dV22 (avClean)
     __shared__ float2 sG2[AVC ? CH : 1]; // dV23, dV33
+    __shared__ float  s_ext[kClusterWaves * SPLIT];
     __shared__ float  s_red[kClusterWaves * SPLIT];
-    const Clu   cu  = setup<SPLIT>(a, s_red);
-    const RecX  ri  = a.rx[cu.iSafe];
-    const RecV  vi  = a.rv[cu.iSafe];
-    const RecT  ti  = a.rt[cu.iSafe];
-    const RecC  ci6 = a.rc[cu.iSafe];
-    const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
-    const float hi = ri.h, mi = ri.m, ci = vi.c, h2 = 2.0f * hi;
-    const float alpha_i = ti.alpha, xmassi = ti.xm, prhoi = ti.prho;
-    const float rhoi    = ti.kx * mi / xmassi;
-    const float rhoiInv = 1.0f / rhoi;
-    const float lxi     = __log2f(xmassi);
-    const float xmi2    = xmassi * xmassi;
-    const float hiInv   = 1.0f / hi;
-    const float hiInv2  = hiInv * hiInv;
-    const float hiInv3  = hiInv2 * hiInv;
-    const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp, AtminLo = a.Atmin * (1.0f - 0x1p-20f);
-    float maxvsignali = 0.0f;
-    float mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
-    bool  res = false;
-    float gradV_i[6] = {0, 0, 0, 0, 0, 0};
-    float eta_crit   = 0.0f;
-    if constexpr (AVC)
+    using Pre                  = MePre<CH, SPLIT, AVC>;
+    constexpr int  NT          = Pre::NT, S = Pre::S, SP = Pre::SP;
+    const int      wave        = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int      sub         = wave & (kClusterWaves - 1);
+    const int      part        = wave / kClusterWaves;
+    const int      tid         = sub * kWave + lane;
+    const uint32_t ucapLoad    = min((uint32_t)CH, a.ucap);
+    constexpr uint32_t kNone   = ~0u; // no further cluster (ids come from clusterList when given, not from [0, n))
+
+    // t-th cluster of this workgroup: virtual block blockIdx.x + t * gridDim.x (gridDim a multiple of 8, so every
+    // virtual block stays on this workgroup's XCD) through the XCD-contiguous mapping of the non-persistent kernels
+    auto clusterAt = [&](uint32_t t) -> uint32_t {
+        const uint64_t b = (uint64_t)blockIdx.x + (uint64_t)t * gridDim.x;
+        if (b >= numClusters) return kNone;
+        const uint32_t blk = xcdBlock((uint32_t)b, numClusters);
+        return a.clusterList ? a.clusterList[blk] : blk;
+    };
+    auto prefetch = [&](uint32_t c) {
+        Pre p;
+        p.c = c;
+        p.U = 0, p.nc = 1, p.act = 1;
+        if (c == kNone) return p;
+        const uint32_t c0 = __builtin_amdgcn_readfirstlane(a.first + c * kCluster), i = c0 + tid;
+        const bool     in = c * kClusterWaves + sub < a.numGroups && i < a.last;
+        const uint32_t iL = in ? i : c0;
+        p.U               = a.ucount[c];
+        p.o               = a.rx[c0];
+        p.nc              = in ? a.nc[i] : 1u;
+        p.act             = (in && a.active) ? a.active[i] : (uint8_t)1;
+        p.ri = a.rx[iL], p.vi = a.rv[iL], p.ti = a.rt[iL], p.ci = meLoadC(a.rc, iL);
+        if constexpr (AVC)
+        {
+            p.gi[0] = a.dV11[iL], p.gi[1] = a.dV12[iL], p.gi[2] = a.dV13[iL];
+            p.gi[3] = a.dV22[iL], p.gi[4] = a.dV23[iL], p.gi[5] = a.dV33[iL];
+        }
+        const uint32_t* un = a.uni + (size_t)c * a.ucap;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+        {
+            const uint32_t u = threadIdx.x + s * NT;
+            p.js[s]          = u < ucapLoad ? un[u] : 0u; // in the cluster's union segment; entries >= U unused
+        }
+        return p;
+    };
+    // every slot is assigned (zeros where nothing is staged), so the records are dead between staging and reload
+    auto loadRecords = [&](const Pre& p, MeRaw<AVC> (&rr)[SP]) {
+        const bool use = p.c != kNone && p.U <= (uint32_t)CH;
+#pragma unroll
+        for (int s = 0; s < SP; ++s)
+        {
+            MeRaw<AVC> r{};
+            if (use && threadIdx.x + s * NT < p.U) r = meLoadRaw<AVC>(a, p.js[s]);
+            rr[s] = r;
+        }
+    };
+
+    float      waveMinDt = INFINITY;
+    uint32_t   t         = 0;
+    Pre        cur       = prefetch(clusterAt(0));
+    MeRaw<AVC> rr[SP];
+    loadRecords(cur, rr);
+    while (cur.c != kNone)
     {
-        const uint32_t q = cu.iSafe;
-        gradV_i[0] = a.dV11[q], gradV_i[1] = a.dV12[q], gradV_i[2] = a.dV13[q];
-        gradV_i[3] = a.dV22[q], gradV_i[4] = a.dV23[q], gradV_i[5] = a.dV33[q];
-        eta_crit   = avEtaCrit(cu.cnt);
-    }
-    neighborLoop<CH, SPLIT, false, SX_ME_LEAN>(
-        cu,
-        [&](uint32_t j, uint32_t slot) {
-            const RecX r   = a.rx[j];
-            const RecV v   = a.rv[j];
-            const RecT t   = a.rt[j];
-            const RecC c6  = a.rc[j];
-            const float rho = t.kx * r.m / t.xm;
+        // ---- cluster setup from the prefetched data (the same fields as setup<SPLIT>)
+        Clu cu;
+        cu.part            = part;
+        cu.tid             = tid;
+        cu.c               = cur.c;
+        cu.gw              = cu.c * kClusterWaves + sub;
+        const uint32_t c0  = a.first + cu.c * kCluster;
+        cu.i               = c0 + tid;
+        cu.valid           = cu.gw < a.numGroups && cu.i < a.last && cur.act != 0;
+        cu.iSafe           = cu.valid ? cu.i : c0;
+        cu.cnt             = 0;
+        if (cu.valid)
+        {
+            const unsigned c1 = cur.nc - 1;
+            cu.cnt            = c1 < a.ngmax ? c1 : a.ngmax;
+        }
+        const uint32_t nw = (cu.cnt + 1) >> 1;
+        cu.wBeg           = nw * cu.part / SPLIT;
+        cu.wEnd           = nw * (cu.part + 1) / SPLIT;
+        cu.U              = cur.U;
+        cu.un             = a.uni + (size_t)cu.c * a.ucap;
+        cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
+        const RecX o      = cur.o;
+        cu.ox = o.x, cu.oy = o.y, cu.oz = o.z;
+        // lanes outside the view read the cluster's first particle, as setup<SPLIT> does
+        const RecX  ri  = cu.valid ? cur.ri : o;
+        const RecV  vi  = cur.vi;
+        const RecT  ti  = cur.ti;
+        RecC ci6;
+        ci6.c11 = cur.ci.a.x, ci6.c12 = cur.ci.a.y, ci6.c13 = cur.ci.a.z, ci6.c22 = cur.ci.a.w;
+        ci6.c23 = cur.ci.b.x, ci6.c33 = cur.ci.b.y;
+        {
+            const float h2  = 2.0f * ri.h;
+            float       ext = 0.0f;
+            if (a.box.pbc[0]) ext = fmaxf(ext, (fabsf(relc(ri.x, cu.ox, a.box, 0)) + h2) * (float)a.box.il[0]);
+            if (a.box.pbc[1]) ext = fmaxf(ext, (fabsf(relc(ri.y, cu.oy, a.box, 1)) + h2) * (float)a.box.il[1]);
+            if (a.box.pbc[2]) ext = fmaxf(ext, (fabsf(relc(ri.z, cu.oz, a.box, 2)) + h2) * (float)a.box.il[2]);
+            ext = waveMax(ext);
+            if (lane == 0) s_ext[wave] = ext;
+            __syncthreads(); // also: every thread is done with the previous cluster's records and share sums
+            float e = s_ext[0];
+            for (int w = 1; w < kClusterWaves * SPLIT; ++w)
+                e = fmaxf(e, s_ext[w]);
+            cu.pbc = __builtin_amdgcn_readfirstlane(e >= 0.49f ? 1 : 0);
+        }
+
+        auto stageRaw = [&](const MeRaw<AVC>& q, uint32_t slot) {
+            const RecX& r   = q.x;
+            const RecT& tq  = q.t;
+            const MeC&  c6  = q.c;
+            const float rho = tq.kx * r.m / tq.xm;
             sP[slot]        = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
                                    relc(r.z, cu.oz, a.box, 2), 1.0f / r.h);
-            sV[slot]        = make_float4(v.vx, v.vy, v.vz, v.c);
-            sT[slot]        = make_float4(r.m, t.xm, rho, r.m * t.prho);
-            sA[slot]        = make_float4(t.alpha, c6.c11, c6.c12, c6.c13);
-            sB[slot]        = make_float4(c6.c22, c6.c23, c6.c33, r.m / rho);
+            sV[slot]        = make_float4(q.v.vx, q.v.vy, q.v.vz, q.v.c);
+            sT[slot]        = make_float4(r.m, tq.xm, rho, r.m * tq.prho);
+            sA[slot]        = make_float4(tq.alpha, c6.a.x, c6.a.y, c6.a.z);
+            sB[slot]        = make_float4(c6.a.w, c6.b.x, c6.b.y, r.m / rho);
             if constexpr (AVC)
             {
-                sG[slot]  = make_float4(a.dV11[j], a.dV12[j], a.dV13[j], a.dV22[j]);
-                sG2[slot] = make_float2(a.dV23[j], a.dV33[j]);
+                sG[slot]  = make_float4(q.g[0], q.g[1], q.g[2], q.g[3]);
+                sG2[slot] = make_float2(q.g[4], q.g[5]);
             }
-        },
-        [&](uint32_t p) {
-            RecM<AVC> r;
-            r.p = sP[p], r.v = sV[p], r.t = sT[p], r.a = sA[p], r.b = sB[p];
-            if constexpr (AVC) r.g = sG[p], r.g2 = sG2[p];
-            return r;
-        },
-        [&](const RecM<AVC>& r) {
-            const float4 &P = r.p, &V = r.v, &T = r.t, &A = r.a, &B = r.b;
-            float         rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
-            pbcRule(cu, a.box, h2, rx, ry, rz);
-            const float r2     = rx * rx + ry * ry + rz * rz;
-            const float rinv   = rsqrtf(r2);
-            const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
-            const float hjInv  = P.w;
-            const float hjInv2 = hjInv * hjInv;
-            const float hjInv3 = hjInv2 * hjInv;
-            const float t1 = r2 * hiInv2, t2 = r2 * hjInv2; // squares of v1 = r/h_i, v2 = r/h_j
-            const float Wi     = hiInv3 * kernelWt(t1);
-            const float Wj     = hjInv3 * kernelWt(t2);
-            // IAD directions u = c r; the reference's termA = -u W (momentum_energy_kern.hpp:134-146) is applied by
-            // folding -W into the per-side coefficients below
-            const float u1i = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
-            const float u2i = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
-            const float u3i = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;
-            const float u1j = A.y * rx + A.z * ry + A.w * rz;
-            const float u2j = A.z * rx + B.x * ry + B.y * rz;
-            const float u3j = A.w * rx + B.y * ry + B.z * rz;
-            const float mj = T.x, rhoj = T.z, cj = V.w;
-            float       rv = rx * vx_ij + ry * vy_ij + rz * vz_ij;
-            if constexpr (AVC)
+        };
+        bool res = false;
+        if (cu.U <= (uint32_t)CH)
+        {
+#pragma unroll
+            for (int s = 0; s < S; ++s)
             {
-                const float gj[6] = {r.g.x, r.g.y, r.g.z, r.g.w, r.g2.x, r.g2.y};
-                rv += avRvCorrection<false>(rx, ry, rz, r2 * rinv * fminf(hiInv, hjInv), eta_crit, gradV_i, gj);
+                const uint32_t u = threadIdx.x + s * NT;
+                if (u < cu.U) stageRaw(s < SP ? rr[s < SP ? s : 0] : meLoadRaw<AVC>(a, cur.js[s]), u);
             }
-            const float wij = rv * rinv;
-            // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
-            const float vij_signal = (alpha_i + A.x) * 0.25f * (ci + cj) - 2.0f * wij;
-            const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
-            const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
-            maxvsignali            = vijsignal > maxvsignali ? vijsignal : maxvsignali;
-            // Atwood = |rho_i - rho_j| / (rho_i + rho_j); the wave-uniform test of the common case (below Atmin
-            // everywhere) multiplies instead of dividing, against a threshold lowered by 2^-20 so that every lane
-            // whose rounded quotient reaches Atmin takes the exact branch
-            const float drho = fabsf(rhoi - rhoj), srho = rhoi + rhoj;
-            float       a_mom, b_mom;
-            if (__ballot(drho >= AtminLo * srho) == 0)
-            {
-                a_mom = xmi2; // the common case: below Atmin in every lane
-                b_mom = T.y * T.y;
-            }
-            else atwoodWeights(drho * __frcp_rn(srho), Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
-            const float a_visc     = mj * rhoiInv * halfVisc;
-            const float b_visc     = B.w * halfVisc;
-            const float momentum_i = mj * prhoi * a_mom;
-            const float momentum_j = T.w * b_mom;
-            // v_ij . termA_i and v_ij . termA_j
-            const float di = -Wi * (vx_ij * u1i + vy_ij * u2i + vz_ij * u3i);
-            const float dj = -Wj * (vx_ij * u1j + vy_ij * u2j + vz_ij * u3j);
-            energy += mj * a_mom * di;
-            a_visc_energy += a_visc * di + b_visc * dj;
-            // momentum_i termA_i + momentum_j termA_j + a_visc (a_visc termA_i + b_visc termA_j)
-            const float ki = -(momentum_i + a_visc) * Wi, kj = -(momentum_j + b_visc) * Wj;
-            mx += ki * u1i + kj * u1j;
-            my += ki * u2i + kj * u2j;
-            mz += ki * u3i + kj * u3j;
-        },
-        res);
-    {
-        float v[6] = {mx, my, mz, energy, a_visc_energy, maxvsignali};
-        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 32u, true);
-        mx = v[0], my = v[1], mz = v[2], energy = v[3], a_visc_energy = v[4], maxvsignali = v[5];
+            __syncthreads();
+            res = true;
+        }
+        // the next cluster's setup and union indices load during this cluster's neighbor loop
+        const Pre nxt = prefetch(clusterAt(++t));
+
+        const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
+        const float hi = ri.h, mi = ri.m, ci = vi.c, h2 = 2.0f * hi;
+        const float alpha_i = ti.alpha, xmassi = ti.xm, prhoi = ti.prho;
+        const float rhoi    = ti.kx * mi / xmassi;
+        const float rhoiInv = 1.0f / rhoi;
+        const float lxi     = __log2f(xmassi);
+        const float xmi2    = xmassi * xmassi;
+        const float hiInv   = 1.0f / hi;
+        const float hiInv2  = hiInv * hiInv;
+        const float hiInv3  = hiInv2 * hiInv;
+        const float Atmin = a.Atmin, Atmax = a.Atmax, ramp = a.ramp, AtminLo = a.Atmin * (1.0f - 0x1p-20f);
+        float maxvsignali = 0.0f;
+        float mx = 0, my = 0, mz = 0, energy = 0, a_visc_energy = 0;
+        float gradV_i[6] = {0, 0, 0, 0, 0, 0};
+        float eta_crit   = 0.0f;
+        if constexpr (AVC)
+        {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                gradV_i[k] = cur.gi[k];
+            eta_crit = avEtaCrit(cu.cnt);
+        }
+        neighborLoop<CH, SPLIT, false, SX_ME_LEAN>(
+            cu, [&](uint32_t j, uint32_t slot) { stageRaw(meLoadRaw<AVC>(a, j), slot); },
+            [&](uint32_t p) {
+                RecM<AVC> r;
+                r.p = sP[p], r.v = sV[p], r.t = sT[p], r.a = sA[p], r.b = sB[p];
+                if constexpr (AVC) r.g = sG[p], r.g2 = sG2[p];
+                return r;
+            },
+            [&](const RecM<AVC>& r) {
+                const float4 &P = r.p, &V = r.v, &T = r.t, &A = r.a, &B = r.b;
+                float         rx = xi - P.x, ry = yi - P.y, rz = zi - P.z;
+                pbcRule(cu, a.box, h2, rx, ry, rz);
+                const float r2     = rx * rx + ry * ry + rz * rz;
+                const float rinv   = rsqrtf(r2);
+                const float vx_ij  = vi.vx - V.x, vy_ij = vi.vy - V.y, vz_ij = vi.vz - V.z;
+                const float hjInv  = P.w;
+                const float hjInv2 = hjInv * hjInv;
+                const float hjInv3 = hjInv2 * hjInv;
+                const float t1 = r2 * hiInv2, t2 = r2 * hjInv2; // squares of v1 = r/h_i, v2 = r/h_j
+                const float Wi     = hiInv3 * kernelWt(t1);
+                const float Wj     = hjInv3 * kernelWt(t2);
+                // IAD directions u = c r; the reference's termA = -u W (momentum_energy_kern.hpp:134-146) is applied
+                // by folding -W into the per-side coefficients below
+                const float u1i = ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz;
+                const float u2i = ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz;
+                const float u3i = ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz;
+                const float u1j = A.y * rx + A.z * ry + A.w * rz;
+                const float u2j = A.z * rx + B.x * ry + B.y * rz;
+                const float u3j = A.w * rx + B.y * ry + B.z * rz;
+                const float mj = T.x, rhoj = T.z, cj = V.w;
+                float       rv = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+                if constexpr (AVC)
+                {
+                    const float gj[6] = {r.g.x, r.g.y, r.g.z, r.g.w, r.g2.x, r.g2.y};
+                    rv += avRvCorrection<false>(rx, ry, rz, r2 * rinv * fminf(hiInv, hjInv), eta_crit, gradV_i, gj);
+                }
+                const float wij = rv * rinv;
+                // artificial_viscosity (kernels.hpp:70-84), halved for the a_visc average below
+                const float vij_signal = (alpha_i + A.x) * 0.25f * (ci + cj) - 2.0f * wij;
+                const float halfVisc   = wij < 0.0f ? -0.5f * vij_signal * wij : 0.0f;
+                const float vijsignal  = 0.5f * (ci + cj) - 2.0f * wij;
+                maxvsignali            = vijsignal > maxvsignali ? vijsignal : maxvsignali;
+                // Atwood = |rho_i - rho_j| / (rho_i + rho_j); the wave-uniform test of the common case (below Atmin
+                // everywhere) multiplies instead of dividing, against a threshold lowered by 2^-20 so that every lane
+                // whose rounded quotient reaches Atmin takes the exact branch
+                const float drho = fabsf(rhoi - rhoj), srho = rhoi + rhoj;
+                float       a_mom, b_mom;
+                if (__ballot(drho >= AtminLo * srho) == 0)
+                {
+                    a_mom = xmi2; // the common case: below Atmin in every lane
+                    b_mom = T.y * T.y;
+                }
+                else atwoodWeights(drho * __frcp_rn(srho), Atmin, Atmax, ramp, xmassi, lxi, T.y, a_mom, b_mom);
+                const float a_visc     = mj * rhoiInv * halfVisc;
+                const float b_visc     = B.w * halfVisc;
+                const float momentum_i = mj * prhoi * a_mom;
+                const float momentum_j = T.w * b_mom;
+                // v_ij . termA_i and v_ij . termA_j
+                const float di = -Wi * (vx_ij * u1i + vy_ij * u2i + vz_ij * u3i);
+                const float dj = -Wj * (vx_ij * u1j + vy_ij * u2j + vz_ij * u3j);
+                energy += mj * a_mom * di;
+                a_visc_energy += a_visc * di + b_visc * dj;
+                // momentum_i termA_i + momentum_j termA_j + a_visc (a_visc termA_i + b_visc termA_j)
+                const float ki = -(momentum_i + a_visc) * Wi, kj = -(momentum_j + b_visc) * Wj;
+                mx += ki * u1i + kj * u1j;
+                my += ki * u2i + kj * u2j;
+                mz += ki * u3i + kj * u3j;
+            },
+            res);
+        // the next cluster's union records load during the share combination and this cluster's stores
+        loadRecords(nxt, rr);
+        {
+            float v[6] = {mx, my, mz, energy, a_visc_energy, maxvsignali};
+            combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 32u, true);
+            mx = v[0], my = v[1], mz = v[2], energy = v[3], a_visc_energy = v[4], maxvsignali = v[5];
+        }
+        float dt_lane = INFINITY;
+        if (cu.valid && cu.part == 0)
+        {
+            if (a_visc_energy < 0.0f) a_visc_energy = 0.0f;
+            a.du[cu.i] = a.K * (double)(prhoi * energy + 0.5f * a_visc_energy);
+            a.ax[cu.i] = (float)(-a.K * (double)mx);
+            a.ay[cu.i] = (float)(-a.K * (double)my);
+            a.az[cu.i] = (float)(-a.K * (double)mz);
+            dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
+            if (a.dtOut) a.dtOut[cu.i] = dt_lane;
+        }
+        // wave min -> per-group minimum, and the workgroup's running minimum (momentum_energy_gpu.cu:94-118)
+        const float wmin = waveMin(dt_lane);
+        if (a.groupDt != nullptr && lane == 0 && cu.part == 0 && cu.gw < a.numGroups)
+        {
+            float old        = a.groupDt[cu.gw];
+            a.groupDt[cu.gw] = wmin < old ? wmin : old;
+        }
+        waveMinDt = fminf(waveMinDt, wmin);
+        cur       = nxt;
     }
-    float dt_lane = INFINITY;
-    if (cu.valid && cu.part == 0)
-    {
-        if (a_visc_energy < 0.0f) a_visc_energy = 0.0f;
-        a.du[cu.i] = a.K * (double)(prhoi * energy + 0.5f * a_visc_energy);
-        a.ax[cu.i] = (float)(-a.K * (double)mx);
-        a.ay[cu.i] = (float)(-a.K * (double)my);
-        a.az[cu.i] = (float)(-a.K * (double)mz);
-        dt_lane    = tsKCourant(maxvsignali, hi, ci, a.Kcour);
-        if (a.dtOut) a.dtOut[cu.i] = dt_lane;
-    }
-    // wave min -> workgroup min -> one atomic per cluster (momentum_energy_gpu.cu:94-118)
-    const float wmin = waveMin(dt_lane);
-    const int   wave = threadIdx.x >> 6;
-    if (a.groupDt != nullptr && (threadIdx.x & 63) == 0 && cu.part == 0 && cu.gw < a.numGroups)
-    {
-        float old         = a.groupDt[cu.gw];
-        a.groupDt[cu.gw] = wmin < old ? wmin : old;
-    }
-    __syncthreads(); // s_red is reused
-    if ((threadIdx.x & 63) == 0) s_red[wave] = wmin;
+    if (lane == 0) s_red[wave] = waveMinDt;
     __syncthreads();
     if (threadIdx.x == 0)
     {
@@ -994,7 +1184,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #define SX_SPLIT_AV 2
 #endif
 #ifndef SX_SPLIT_ME
-#define SX_SPLIT_ME 4 // 16 waves on the CU's one momentum workgroup (104 VGPRs with one record in flight: four per SIMD)
+#define SX_SPLIT_ME 3 // 12 waves on the CU's one (persistent) momentum workgroup: the loop's 104 VGPRs + the next cluster's prefetch
 #endif
 #ifndef SX_SPLIT_ME_AVC
 #define SX_SPLIT_ME_AVC 2 // the avClean variant needs 190 VGPRs: two waves per SIMD
@@ -1051,12 +1241,29 @@ static void reduceBlockDt(const PairArgs& a, hipStream_t s)
     if (a.blockDt) reduceBlockDtKernel<<<1, 1024, 0, s>>>(a.blockDt, clusters(a), a.minDt);
 }
 
+//! workgroups of the persistent momentum kernel: one per CU (its records fill the LDS), a multiple of 8 (XCDs)
+static uint32_t momentumGrid(uint32_t numClusters)
+{
+    static int cus[64] = {};
+    int        dev     = 0;
+    (void)hipGetDevice(&dev);
+    int& n = cus[dev & 63];
+    if (n == 0)
+    {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        n = std::max(8, n & ~7);
+    }
+    return std::min<uint32_t>(numClusters, (uint32_t)n);
+}
+
 void momentumEnergy(const PairArgs& a, hipStream_t s)
 {
-    if (!a.numGroups || !clusters(a)) return;
-    if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME_AVC, true><<<clusters(a), kB * SX_SPLIT_ME_AVC, 0, s>>>(a);
-    else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<clusters(a), kB * SX_SPLIT_ME, 0, s>>>(a);
-    reduceBlockDt(a, s);
+    const uint32_t ncl = clusters(a);
+    if (!a.numGroups || !ncl) return;
+    const uint32_t grid = momentumGrid(ncl);
+    if (a.avClean) momentumEnergyKernel<kChMeAvc, SX_SPLIT_ME_AVC, true><<<grid, kB * SX_SPLIT_ME_AVC, 0, s>>>(a, ncl);
+    else momentumEnergyKernel<kChMe, SX_SPLIT_ME, false><<<grid, kB * SX_SPLIT_ME, 0, s>>>(a, ncl);
+    if (a.blockDt) reduceBlockDtKernel<<<1, 1024, 0, s>>>(a.blockDt, grid, a.minDt);
 }
 // std propagator: the IAD kernel without velocity derivatives (16 B records), momentum with 68 B records
 constexpr int kChIadStd = 2048, kChMeStd = 2048;
