@@ -544,14 +544,15 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
             float         rx = xi - q.x, ry = yi - q.y, rz = zi - q.z;
             pbcRule(cu, a.box, h2, rx, ry, rz);
             const float W      = kernelWt((rx * rx + ry * ry + rz * rz) * hiInv2);
-            const float volj_w = q.w * W;
-            t11 += rx * rx * volj_w;
-            t12 += rx * ry * volj_w;
-            t13 += rx * rz * volj_w;
-            t22 += ry * ry * volj_w;
-            t23 += ry * rz * volj_w;
-            t33 += rz * rz * volj_w;
             const float rW[3] = {rx * W, ry * W, rz * W};
+            // tau_ab += r_a r_b vol_j W: (r_a W vol_j) r_b, three products shared by the six sums
+            const float px = rW[0] * q.w, py = rW[1] * q.w, pz = rW[2] * q.w;
+            t11 = fmaf(px, rx, t11);
+            t12 = fmaf(px, ry, t12);
+            t13 = fmaf(px, rz, t13);
+            t22 = fmaf(py, ry, t22);
+            t23 = fmaf(py, rz, t23);
+            t33 = fmaf(pz, rz, t33);
             const float f[3]  = {(v.x - vi.vx) * v.w, (v.y - vi.vy) * v.w, (v.z - vi.vz) * v.w};
 #pragma unroll
             for (int aa = 0; aa < 3; ++aa)
@@ -652,14 +653,12 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
             const float rv    = rx * vx_ij + ry * vy_ij + rz * vz_ij;
             const float vsig  = rv < 0.0f ? ci + v.w - 3.0f * rv * rinv : 0.0f;
             vijsignal_i       = fmaxf(vijsignal_i, vsig);
-            const float Wi     = hiInv3K * kernelWt(r2 * hiInv2);
-            const float termA1 = -(ci6.c11 * rx + ci6.c12 * ry + ci6.c13 * rz) * Wi;
-            const float termA2 = -(ci6.c12 * rx + ci6.c22 * ry + ci6.c23 * rz) * Wi;
-            const float termA3 = -(ci6.c13 * rx + ci6.c23 * ry + ci6.c33 * rz) * Wi;
-            const float factor = q.w * (divv_i - r.s);
-            gx += factor * termA1;
-            gy += factor * termA2;
-            gz += factor * termA3;
+            // termA_j = -(c_i r) K h_i^-3 W_j is linear in r with the target's c_i: the pass sums s = sum_j factor_j
+            // W_j r and c_i is applied once after it (same terms, different float summation order)
+            const float fw = kernelWt(r2 * hiInv2) * (q.w * (divv_i - r.s));
+            gx = fmaf(fw, rx, gx);
+            gy = fmaf(fw, ry, gy);
+            gz = fmaf(fw, rz, gz);
         },
         res);
     {
@@ -668,6 +667,12 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         gx = v[0], gy = v[1], gz = v[2], vijsignal_i = v[3];
     }
     if (!cu.valid || cu.part != 0) return;
+    {
+        const float sx = gx, sy = gy, sz = gz;
+        gx = -hiInv3K * (ci6.c11 * sx + ci6.c12 * sy + ci6.c13 * sz);
+        gy = -hiInv3K * (ci6.c12 * sx + ci6.c22 * sy + ci6.c23 * sz);
+        gz = -hiInv3K * (ci6.c13 * sx + ci6.c23 * sy + ci6.c33 * sz);
+    }
     const float graddivv = norm3(gx, gy, gz);
     float       alphaloc = 0.0f;
     if (divv_i < 0.0f)
