@@ -45,8 +45,8 @@
 
 // Two builds of this file: the default one (large capacities: 2048 candidate leaves, 2^16 candidate particles per
 // cluster, 53 KB of LDS, three workgroups per CU) and, with SX_NS_SMALL, a compact one in namespace sx::small
-// (1024 leaves, 2^14 particles, 36 KB, four workgroups per CU; Makefile).  findNeighbors runs the compact one
-// and falls back to the large one when a cluster exceeds its capacities.
+// (1024 leaves, 2^14 particles, 36 KB, four workgroups per CU; Makefile).  findNeighbors runs the compact one;
+// a cluster that exceeds its capacities is left unwritten and listed, and the large one redoes the listed clusters.
 #ifdef SX_NS_SMALL
 namespace sx
 {
@@ -235,14 +235,18 @@ findNeighborsKernel(NsArgs a)
     __shared__ uint32_t    s_wsum[kClusterWaves];
     __shared__ NsStreamLds s_str;
     __shared__ int         s_numCand;
+    __shared__ int         s_abandon; // the compact build gives this cluster up (capacity): the large build redoes it
     __shared__ uint4       s_cst[kClusterWaves]; // per-wave statistics
     __shared__ uint32_t    s_next;               // the cluster this workgroup takes next
     __shared__ uint2       s_bfsCnt[kClusterWaves];
     double4* const s_reg = s_str.reg;            // search regions: pairs {cx, cy, cz, R}, {hx, hy, hz, owner wave}
 
-    // the fallback launch (a.gate) exits at once unless the compact build overflowed
-    if (a.gate && *a.gate == 0u) return;
-    const uint32_t numClusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    // the fallback launch (a.redoList) redoes the clusters the compact build gave up: redoList[0] of them, ids at
+    // redoList[1..]; it exits at once when there are none
+    const uint32_t numClusters =
+        a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[0]) : (a.numGroups + kClusterWaves - 1) / kClusterWaves;
+    if (numClusters == 0) return;
+    if (a.redo && blockIdx.x == 0 && threadIdx.x == 0) a.stats[11] = 1u; // the compact build ran first
     const int      wave        = threadIdx.x >> 6;
     const int      lane        = threadIdx.x & 63;
     NsWaveLds&     wl          = s_str.w[wave];
@@ -250,9 +254,10 @@ findNeighborsKernel(NsArgs a)
     uint64_t* const maskRow = a.hitMasks + ((size_t)blockIdx.x * kClusterWaves + wave) * kBatch * kWave + lane;
     if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters);
     __syncthreads();
-    uint32_t c = s_next;
-    while (c < numClusters)
+    uint32_t ci = s_next; // this workgroup's work item: a cluster, or a position in the redo list
+    while (ci < numClusters)
     {
+    const uint32_t c = a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[1 + ci]) : ci;
     __syncthreads(); // every thread has read s_next
     // the next ticket of this workgroup's XCD range is drawn now and read at the end of the cluster, so the atomic's
     // round trip overlaps the search instead of stalling wave 0 before its first barrier
@@ -391,7 +396,8 @@ findNeighborsKernel(NsArgs a)
         nzq = 0;
     };
 
-    int numCand = 0;
+    int  numCand   = 0;
+    bool abandoned = false;
     while (true)
     {
         // ---- 1./2. search regions, then the candidate leaves within reach of one, numbered into the candidate space
@@ -507,12 +513,25 @@ findNeighborsKernel(NsArgs a)
 #ifdef SX_NS_SMALL
                 if (a.forceOverflow) f |= 4u; // test hook (sx_set_search_mode 3): exercise the device-side fallback
 #endif
-                if (f) atomicOr(&a.stats[0], 1u | f);
+                // with a redo list (compact build first) an over-capacity cluster is handed to the large build,
+                // otherwise it is an error of the search
+                s_abandon = f && a.redo ? 1 : 0;
+                if (f && a.redo)
+                {
+                    a.redo[1 + atomicAdd(&a.redo[0], 1u)] = c;
+                    atomicAdd(&a.stats[10], 1u);
+                }
+                else if (f) atomicOr(&a.stats[0], 1u | f);
                 s_numCand = f ? 0 : nCand;
             }
         }
         __syncthreads();
         numCand = s_numCand;
+        if (s_abandon)
+        {
+            abandoned = true; // nothing of this cluster is written: h, nc, lists and union stay for the redo
+            break;
+        }
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
@@ -855,7 +874,7 @@ findNeighborsKernel(NsArgs a)
 
     // ---- 5. cluster union: prefix popcount of the bitmap, union entries, list expansion ------------------------
     uint32_t ucnt = 0;
-    if (local)
+    if (local && !abandoned)
     {
         const uint32_t nw  = (s_cOff[numCand] + 31) / 32;
         const uint32_t per = (nw + kCluster - 1) / kCluster; // words per thread, consecutive
@@ -956,7 +975,7 @@ findNeighborsKernel(NsArgs a)
         if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
     }
 
-    if (valid)
+    if (valid && !abandoned)
     {
         a.nc[i] = count + 1;
         if (a.iterateH) a.h[i] = hi;
@@ -969,12 +988,12 @@ findNeighborsKernel(NsArgs a)
     const unsigned long long tested = waveSum(valid ? candTested : 0ull);
     if (lane == 0)
     {
-        if (nfail) atomicAdd(&a.stats[1], nfail); // failures only: rare
+        if (nfail && !abandoned) atomicAdd(&a.stats[1], nfail); // failures only: rare
         s_cst[wave] = make_uint4(maxCnt, (uint32_t)nstore, (uint32_t)tested, 0u);
     }
     if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters, ticket);
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0 && !abandoned)
     {
         uint4 t = s_cst[0];
         for (int w = 1; w < kClusterWaves; ++w)
@@ -986,7 +1005,7 @@ findNeighborsKernel(NsArgs a)
         a.clStats[c] = t;
     }
     __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
-    c = s_next;
+    ci = s_next;
     }
 }
 
@@ -1049,7 +1068,7 @@ hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
     const unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    findNeighborsKernel<<<std::min(searchGrid(), clusters), kCluster, 0, s>>>(a);
+    findNeighborsKernel<<<std::min(searchGrid(), clusters), kCluster, 0, s>>>(a); // a redo list holds <= clusters
     return hipGetLastError();
 }
 
@@ -1061,23 +1080,6 @@ size_t     searchScratchWords();
 } // namespace small
 
 size_t searchScratchBytes() { return std::max(searchScratchWords(), small::searchScratchWords()) * sizeof(uint64_t); }
-
-//! after the compact build: if it overflowed (stats bits 2 / 4), restore the saved h of its range
-__global__ void fallbackRestoreKernel(float* h, const float* hSave, uint32_t n, const uint32_t* stats)
-{
-    if (!(stats[0] & 6u)) return;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
-        h[k] = hSave[k];
-}
-
-//! ... and reset the statistics, raising the gate word [10] of the large-build launch; [11] = compact ran first
-__global__ void fallbackGateKernel(uint32_t* stats)
-{
-    const bool redo = (stats[0] & 6u) != 0u;
-    __syncthreads();
-    if (threadIdx.x < kStatsWords)
-        stats[threadIdx.x] = threadIdx.x == 10 ? (redo ? 1u : 0u) : threadIdx.x == 11 ? 1u : (redo ? 0u : stats[threadIdx.x]);
-}
 
 //! per-cluster statistics -> stats[2] (max count), u64 stats[4] (stored), [6] (tested), [8] (union entries)
 __global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
@@ -1125,19 +1127,18 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
         if ((e = findNeighborsOnce(a, s))) return e;
         return reduceClusterStats(a, s);
     }
-    const uint32_t n = a.last - a.first;
-    if (a.iterateH &&
-        (e = hipMemcpyAsync(a.hSave, a.h + a.first, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s)))
-        return e;
-    NsArgs c = a;
+    // compact build first: a cluster over its capacities is not written and goes to a redo list (in the hSave
+    // scratch: clusters + 1 words fit in its last - first floats), which the large build then takes -- only those
+    // clusters, no host synchronisation, h untouched for them
+    uint32_t* redo = reinterpret_cast<uint32_t*>(a.hSave);
+    if ((e = hipMemsetAsync(redo, 0, sizeof(uint32_t), s))) return e;
+    NsArgs c        = a;
     c.forceOverflow = mode == 3;
+    c.redo          = redo;
     if ((e = small::findNeighborsOnce(c, s))) return e;
-    if (a.iterateH)
-        fallbackRestoreKernel<<<std::min(2048u, (n + 255) / 256), 256, 0, s>>>(a.h + a.first, a.hSave, n, a.stats);
-    fallbackGateKernel<<<1, 64, 0, s>>>(a.stats);
-    NsArgs b = a;
-    b.gate   = a.stats + 10;
-    b.work   = a.work + 8;
+    NsArgs b   = a;
+    b.redoList = redo;
+    b.work     = a.work + 8;
     if ((e = findNeighborsOnce(b, s))) return e;
     return reduceClusterStats(a, s);
 }

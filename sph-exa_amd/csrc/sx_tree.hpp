@@ -148,8 +148,8 @@ struct NbLists
 };
 
 constexpr int kStatsWords = 28; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
-                                //!< neighbors, [6] candidates tested, [8] union entries, [10] compact-build
-                                //!< overflow redone by the large build, [11] the compact build ran first,
+                                //!< neighbors, [6] candidates tested, [8] union entries, [10] clusters the
+                                //!< compact build handed to the large one, [11] the compact build ran first,
                                 //!< [12..27] phase probes of a profiling build
 
 //! which search build runs: the compact one (four workgroups per CU) with a device-side fallback to the large one,
@@ -159,20 +159,23 @@ struct NsPolicy
 {
     int      mode{0};        //!< 0 auto, 1 large build only, 2 compact first (fallback on overflow), 3 = 2 with a
                              //!< forced overflow of every cluster (test hook: the device-side fallback path)
-    int      largeRuns{0};   //!< searches left that go straight to the large build (after a compact overflow)
+    int      largeRuns{0};   //!< searches left that go straight to the large build (after many compact overflows)
     uint64_t prevStored{0};  //!< stored neighbors of the previous search
     uint32_t prevTargets{0}; //!< its target count
-    uint32_t lastBuild{0};   //!< 0 compact, 1 large, 2 compact overflowed and redone by the large build
+    uint32_t lastBuild{0};   //!< 0 compact, 1 large, 2 compact with some clusters redone by the large build
 
     void observe(const uint32_t* statsHost, uint32_t targets)
     {
         lastBuild = statsHost[10] ? 2u : (statsHost[11] ? 0u : 1u);
-        if (statsHost[10]) largeRuns = 64;
+        // redoing a few clusters costs little; when more than an eighth of them overflow, go large directly
+        const uint64_t clusters = (targets + kCluster - 1) / kCluster;
+        if (8ull * statsHost[10] > clusters) largeRuns = 64;
         prevStored  = *reinterpret_cast<const uint64_t*>(statsHost + 4);
         prevTargets = targets;
     }
-    //! the compact build spills registers in the hit-append loop: with many neighbors per target (> 105 on
-    //! average in the previous search) the large build is faster
+    //! the large build directly only after a search in which many clusters overflowed the compact one (with the
+    //! deferred list expansion the compact build stays faster at every neighbor count measured: Noh -n 300 at 100-120
+    //! stored neighbors per target, compact + redo 9.3-10.5 ms against 12.0-14.8 ms for the large build)
     bool useLarge()
     {
         if (largeRuns > 0)
@@ -180,7 +183,7 @@ struct NsPolicy
             --largeRuns;
             return true;
         }
-        return prevTargets && prevStored > 105ull * prevTargets;
+        return false;
     }
 };
 
@@ -219,12 +222,13 @@ struct NsArgs
     uint4*          clStats;   // per cluster {max count, stored, tested, union}: reduced into stats by one small
                                // kernel after the search (per-wave atomics on the stats words serialised: 10 ms of a
                                // 64M-particle search)
-    // optional (both non-null): the compact build runs first (policy permitting) with h saved to hSave
-    // (last - first floats); if one of its capacities was exceeded, kernels on the stream restore h and redo the
-    // range with the large build -- no host synchronisation
+    // optional (both non-null): the compact build runs first (policy permitting); a cluster that exceeds one of its
+    // capacities is left unwritten and listed in hSave (scratch of last - first floats, used as a u32 list), and the
+    // large build then redoes exactly the listed clusters -- no host synchronisation
     float*          hSave;
     NsPolicy*       policy;
-    const uint32_t* gate; // set by findNeighbors for the fallback launch: the kernel runs only if *gate != 0
+    uint32_t*       redo;           // set by findNeighbors, compact build: [0] count, [1..] clusters it gave up
+    const uint32_t* redoList;       // set by findNeighbors, large build: process only these clusters
     int             forceOverflow; // compact build only: report a capacity overflow for every cluster (mode 3)
     // persistent-grid state (findNeighbors sets up both): 16 work counters (8 XCD ranges per launch) and the
     // per-workgroup hit-mask scratch, searchScratchBytes() bytes

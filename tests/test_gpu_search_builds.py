@@ -1,11 +1,12 @@
 """The two neighbor-search builds and the device-side fallback between them (sx_neighbors.hip findNeighbors).
 
-The compact build (four workgroups per CU) runs first; when a cluster exceeds its capacities the kernels on the
-stream restore h from the saved copy and redo the whole range with the large build, without a host sync.  All
-paths must give bit-identical h, nc, neighbor lists, union sizes and statistics:
-  mode 1 large only, mode 2 compact, mode 3 compact with a forced overflow of every cluster (the fallback path,
-  including the h restore after the compact build's h iteration mutated h), with the h-nc iteration on, on inputs
-  where it actually iterates (h0 far from the converged value), plus the reference oracle's sets as the anchor.
+The compact build (four workgroups per CU) runs first; a cluster that exceeds its capacities is left unwritten (h,
+nc, lists, union) and listed, and the large build then redoes exactly the listed clusters, without a host sync.
+All paths must give bit-identical h, nc, neighbor lists, union sizes and statistics:
+  mode 1 large only, mode 2 compact (on Noh some sphere-surface clusters go to the large build), mode 3 compact
+  with a forced overflow of every cluster (every cluster redone by the large build from the untouched h), with the
+  h-nc iteration on, on inputs where it actually iterates (h0 far from the converged value), plus the reference
+  oracle's sets as the anchor.
 """
 import ctypes as C
 
