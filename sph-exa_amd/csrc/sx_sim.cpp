@@ -1561,7 +1561,7 @@ extern "C"
             na.stats          = s->stats;
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
             na.prefilter      = 1;
-            na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(1, s->last - s->first));
+            na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(2, s->last - s->first)); // the redo list
             na.policy         = &s->nsPolicy;
             na.clStats        = s->mem.get<uint4>("ns.clstats", (na.numGroups + kClusterWaves - 1) / kClusterWaves);
             na.work           = s->mem.get<uint32_t>("ns.work", 16);
