@@ -355,7 +355,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     s_tgt[wave][lane] = make_float4(txr, tyr, tzr, hi); // SX_LOAD_QUARTER: one LDS read instead of five bpermutes
     float qx = 0, qy = 0, qz = 0, qh = 0;
     bool  qok = false;
-    float fq[4] = {0, 0, 0, 0}, fo[4] = {0, 0, 0, 0};
+    // per quarter its partial sums, folded across the four subs once per flush (not once per window / chunk)
+    float fq[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}}, fo[4] = {0, 0, 0, 0};
 #define SX_LOAD_QUARTER(qq)                                                                                            \
     {                                                                                                                  \
         const float4 t_ = s_tgt[wave][16 * (qq) + tq];                                                                 \
@@ -365,10 +366,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
 #define SX_FOLD_QUARTER(qq)                                                                                            \
     _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_)                                                                  \
     {                                                                                                                  \
-        const float v_ = rowSum4(fq[c_]);                                                                              \
+        const float v_ = rowSum4(fq[qq][c_]);                                                                          \
         if (sub == (qq)) fo[c_] += v_;                                                                                 \
-        fq[c_] = 0.0f;                                                                                                 \
+        fq[qq][c_] = 0.0f;                                                                                             \
     }
+#define SX_FOLD_ALL() SX_FOLD_QUARTER(0) SX_FOLD_QUARTER(1) SX_FOLD_QUARTER(2) SX_FOLD_QUARTER(3)
 #define SX_FLUSH_FO()                                                                                                  \
     _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_) acc[c_] += (double)fo[c_], fo[c_] = 0.0f;
     auto flushM2P = [&]() {
@@ -415,11 +417,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                         for (int k = sub; k < cnt; k += 4)
                         {
                             const int e = s_idx[wave][k];
-                            m2pRec(fq, qx, qy, qz, sA[e], sB[e], sC[e]);
+                            m2pRec(fq[qq], qx, qy, qz, sA[e], sB[e], sC[e]);
                         }
-                    SX_FOLD_QUARTER(qq)
                 }
             }
+            SX_FOLD_ALL()
             SX_FLUSH_FO()
         }
         else
@@ -546,12 +548,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     }
 #pragma unroll
                     for (int c_ = 0; c_ < 4; ++c_)
-                        fq[c_] += f2[c_].x + f2[c_].y;
+                        fq[qq][c_] += f2[c_].x + f2[c_].y;
                 }
-                SX_FOLD_QUARTER(qq)
             }
             buf ^= 1;
         }
+        SX_FOLD_ALL()
         SX_FLUSH_FO()
         nP = 0;
     };
@@ -655,6 +657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     else if (lane == 0 && a.egrav) atomicAdd(a.egrav, 0.5 * u);
 #undef SX_LOAD_QUARTER
 #undef SX_FOLD_QUARTER
+#undef SX_FOLD_ALL
 #undef SX_FLUSH_FO
 }
 
