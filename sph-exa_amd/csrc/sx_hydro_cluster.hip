@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #define SX_CH_IAD 1660 // 53 KB: three IAD workgroups per CU (24 waves at 79 VGPRs; 2 at CH 1900: 10.3 -> 9.4 ms at 64M)
 #endif
 #ifndef SX_CH_AV
-#define SX_CH_AV 2048
+#define SX_CH_AV 1470 // 53 KB: three AV workgroups per CU (2048: two; Sedov 64M AV 10.0 -> 8.6 ms, step -1.2 ms)
 #endif
 constexpr int kChXm = 2048, kChVd = 2000, kChIad = SX_CH_IAD, kChAv = SX_CH_AV, kChMe = SX_CH_ME, kChMeAvc = 1536;
 
