@@ -612,13 +612,20 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
 }
 
 // ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
-template<int CH, int SPLIT>
+template<int CH, int SPLIT, int UMIN = 0, int UMAX = 0>
 __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
 {
     __shared__ float4 sP[CH]; // x, y, z, vol
     __shared__ float4 sV[CH]; // vx, vy, vz, c
     __shared__ float  sD[CH]; // divv
     __shared__ float  s_red[kClusterWaves * SPLIT];
+    if constexpr (UMIN > 0 || UMAX > 0)
+    {
+        // one of the two capacity launches (avSwitches): this workgroup's cluster belongs to the other one
+        const uint32_t blk = xcdBlock(blockIdx.x, gridDim.x);
+        const uint32_t U   = a.ucount[a.clusterList ? a.clusterList[blk] : blk];
+        if (U < (uint32_t)UMIN || (UMAX > 0 && U > (uint32_t)UMAX)) return;
+    }
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
@@ -1201,7 +1208,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #ifndef SX_CH_AV
 #define SX_CH_AV 1470 // 53 KB: three AV workgroups per CU (2048: two; Sedov 64M AV 10.0 -> 8.6 ms, step -1.2 ms)
 #endif
-constexpr int kChXm = 2048, kChVd = 2000, kChIad = SX_CH_IAD, kChAv = SX_CH_AV, kChMe = SX_CH_ME, kChMeAvc = 1536;
+constexpr int kChXm = 2048, kChVd = 2000, kChIad = SX_CH_IAD, kChAv = SX_CH_AV, kChAvLarge = 2048, kChMe = SX_CH_ME,
+              kChMeAvc = 1536;
 
 static inline unsigned clusters(const PairArgs& a)
 {
@@ -1220,9 +1228,14 @@ void iadDivvCurlv(const PairArgs& a, hipStream_t s)
 {
     if (a.numGroups && clusters(a)) iadDivvCurlvFusedKernel<kChIad, SX_SPLIT_IAD><<<clusters(a), kB * SX_SPLIT_IAD, 0, s>>>(a);
 }
+//! AV switches in two launches by union size: clusters whose union fits 1470 records run three workgroups per CU (53
+//! KB), larger ones (the lattice's 122-neighbor steps: ~1485 per cluster) two per CU with 2048 records instead of the
+//! chunked path; each launch's workgroups of the other class exit after one load
 void avSwitches(const PairArgs& a, hipStream_t s)
 {
-    if (a.numGroups && clusters(a)) avSwitchesKernel<kChAv, SX_SPLIT_AV><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
+    if (!a.numGroups || !clusters(a)) return;
+    avSwitchesKernel<kChAv, SX_SPLIT_AV, 0, kChAv><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
+    avSwitchesKernel<kChAvLarge, SX_SPLIT_AV, kChAv + 1, 0><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
 }
 //! min over the per-workgroup Courant time-steps of one launch -> *minDt (one atomic)
 __global__ __launch_bounds__(1024) void reduceBlockDtKernel(const float* v, uint32_t n, float* minDt)
