@@ -353,6 +353,15 @@ int  sx_comm_unique_id(void* id128);
 int  sx_comm_create_rccl(sx_comm** comm, int rank, int size, const void* id128);
 int  sx_comm_create_host(sx_comm** comm, int rank, int size, sx_alltoallv_cb a2a, sx_allreduce_cb ar, void* user);
 void sx_comm_destroy(sx_comm* comm);
+/*! the transport's two operations on device buffers, as the domain sync uses them (sx_comm.hpp): every rank sends
+ *  sendBytes[q] bytes from send + sendOff[q] to rank q and receives recvBytes[q] at recv + recvOff[q] (MPI_Alltoallv
+ *  shape of the reference's Isend/Recv halo and particle exchange, halos/exchange_halos_gpu.cuh:51-143,
+ *  domain/domaindecomp_mpi_gpu.cuh:86-171), enqueued on hipStream; and an in-place allreduce of count elements, op 0 =
+ *  u32 sum (tree counts, update_mpi_gpu.cuh:75), 1 = f64 min (time-step, ts_global.hpp:106), 2 = f64 sum
+ *  (conserved quantities, conserved_quantities.hpp:163-165).  Results are complete when the stream is. */
+int  sx_comm_alltoallv(sx_comm* comm, const void* send, const uint64_t* sendBytes, const uint64_t* sendOff, void* recv,
+                       const uint64_t* recvBytes, const uint64_t* recvOff, void* hipStream);
+int  sx_comm_allreduce(sx_comm* comm, void* dev, uint64_t count, int op, void* hipStream);
 
 /* ---- block time-step host bookkeeping (HydroVeBdtProp::computeRungs, ve_hydro_bdt.hpp:292-331) ---------------- */
 /*! sph::Timestep (sph/timestep.h:38-48) */
@@ -443,6 +452,13 @@ int    sx_sim_kernel_times(sx_sim* sim, float* ms, int cap, const char** names);
  *  every particle active); the others drift the inactive rungs and compute the active ones (partial sync: halo
  *  x,y,z,h refreshed, order, tree and halo lists kept).  SX_ERR_ARG for the other propagators. */
 int    sx_sim_timestep(sx_sim* sim, sx_timestep* ts);
+/*! the simulation time d.ttot (a restart's "time" attribute, particles_data.hpp:170-190; set_state starts at 0) */
+int    sx_sim_set_time(sx_sim* sim, double ttot);
+/*! propagator 2: restart state after sx_sim_set_state (HydroVeBdtProp::load, ve_hydro_bdt.hpp:155-168): the Timestep
+ *  saved with the file and the `rung` of each set_state particle (host array, set_state order; NULL keeps rung 0).
+ *  SX_ERR_ARG unless activeRung(ts->substep, ts->numRungs) == 0: restart files exist only at hierarchy boundaries
+ *  (the reference writes them only when isSynced(), sphexa.cpp:165). */
+int    sx_sim_set_timestep(sx_sim* sim, const sx_timestep* ts, const uint8_t* rung);
 
 #ifdef __cplusplus
 }

@@ -463,3 +463,32 @@ extern "C" int sx_sim_timestep(sx_sim* s, sx_timestep* out)
     *out = s->bdt.ts;
     return SX_OK;
 }
+
+/*! restart of a ve-bdt run (HydroVeBdtProp::load, ve_hydro_bdt.hpp:155-168): after sx_sim_set_state, the Timestep
+ *  the file stored and the conserved field `rung` (ConservedFields, :94) of the set_state particles, in their order.
+ *  Only a Timestep at a hierarchy boundary is accepted -- the reference writes restart files only when isSynced()
+ *  (sphexa.cpp:165, :220) -- so the next substep is a full sync that starts a new hierarchy from this Timestep, as the
+ *  uninterrupted run's next substep does. */
+extern "C" int sx_sim_set_timestep(sx_sim* s, const sx_timestep* ts, const uint8_t* rung)
+{
+    if (!s || !ts || s->p.propagator != 2) return SX_ERR_ARG;
+    if (ts->numRungs < 1 || ts->numRungs > SX_MAX_RUNGS) return SX_ERR_ARG;
+    if (sx::sim::activeRung(ts->substep, ts->numRungs) != 0) return SX_ERR_ARG;
+    const size_t n = s->last - s->first;
+    if (rung && n)
+    {
+        for (size_t i = 0; i < n; ++i)
+            if (rung[i] >= SX_MAX_RUNGS) return SX_ERR_ARG;
+        if (hipMemcpy(s->rung + s->first, rung, n, hipMemcpyHostToDevice) != hipSuccess) return SX_ERR_HIP;
+    }
+    sx::sim::Scalars sc{};
+    if (hipMemcpy(&sc, s->sc, sizeof(sc), hipMemcpyDeviceToHost) != hipSuccess) return SX_ERR_HIP;
+    sx::sim::BdtState& b = s->bdt;
+    b.ts                 = *ts;
+    b.prev               = sx_timestep{};
+    b.minDt              = sc.minDt;
+    b.minDt_m1           = sc.minDt_m1;
+    b.ttot               = sc.ttot;
+    b.started            = true;
+    return SX_OK;
+}

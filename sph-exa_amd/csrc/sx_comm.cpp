@@ -56,15 +56,18 @@ public:
                 hipSuccess)
             return false;
         if (ncclGroupStart() != ncclSuccess) return false;
-        for (int q = 0; q < size_; ++q)
+        // a failed enqueue stops issuing further peers, but the group is always closed: returning between
+        // ncclGroupStart and ncclGroupEnd would leave the thread's group open and poison every later RCCL call
+        bool ok = true;
+        for (int q = 0; q < size_ && ok; ++q)
         {
             if (q == rank_) continue;
-            if (sendBytes[q] && ncclSend(sb + sendOff[q], sendBytes[q], ncclUint8, q, comm_, s) != ncclSuccess)
-                return false;
-            if (recvBytes[q] && ncclRecv(rb + recvOff[q], recvBytes[q], ncclUint8, q, comm_, s) != ncclSuccess)
-                return false;
+            if (sendBytes[q]) ok = ncclSend(sb + sendOff[q], sendBytes[q], ncclUint8, q, comm_, s) == ncclSuccess;
+            if (ok && recvBytes[q])
+                ok = ncclRecv(rb + recvOff[q], recvBytes[q], ncclUint8, q, comm_, s) == ncclSuccess;
         }
-        return ncclGroupEnd() == ncclSuccess;
+        bool closed = ncclGroupEnd() == ncclSuccess;
+        return ok && closed;
     }
     bool allreduceSumU32(uint32_t* dev, size_t count, hipStream_t s) override
     {
@@ -187,6 +190,27 @@ extern "C"
     {
         *out = new sx_comm{new sx::HostTransport(rank, size, a2a, ar, user)};
         return SX_OK;
+    }
+
+    int sx_comm_alltoallv(sx_comm* c, const void* send, const uint64_t* sendBytes, const uint64_t* sendOff,
+                          void* recv, const uint64_t* recvBytes, const uint64_t* recvOff, void* hipStream)
+    {
+        if (!c || !c->t) return SX_ERR_ARG;
+        return c->t->alltoallv(send, sendBytes, sendOff, recv, recvBytes, recvOff, static_cast<hipStream_t>(hipStream)) ? SX_OK : SX_ERR_HIP;
+    }
+
+    int sx_comm_allreduce(sx_comm* c, void* dev, uint64_t count, int op, void* hipStream)
+    {
+        if (!c || !c->t) return SX_ERR_ARG;
+        bool ok;
+        switch (op)
+        {
+            case 0: ok = c->t->allreduceSumU32(static_cast<uint32_t*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
+            case 1: ok = c->t->allreduceMinF64(static_cast<double*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
+            case 2: ok = c->t->allreduceSumF64(static_cast<double*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
+            default: return SX_ERR_ARG;
+        }
+        return ok ? SX_OK : SX_ERR_HIP;
     }
 
     void sx_comm_destroy(sx_comm* c)

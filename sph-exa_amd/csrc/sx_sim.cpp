@@ -355,18 +355,22 @@ __global__ __launch_bounds__(256) void markHalosKernel(const ReqBox* boxes, int 
 
 //! send flags of every peer at once: segment q of (n + 1) entries holds bit q of each particle's mark (0 for q == r
 //! and for the segment's closing entry), so one exclusive scan numbers the send lists of all peers in peer order
-__global__ void maskFlagsKernel(const unsigned long long* mark, size_t n, int P, int r, uint32_t* flag)
+//! send flags of peers [q0, q0 + Pb): one segment of n + 1 flags per peer (the extra 0 makes the scan's last entry
+//! the batch total)
+__global__ void maskFlagsKernel(const unsigned long long* mark, size_t n, int q0, int Pb, int r, uint32_t* flag)
 {
     const size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (k >= (size_t)P * (n + 1)) return;
-    const size_t q = k / (n + 1), i = k - q * (n + 1);
-    flag[k]        = (i < n && (int)q != r) ? (uint32_t)((mark[i] >> q) & 1ull) : 0u;
+    if (k >= (size_t)Pb * (n + 1)) return;
+    const size_t j = k / (n + 1), i = k - j * (n + 1);
+    const int    q = q0 + (int)j;
+    flag[k]        = (i < n && q != r) ? (uint32_t)((mark[i] >> q) & 1ull) : 0u;
 }
 
-__global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, size_t n, int P, uint32_t* out)
+__global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, size_t n, int Pb, uint64_t base,
+                                 uint32_t* out)
 {
     const size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (k < (size_t)P * (n + 1) && flag[k]) out[scan[k]] = (uint32_t)(k % (n + 1));
+    if (k < (size_t)Pb * (n + 1) && flag[k]) out[base + scan[k]] = (uint32_t)(k % (n + 1));
 }
 
 //! start of every peer's send list in the scan (P entries) and the total (entry P)
@@ -801,6 +805,8 @@ int exchangeThen(sx_sim* s, const HydroLaunch& H, std::initializer_list<std::pai
 
 /*! distributed sync: SFC assignment, particle exchange, halo discovery + setup exchange, combined tree.
  *  On entry the local particles are [first,last); on exit [first,last) again with halos around them. */
+int anyRank(sx_sim* s, bool bad, hipStream_t st, bool& out);
+
 int distributedSync(sx_sim* s, hipStream_t st, double margin)
 {
     sx::Transport* T  = s->comm;
@@ -884,7 +890,11 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     }
 
     // --- 4. halo discovery: request boxes, exchange, mark, send lists
-    if (nl != nlOf[r]) return SX_ERR_ARG; // the exchange must deliver exactly this rank's bins
+    {   // the exchange must deliver exactly this rank's bins; the peers size their box receives from nlOf
+        bool bad = false;
+        if (int e = anyRank(s, nl != nlOf[r], st, bad)) return e;
+        if (bad) return SX_ERR_ARG;
+    }
     const size_t nChunks = (nl + kChunk - 1) / kChunk;
     ReqBox*      myBoxes = s->work.get<ReqBox>("dom.mybox", nChunks);
     if (nChunks) chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
@@ -917,39 +927,74 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         markHalosKernel<<<grid(nRemote, 4), 256, 0, st>>>(
             remote, (int)nRemote, s->localTree.childOffsets, s->localTree.internalToLeaf, s->localTree.layout,
             s->localTree.centers, s->localTree.sizes, s->x, s->y, s->z, s->dbox, qm, mark, err);
-    // send lists of all peers from one flag array and one scan (peer order), one host read of the P + 1 offsets
-    const size_t nf   = (size_t)P * (nl + 1);
-    uint32_t*    flag = s->work.get<uint32_t>("dom.flag", nf);
-    uint32_t*    scan = s->work.get<uint32_t>("dom.scan", nf);
-    uint32_t*    segs = s->work.get<uint32_t>("dom.segs", P + 1);
-    uint32_t*    hseg = s->work.pinned<uint32_t>("dom.hseg", P + 1);
+    // send lists of the peers from one flag array and one scan per batch of peers (peer order), one host read of the
+    // batch's offsets; a batch holds as many peers as keep its flags within kFlagCap entries (and the scan's int
+    // count), so the scratch does not grow with the rank count
+    constexpr size_t kFlagCap = size_t(1) << 27;
+    const int        Pb       = (int)std::max<size_t>(1, std::min<size_t>(P, kFlagCap / (nl + 1)));
+    const size_t     nf       = (size_t)Pb * (nl + 1);
+    if (nf > (size_t)INT32_MAX) return SX_ERR_NOMEM; // one peer's segment alone beyond the scan's range
+    uint32_t* flag = s->work.get<uint32_t>("dom.flag", nf);
+    uint32_t* scan = s->work.get<uint32_t>("dom.scan", nf);
+    uint32_t* segs = s->work.get<uint32_t>("dom.segs", Pb + 1);
+    uint32_t* hseg = s->work.pinned<uint32_t>("dom.hseg", Pb + 1);
+    if (!flag || !scan || !segs || !hseg) return SX_ERR_NOMEM;
     s->haloSend.assign(P, 0);
     s->haloSendOff.assign(P, 0);
-    const size_t sendCap = std::max<size_t>(1, nl) * std::min(P - 1, 8);
-    s->sendIdx           = s->work.get<uint32_t>("dom.sendIdx", sendCap);
-    if (!flag || !scan || !s->sendIdx) return SX_ERR_NOMEM;
     size_t tmpB = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nf, st);
     void* tmp = s->work.get<char>("dom.scantmp", tmpB);
-    maskFlagsKernel<<<grid(nf), 256, 0, st>>>(mark, nl, P, r, flag);
-    SIM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nf, st));
-    segStartsKernel<<<1, 128, 0, st>>>(scan, nl, P, segs);
-    SIM_HIP(hipMemcpyAsync(hseg, segs, 4 * (P + 1), hipMemcpyDeviceToHost, st));
-    SIM_HIP(hipStreamSynchronize(st));
-    if (hseg[P] > sendCap) return SX_ERR_NOMEM; // more than 8 full copies of the locals: give up loudly
-    scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, s->sendIdx);
-    for (int q = 0; q < P; ++q)
+    if (!tmp) return SX_ERR_NOMEM;
+    // flags + scan of one batch; with scatter, the batch's send indices go to sendIdx[base, ...)
+    auto batch = [&](int q0, int nb, bool scatter, uint64_t base) -> int
     {
-        s->haloSendOff[q] = hseg[q];
-        s->haloSend[q]    = (q < P - 1 ? hseg[q + 1] : hseg[P]) - hseg[q];
+        const size_t nfb = (size_t)nb * (nl + 1);
+        maskFlagsKernel<<<grid(nfb), 256, 0, st>>>(mark, nl, q0, nb, r, flag);
+        SIM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nfb, st));
+        if (scatter) scatterIdxKernel<<<grid(nfb), 256, 0, st>>>(flag, scan, nl, nb, base, s->sendIdx);
+        segStartsKernel<<<1, 128, 0, st>>>(scan, nl, nb, segs);
+        SIM_HIP(hipMemcpyAsync(hseg, segs, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        for (int j = 0; j < nb; ++j)
+        {
+            s->haloSendOff[q0 + j] = base + hseg[j];
+            s->haloSend[q0 + j]    = (j < nb - 1 ? hseg[j + 1] : hseg[nb]) - hseg[j];
+        }
+        return SX_OK;
+    };
+    // the send list is sized by what the peers request (a local may go to several peers): with one batch the scan
+    // is read before the scatter; with several, a counting pass first (the arena's growth does not keep contents)
+    uint64_t total = 0;
+    for (int q0 = 0; q0 < P; q0 += Pb)
+    {
+        const int nb = std::min(Pb, P - q0);
+        if (int e = batch(q0, nb, false, total)) return e;
+        total += hseg[nb];
     }
-    s->numSend = hseg[P];
+    s->sendIdx = s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
+    if (!s->sendIdx) return SX_ERR_NOMEM;
+    if (Pb >= P) scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, 0, s->sendIdx);
+    else
+    {
+        uint64_t base = 0;
+        for (int q0 = 0; q0 < P; q0 += Pb)
+        {
+            const int nb = std::min(Pb, P - q0);
+            if (int e = batch(q0, nb, true, base)) return e;
+            base += hseg[nb];
+        }
+    }
+    s->numSend = total;
     SIM_COMM(T->exchangeCounts(s->haloSend, s->haloRecv, st, s->cntBuf));
     s->haloRecv[r] = 0;
     uint64_t nLow = 0, nHigh = 0;
     for (int q = 0; q < P; ++q)
         (q < r ? nLow : nHigh) += s->haloRecv[q];
-    if (nLow + nl + nHigh > s->cap) return SX_ERR_NOMEM;
+    {
+        bool full = false;
+        if (int e = anyRank(s, nLow + nl + nHigh > s->cap, st, full)) return e;
+        if (full) return SX_ERR_NOMEM;
+    }
     s->haloRecvOff.assign(P, 0);
     {
         uint64_t lay[3];
@@ -1230,6 +1275,22 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     return SX_OK;
 }
 
+/*! a decision every rank must take together: true on all ranks if `bad` holds on any (one allreduce).  A rank that
+ *  returned alone from the middle of distributedSync would leave its peers waiting in the next collective. */
+int anyRank(sx_sim* s, bool bad, hipStream_t st, bool& out)
+{
+    auto*     flg  = s->work.get<uint32_t>("dom.agree", 1);
+    uint32_t* hflg = s->work.pinned<uint32_t>("dom.agreeh", 1);
+    if (!flg || !hflg) return SX_ERR_NOMEM;
+    *hflg = bad ? 1u : 0u;
+    SIM_HIP(hipMemcpyAsync(flg, hflg, 4, hipMemcpyHostToDevice, st));
+    SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
+    SIM_HIP(hipMemcpyAsync(hflg, flg, 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    out = *hflg != 0;
+    return SX_OK;
+}
+
 int halosOutgrown(sx_sim* s, hipStream_t st, unsigned& hf)
 {
     const size_t nl  = s->last - s->first;
@@ -1393,6 +1454,11 @@ extern "C"
                          const float* alpha, const uint64_t* id, double minDt, double minDt_m1)
     {
         if (n > s->cap) return SX_ERR_ARG;
+        if (s->p.propagator == 2)
+        {   // ve-bdt carries the rung in the id's top byte through the particle exchange (PRec): ids must fit 56 bits
+            for (size_t i = 0; i < n; ++i)
+                if (id[i] >> 56) return SX_ERR_ARG;
+        }
         s->n     = n;
         s->first = 0;
         s->last  = n;
@@ -1843,6 +1909,19 @@ extern "C"
                 return SX_ERR_TRAVERSAL;
             }
         }
+        return SX_OK;
+    }
+
+    int sx_sim_set_time(sx_sim* s, double ttot)
+    {
+        if (!s) return SX_ERR_ARG;
+        hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        SIM_HIP(hipMemcpyAsync(s->scHost, s->sc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        s->scHost->ttot = ttot;
+        SIM_HIP(hipMemcpyAsync(s->sc, s->scHost, sizeof(Scalars), hipMemcpyHostToDevice, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        s->bdt.ttot = ttot; // ve-bdt keeps d.ttot on the host between substeps
         return SX_OK;
     }
 

@@ -197,10 +197,14 @@ def lib():
         "sx_sim_set_overlap": (C.c_int, [vp, C.c_int]),
         "sx_sim_overlap_stats": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
         "sx_sim_timestep": (C.c_int, [vp, C.POINTER(SxTimestep)]),
+        "sx_sim_set_timestep": (C.c_int, [vp, C.POINTER(SxTimestep), vp]),
+        "sx_sim_set_time": (C.c_int, [vp, C.c_double]),
         "sx_comm_unique_id": (C.c_int, [vp]),
         "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
         "sx_comm_destroy": (None, [vp]),
+        "sx_comm_alltoallv": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "sx_comm_allreduce": (C.c_int, [vp, vp, C.c_uint64, C.c_int, vp]),
         "sx_domain_splitters": (C.c_int, [vp, u32, C.c_int, vp]),
         "sx_gravity_upsweep": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.c_float, vp, vp]),
         "sx_gravity_traverse": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxTree),
@@ -447,6 +451,24 @@ class Comm:
         if rc != SX_OK:
             raise SxError(f"communicator creation failed ({backend}): {rc}")
 
+    def alltoallv(self, send, send_bytes, send_off, recv, recv_bytes, recv_off, stream=None):
+        """sx_comm_alltoallv on device pointers (byte counts / offsets per rank); enqueued on `stream`"""
+        arr = [np.ascontiguousarray(a, dtype=np.uint64) for a in (send_bytes, send_off, recv_bytes, recv_off)]
+        if any(a.size != self.size for a in arr):
+            raise ValueError("alltoallv: one count and one offset per rank")
+        rc = self.L.sx_comm_alltoallv(self.h, send, arr[0].ctypes.data, arr[1].ctypes.data, recv, arr[2].ctypes.data,
+                                      arr[3].ctypes.data, stream)
+        if rc != SX_OK:
+            raise SxError(f"sx_comm_alltoallv failed: {rc}")
+
+    ALLREDUCE_OPS = {"sum_u32": 0, "min_f64": 1, "sum_f64": 2}
+
+    def allreduce(self, dev, count, op, stream=None):
+        """sx_comm_allreduce in place on a device buffer: op 'sum_u32', 'min_f64' or 'sum_f64'"""
+        rc = self.L.sx_comm_allreduce(self.h, dev, int(count), self.ALLREDUCE_OPS[op], stream)
+        if rc != SX_OK:
+            raise SxError(f"sx_comm_allreduce failed: {rc}")
+
     def close(self):
         if self.h:
             self.L.sx_comm_destroy(self.h)
@@ -503,8 +525,17 @@ class Sim:
         (ParticlesData::fieldNames, particles_data.hpp:247-251; the set HydroVeProp restarts from,
         ve_hydro.hpp:74 + x,y,z,h,m) and the step attributes under the reference's names
         (reference_attributes: ParticlesData::loadOrStoreAttributes, particles_data.hpp:142-193, and
-        Box::loadOrStore, box.hpp:168-175), as an .npz (HDF5/H5Part is not in this image)"""
-        st = self.get(self.CONSERVED)
+        Box::loadOrStore, box.hpp:168-175).  A path ending in ".h5" appends a step to an H5Part-layout file (the
+        reference's format, sphexa_amd.h5part over the image's serial HDF5); any other path writes an .npz."""
+        bdt = self.params.propagator == 2
+        if bdt:
+            ts = self.timestep()
+            if not self._hierarchy_boundary(ts):
+                # the reference writes files only when isSynced() (sphexa.cpp:165): inside a block time-step hierarchy
+                # the state is not restartable (drifted inactive rungs, halo lists of the hierarchy's sync)
+                raise ValueError(f"ve-bdt checkpoint inside a time-step hierarchy (substep {ts['substep']} of "
+                                 f"{1 << (ts['numRungs'] - 1)}): save after the hierarchy's last substep")
+        st = self.get(self.CONSERVED + (["rung"] if bdt else []))
         if num_particles_global is None:
             num_particles_global = self.size()
             comm = getattr(self, "comm", None)
@@ -516,28 +547,71 @@ class Sim:
                 dist.all_reduce(t, op=dist.ReduceOp.SUM)
                 num_particles_global = int(t.item())
         attrs = reference_attributes(self.params, self.box, self.scalars(), self.iteration, num_particles_global)
-        np.savez(path, **st, **attrs)
+        if bdt:  # Timestep::loadOrStore(writer, "ts::") (sph/timestep.h:29-33, HydroVeBdtProp::save)
+            attrs["ts::numRungs"] = np.int32(ts["numRungs"])
+            attrs["ts::dt_m1"] = np.array(ts["dt_m1"], dtype=np.float32)
+        if str(path).endswith(".h5"):
+            from . import h5part
+
+            h5part.write_step(path, st, attrs, mode="a")
+        else:
+            np.savez(path, **st, **attrs)
+
+    @staticmethod
+    def _hierarchy_boundary(ts):
+        """HydroVeBdtProp::isSynced (ve_hydro_bdt.hpp:108-112, :220) for the NEXT substep"""
+        return ts["substep"] == 0 or ts["substep"] >= (1 << (ts["numRungs"] - 1))
 
     # attributes ParticlesData::loadOrStoreAttributes restores (particles_data.hpp:170-190) that are parameters of
     # this Sim (fixed at sx_sim_create): a restart must run with the stored values
     PARAM_ATTRIBUTES = ["ng0", "ngmax", "Kcour", "Krho", "gravConstant", "gamma", "eps", "etaAcc", "muiConst",
                         "alphamin", "alphamax", "decay_constant"]
 
-    def load_checkpoint(self, path):
-        """continue from save_checkpoint's file: set_state with the saved fields and time-steps; returns the time.
+    def _read_checkpoint(self, path, step):
+        """{name: array or scalar} of a restart file: the conserved fields (+ rung), and the attributes present"""
+        mine = reference_attributes(self.params, self.box, {"ttot": 0.0, "minDt": 0.0, "minDt_m1": 0.0}, 0, 0)
+        if str(path).endswith(".h5"):
+            from . import h5part
+
+            names = self.CONSERVED + (["rung"] if self.params.propagator == 2 else [])
+            with h5part.H5PartFile(path, "r") as f:
+                f.set_step(step)
+                present = set(f.attrib_names())
+                fields = {k: f.read_field(k, DTYPES.get(k, np.uint64)) for k in names if f.field_info(k) is not None}
+            types = {k: np.asarray(v).dtype for k, v in mine.items()}
+            types.update({"ts::numRungs": np.int32, "ts::dt_m1": np.float32, "ttot": np.float64})
+            _, attrs = h5part.read_step(path, {}, {k: t for k, t in types.items() if k in present}, step)
+            return {**fields, **attrs}
+        with np.load(path, allow_pickle=False) as d:
+            return {k: d[k] for k in d.files}
+
+    def load_checkpoint(self, path, step=-1):
+        """continue from save_checkpoint's file (.h5: its step `step`, negative = the last, as the reference's
+        --init file.h5:step; .npz: the one state): set_state with the saved fields and time-steps; returns the time.
         The stored parameters must equal this Sim's (ValueError otherwise: the reference would load them, a Sim's
         parameters are fixed at creation).  Files of the earlier format (time under 'ttot', no 'iteration') load
         with iteration 0."""
-        with np.load(path, allow_pickle=False) as d:
-            mine = reference_attributes(self.params, self.box, {"ttot": 0.0, "minDt": 0.0, "minDt_m1": 0.0}, 0, 0)
-            bad = [k for k in self.PARAM_ATTRIBUTES if k in d.files and d[k] != mine[k]]
-            if bad:
-                raise ValueError("restart file parameters differ from this Sim's: " +
-                                 ", ".join(f"{k}={d[k]!r} (Sim: {mine[k]!r})" for k in bad))
-            st = {k: d[k] for k in self.CONSERVED}
-            self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
-            self.iteration = int(d["iteration"]) if "iteration" in d.files else 0
-            return float(d["time"] if "time" in d.files else d["ttot"])
+        d = self._read_checkpoint(path, step)
+        mine = reference_attributes(self.params, self.box, {"ttot": 0.0, "minDt": 0.0, "minDt_m1": 0.0}, 0, 0)
+        bad = [k for k in self.PARAM_ATTRIBUTES if k in d and d[k] != mine[k]]
+        if bad:
+            raise ValueError("restart file parameters differ from this Sim's: " +
+                             ", ".join(f"{k}={d[k]!r} (Sim: {mine[k]!r})" for k in bad))
+        st = {k: d[k] for k in self.CONSERVED}
+        self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
+        if self.params.propagator == 2 and "ts::numRungs" in d:
+            # HydroVeBdtProp::load (ve_hydro_bdt.hpp:155-168): Timestep numRungs + dt_m1, substep 0, and the rungs
+            ts = SxTimestep()
+            ts.numRungs = int(d["ts::numRungs"])
+            for k, v in enumerate(np.asarray(d["ts::dt_m1"], np.float32)):
+                ts.dt_m1[k] = float(v)
+            rung = np.ascontiguousarray(d["rung"], dtype=np.uint8)
+            self._keep_rung = rung
+            self.ctx.check(self.L.sx_sim_set_timestep(self.h, C.byref(ts), rung.ctypes.data), "set_timestep")
+        self.iteration = int(d["iteration"]) if "iteration" in d else 0
+        t = float(d["time"] if "time" in d else d["ttot"])
+        self.ctx.check(self.L.sx_sim_set_time(self.h, t), "set_time")
+        return t
 
     def step(self):
         rc = self.L.sx_sim_step(self.h)

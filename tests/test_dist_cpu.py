@@ -2,7 +2,7 @@
 
 * the host-side decisions of the decomposition that the GPU path calls (sx_domain_splitters,
   sx_domain_halo_layout in libsphexa_hip.so) against a numpy restatement;
-* the decomposed VE step (oracle/dist_oracle.py: SFC assignment from the all-reduced key histogram through
+* the decomposed VE step with 2, 3 and 8 ranks (8 = one node's GPUs, seven peers per rank; oracle/dist_oracle.py: SFC assignment from the all-reduced key histogram through
   sx_domain_splitters, particle exchange, halo discovery, the five halo exchanges, global dt) against the
   single-domain oracle: after step 1 nc and h exact, floats within the full-step tolerance of
   tests/test_gpu_parity.py (neighbor sums run in another order), identical dt on every rank.
@@ -85,7 +85,8 @@ def merged(ranks, s):
     return {k: v[o] for k, v in out.items()}
 
 
-@pytest.mark.parametrize("nproc,ic,side", [(2, "sedov", 16), (3, "sedov", 14), (2, "noh", 18)])
+@pytest.mark.parametrize("nproc,ic,side", [(2, "sedov", 16), (3, "sedov", 14), (2, "noh", 18), (8, "sedov", 24),
+                                           (8, "noh", 26)])
 def test_decomposed_steps_match_single_domain(tmp_path, nproc, ic, side):
     steps = 2
     ranks = run_ranks(tmp_path, nproc, side, steps, ic)

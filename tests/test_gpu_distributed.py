@@ -4,7 +4,8 @@ The SFC decomposition, particle exchange, halo discovery and the five halo excha
 the physics: after step 1 (identical inputs) every particle's nc and h equal the oracle's and the float fields
 agree within the full-step tolerance of test_gpu_parity.py; the global time-step is identical on all ranks.
 (On the Sedov lattice the h-nc iteration does not trigger, so the reference's stale-halo-h convention does not
-come into play.)  RCCL itself needs one GPU per rank; it is exercised by bench.py --gpus N on a full node.
+come into play.)  RCCL with several ranks needs one GPU per rank (bench.py --gpus N on a full node); the RCCL
+transport's own calls run here on a one-rank communicator (test_rccl_one_rank_transport).
 """
 import os
 import subprocess
@@ -39,9 +40,10 @@ def merged(ranks, s):
     return {k: v[o] for k, v in out.items()}
 
 
-@pytest.mark.parametrize("nproc,port", [(2, 29641), (3, 29642)])
-def test_distributed_steps_match_oracle(tmp_path, nproc, port):
-    side, steps = 16, 2
+@pytest.mark.parametrize("nproc,port,side", [(2, 29641, 16), (3, 29642, 16), (8, 29644, 24)])
+def test_distributed_steps_match_oracle(tmp_path, nproc, port, side):
+    """8 ranks = one node's GPUs (seven peers per rank), all on the one GPU of the test box"""
+    steps = 2
     ranks = run_ranks(tmp_path, nproc, side, steps, port)
     st, obox = po.sedov_state(side)
     ora = po.load_oracle()
@@ -207,3 +209,14 @@ def test_overlapped_exchanges_bitwise_equal_serial(tmp_path, opts, port):
             inner, bound = ovl[q][f"s{s}_overlap"]
             assert inner + bound == ncl and inner > 0 and bound > 0, (q, s, inner, bound, ncl)
             assert tuple(ser[q][f"s{s}_overlap"]) == (0, 0)
+
+
+def test_rccl_one_rank_transport():
+    """the RCCL transport (sx_comm.cpp RcclTransport) executes on the device: a one-rank communicator from a real
+    ncclGetUniqueId / ncclCommInitRank, the self segment of alltoallv (device copy + an empty ncclGroupStart/End),
+    and ncclAllReduce sum-u32 / min-f64 / sum-f64 in place on device buffers, each checked against the host values"""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29671", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py")], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "RCCL one-rank OK" in r.stdout, r.stdout[-2000:]

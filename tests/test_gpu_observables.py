@@ -67,16 +67,18 @@ def test_sim_conserved_energy(ctx):
     sim.close()
 
 
-def test_checkpoint_restart_bitwise(ctx, tmp_path):
+@pytest.mark.parametrize("suffix", ["npz", "h5"])
+def test_checkpoint_restart_bitwise(ctx, tmp_path, suffix):
     """save after 2 Sedov steps, continue 2 steps; a new simulation restarted from the file reproduces those 2
-    steps bit for bit (the step is deterministic: atomics only take minima / ORs)"""
+    steps bit for bit (the step is deterministic: atomics only take minima / ORs); .h5 = the reference's H5Part
+    layout (sphexa_amd.h5part, pinned to the reference's reader/writer in tests/test_h5part.py)"""
     st, obox = po.sedov_state(20)
     box = gutil.box_to_sx(obox)
     a = sx.Sim(ctx, st.n, box)
     a.set_state(st.arrays, st.minDt, st.minDt_m1)
     a.step()
     a.step()
-    ck = str(tmp_path / "restart.npz")
+    ck = str(tmp_path / f"restart.{suffix}")
     a.save_checkpoint(ck)
     a.step()
     a.step()
@@ -90,10 +92,58 @@ def test_checkpoint_restart_bitwise(ctx, tmp_path):
     oa, ob = np.argsort(ga["id"]), np.argsort(gb["id"])
     for k in names:
         assert np.array_equal(ga[k][oa], gb[k][ob]), k
-    assert a.scalars()["minDt"] == b.scalars()["minDt"]
-    with np.load(ck, allow_pickle=False) as d:  # the reference's restart attributes (particles_data.hpp:170-190)
-        assert all(n in d for n in sx.ATTRIBUTE_NAMES)
-        assert int(d["iteration"]) == 2 and int(d["numParticlesGlobal"]) == st.n
+    assert a.scalars() == b.scalars()  # incl. ttot: the restart continues the file's time
+    d = b._read_checkpoint(ck, -1)  # the reference's restart attributes (particles_data.hpp:170-190)
+    assert all(n in d for n in sx.ATTRIBUTE_NAMES)
+    assert int(d["iteration"]) == 2 and int(d["numParticlesGlobal"]) == st.n
     assert b.iteration == 4
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("suffix", ["npz", "h5"])
+def test_ve_bdt_checkpoint_restart_bitwise(ctx, tmp_path, suffix):
+    """ve-bdt (propagator 2) restart: the file holds the rung of every particle (ConservedFields,
+    ve_hydro_bdt.hpp:94) and the Timestep's numRungs and dt_m1 under "ts::" (HydroVeBdtProp::save/load, :153-168);
+    restarting from a hierarchy boundary reproduces the uninterrupted run's next hierarchy bit for bit, and a save
+    inside a hierarchy is refused (the reference writes files only when isSynced(), sphexa.cpp:165)"""
+    st, obox = po.sedov_state(20)
+    box = gutil.box_to_sx(obox)
+    params = sx.default_params(bdt=True)
+    a = sx.Sim(ctx, st.n, box, params=params)
+    a.set_state(st.arrays, st.minDt, st.minDt_m1)
+    ck = str(tmp_path / f"restart_bdt.{suffix}")
+    seen_multi, saved, refused = False, False, False
+    for _ in range(60):
+        a.step()
+        ts = a.timestep()
+        seen_multi |= ts["numRungs"] > 1
+        if not sx.Sim._hierarchy_boundary(ts):
+            if not refused:
+                with pytest.raises(ValueError):
+                    a.save_checkpoint(str(tmp_path / f"mid.{suffix}"))
+                refused = True
+        elif seen_multi:
+            a.save_checkpoint(ck)
+            saved = True
+            break
+    assert saved and refused, "no multi-rung hierarchy formed"
+    d = a._read_checkpoint(ck, -1)
+    num_rungs = int(d["ts::numRungs"])
+    assert num_rungs > 1 and np.asarray(d["ts::dt_m1"]).dtype == np.float32 and d["rung"].max() > 0
+    substeps = 2 * (1 << num_rungs) + 1  # past the end of the next hierarchy, into the one after
+    for _ in range(substeps):
+        a.step()
+    names = ["id", "x", "y", "z", "vx", "vy", "vz", "temp", "h", "alpha", "du_m1", "rung"]
+    ga = a.get(names)
+    b = sx.Sim(ctx, st.n, box, params=params)
+    b.load_checkpoint(ck)
+    for _ in range(substeps):
+        b.step()
+    gb = b.get(names)
+    oa, ob = np.argsort(ga["id"]), np.argsort(gb["id"])
+    for k in names:
+        assert np.array_equal(ga[k][oa], gb[k][ob]), k
+    assert a.scalars() == b.scalars() and a.timestep() == b.timestep()
     a.close()
     b.close()
