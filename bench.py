@@ -32,6 +32,15 @@ CLOCK_HZ = 2.4e9
 # (measured: VeDefGradh issues faster than one op per 4 cycles per SIMD)
 VALU_ISSUE_PEAK = NUM_CU * 4 * CLOCK_HZ / 2
 MOM_FLOP_PER_PAIR = 150  # SURVEY.md 8(d) secondary VALU figure
+# SURVEY.md 8(d) flop per neighbor pair of each pair kernel (the reference's J-loops: XMass 17, VeDefGradh 29,
+# IAD+divv/curlv 95, AV switches 57, momentum 150); valu_frac = pairs x flop / time / FP32 peak (157.3 TF = 2.4 GHz x
+# 256 CUs x 128 lanes x 2 flop per FMA x 2 packed lanes -- the clock is the peak's 2.4 GHz, the kernels run at
+# 1.83-2.34 GHz, profiles/r3b_pmc_clock_waits_sedov_n400.txt)
+FLOP_PER_PAIR = {"xmass": 17, "veDefGradh": 29, "iadDivvCurlv": 95, "avSwitches": 57, "momentumEnergy": 150}
+# self-gravity flop per interaction: the reference's own accounting (nbody/traversal.cuh:632: 20 per P2P, 2 P^3 = 16
+# per quadrupole M2P) and this kernel's (sx_gravity.hip: P2P 23 flop -- as ryoanji/test/demo_mpi.cpp:118 --, M2P 54)
+GRAV_FLOP_REF = (20, 16)
+GRAV_FLOP_IMPL = (23, 54)
 # SURVEY.md 8(d) edge model per kernel: own record R+W, and index + neighbor record per edge.  Reads of neighbor
 # records come from LDS/L2, so edge-model bytes / time is an EFFECTIVE bandwidth, reported as effective_gbs only.
 EDGE_MODEL = {"findNeighbors": (32, 28), "xmass": (44, 32), "veDefGradh": (48, 36), "iadDivvCurlv": (80, 48),
@@ -142,6 +151,28 @@ def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
         r["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / NUM_CU / (ms * 1e-3 * CLOCK_HZ)
     if c and "profiled_ms" in c:
         r["pmc_profiled_ms"] = c["profiled_ms"]
+    if slot in FLOP_PER_PAIR:
+        r["tflops"] = n_local * ng * FLOP_PER_PAIR[slot] / (ms * 1e-3) / 1e12
+        r["valu_frac"] = r["tflops"] / FP32_PEAK_TFLOPS
+    return r
+
+
+def gravity_roofline(ms, n_local, inter, pmc):
+    """self-gravity traversal: FLOP roofline (FP32 VALU) from the per-target interaction counts of the same step
+    (sx_sim_gravity_interactions, the reference's BhStats) -- the kernel is compute/latency bound, its HBM traffic is
+    a few % of the peak"""
+    p2p, m2p = inter["p2p"], inter["m2p"]
+    flop_impl = GRAV_FLOP_IMPL[0] * p2p + GRAV_FLOP_IMPL[1] * m2p
+    flop_ref = GRAV_FLOP_REF[0] * p2p + GRAV_FLOP_REF[1] * m2p
+    r = {"avg_launch_ms": ms, "p2p_per_target": p2p / max(1, n_local), "m2p_per_target": m2p / max(1, n_local),
+         "tflops": flop_impl / (ms * 1e-3) / 1e12, "tflops_reference_model": flop_ref / (ms * 1e-3) / 1e12}
+    r["flop_frac"] = r["tflops"] / FP32_PEAK_TFLOPS
+    c = pmc_slot(pmc, "gravity")
+    if c and "SQ_INSTS_VALU" in c:
+        r["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (ms * 1e-3 * VALU_ISSUE_PEAK)
+    if c and "hbm_read_bytes_est" in c and "hbm_write_bytes_est" in c:
+        r["traffic"] = c["hbm_read_bytes_est"] + c["hbm_write_bytes_est"]
+        r["hbm_frac"] = r["traffic"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     return r
 
 
@@ -313,26 +344,37 @@ def main():
     pmc = load_pmc(pmc_key, n_local, workload) if not std_prop else None
     per_kernel = {}
     for k, ms in kern_ms.items():
-        if ms > 0.01 and (k in EDGE_MODEL or k == "gravity"):
+        if ms > 0.01 and k in EDGE_MODEL:
             per_kernel[k] = kernel_roofline(k, ms, n_local, ng, union_pp, pmc)
+        elif ms > 0.01 and k == "gravity":
+            per_kernel[k] = gravity_roofline(ms, n_local, sim.gravity_interactions(), pmc)
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["avg_launch_ms"]) if per_kernel else "momentumEnergy"
     dom = per_kernel.get(dominant, {})
-    roofline = {"bound": "hbm", "kernel": dominant, "achieved": dom.get("achieved"), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": dom.get("frac"), "traffic": dom.get("traffic"),
+    grav_dom = dominant == "gravity"
+    roofline = {"bound": "valu" if grav_dom else "hbm", "kernel": dominant,
+                "achieved": dom.get("tflops") if grav_dom else dom.get("achieved"),
+                "peak": FP32_PEAK_TFLOPS if grav_dom else HBM_PEAK_GBS,
+                "unit": "TFLOP/s" if grav_dom else "GB/s",
+                "frac": dom.get("flop_frac") if grav_dom else dom.get("frac"), "traffic": dom.get("traffic"),
                 "avg_launch_ms": dom.get("avg_launch_ms"),
                 "share_of_step": dom.get("avg_launch_ms", 0.0) / ms_step,
-                "binding": ("valu-issue/latency (HBM frac < 0.5; see valu_issue_frac, lds_conflict_frac)"
+                "binding": ("FP32 VALU / latency: flop roofline from the per-target P2P/M2P counts (see "
+                            "tflops_reference_model, valu_issue_frac, hbm_frac)" if grav_dom else
+                            "valu-issue/latency (HBM frac < 0.5; see valu_issue_frac, lds_conflict_frac)"
                             if (dom.get("frac") or 0) < 0.5 else "hbm"),
                 "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) if pmc else None,
                 "definition": "achieved = rocprofv3 PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, same "
                               "workload; the x2 is measured for coalesced 4/8/16-B, leaf-run and random 16-B/4-B "
                               "gathers alike, profiles/r3_fetch_calib.json) / avg launch time measured live with HIP "
                               "events; frac = achieved / 8 TB/s; "
-                              "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); lds_conflict_frac = "
+                              "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); valu_frac = SURVEY 8(d) flop "
+                              "per pair x pairs / time / 157.3 TF (FP32 peak at 2.4 GHz); gravity: flop_frac = "
+                              "(23 P2P + 54 M2P) / time / 157.3 TF; lds_conflict_frac = "
                               "SQ_LDS_BANK_CONFLICT / 256 CUs / (time x 2.4 GHz); effective_gbs = SURVEY 8(d) edge "
                               "model (neighbor records served from LDS/L2, not a roofline)",
                 **{k: dom[k] for k in ("valu_issue_frac", "lds_conflict_frac", "effective_gbs",
-                                       "algorithmic_bytes_per_launch", "algorithmic_frac") if k in dom},
+                                       "algorithmic_bytes_per_launch", "algorithmic_frac", "hbm_frac",
+                                       "tflops_reference_model", "p2p_per_target", "m2p_per_target") if k in dom},
                 "per_kernel": per_kernel}
     st_bytes = step_traffic(pmc)
     if st_bytes:

@@ -260,10 +260,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         uint32_t        first, last;
         float           G;
         const uint8_t*  active;
+        unsigned long long* inter;
     } const a{args.x, args.y, args.z, args.centers4, args.m, args.h, args.multipoles, args.childOffsets,
               args.internalToLeaf, args.layout, args.ax, args.ay, args.az, args.egrav, args.waveE, args.err, args.first,
               args.last,
-              args.G, args.active};
+              args.G, args.active, args.interactions};
     __shared__ int  s_stack[4][kGStack];
     __shared__ int  s_m2p[4][kGList];
     __shared__ int  s_p2p[4][kGList];
@@ -317,6 +318,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     const uint64_t bv     = __ballot(valid); // quarters with at least one valid target (lanes fill in order)
     const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
                             (((bv >> 32) & 0xffffull) ? 4u : 0u) | (((bv >> 48) & 0xffffull) ? 8u : 0u);
+    // interaction statistics as the reference counts them (per target: sources evaluated by P2P, nodes by M2P), only
+    // for the valid targets of a quarter (the lanes the evaluation pads with do not count); wave-uniform scalars
+    const unsigned qn[4] = {(unsigned)__popcll(bv & 0xffffull), (unsigned)__popcll((bv >> 16) & 0xffffull),
+                            (unsigned)__popcll((bv >> 32) & 0xffffull), (unsigned)__popcll(bv >> 48)};
+    auto targetsOf = [&](unsigned mask) -> unsigned {
+        return ((mask & 1u) ? qn[0] : 0u) + ((mask & 2u) ? qn[1] : 0u) + ((mask & 4u) ? qn[2] : 0u) +
+               ((mask & 8u) ? qn[3] : 0u);
+    };
+    unsigned long long numP2P = 0, numM2P = 0;
 
     // evaluateMac: true = the target box is inside the node's acceptance radius (descend / P2P).  Massless nodes
     // (mac^2 = 0, setMac) never violate and are dropped by the caller: their M2P adds exactly zero, and skipping it
@@ -408,6 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const uint64_t W    = __ballot(mine);
                     const int      cnt  = __popcll(W);
                     if (cnt == 0) continue;
+                    numM2P += (unsigned long long)cnt * qn[qq];
                     SX_LOAD_QUARTER(qq)
                     __builtin_amdgcn_wave_barrier(); // the previous quarter's reads of s_idx are done
                     if (mine) s_idx[wave][__popcll(W & ltMask)] = (uint8_t)lane;
@@ -429,6 +440,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             {
                 const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
                 const int node = e >> 4;
+                numM2P += targetsOf((unsigned)(e & 15));
                 if (valid && (((e & 15) >> q) & 1))
                     m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
             }
@@ -499,6 +511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         {
             const uint32_t cn = jn;
             const unsigned cm = jm;
+            numP2P += (unsigned long long)cn * targetsOf(cm);
             __builtin_amdgcn_wave_barrier();
             {
                 // source l goes to pair P = 4 (l / 8) + l % 4 as half (l / 4) % 2: the lane of sub s evaluates sources
@@ -566,6 +579,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             const bool     mine = valid && (((e & 15) >> q) & 1);
             const int      lidx = a.internalToLeaf[node];
             const uint32_t s0 = a.layout[lidx], s1 = a.layout[lidx + 1];
+            numP2P += (unsigned long long)(s1 - s0) * targetsOf((unsigned)(e & 15));
             for (uint32_t c0 = s0; c0 < s1; c0 += kWave)
             {
                 const uint32_t cnt = min((uint32_t)kWave, s1 - c0);
@@ -651,6 +665,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         a.ax[i]        = (float)((double)a.ax[i] + G * acc[1]);
         a.ay[i]        = (float)((double)a.ay[i] + G * acc[2]);
         a.az[i]        = (float)((double)a.az[i] + G * acc[3]);
+    }
+    if (lane == 0 && a.inter)
+    {
+        atomicAdd(a.inter, numP2P);
+        atomicAdd(a.inter + 1, numM2P);
     }
     u = waveSum(u);
     if (lane == 0 && a.waveE) a.waveE[g] = 0.5 * u;

@@ -33,6 +33,8 @@ struct GravArgs
     uint32_t* err;        // bit 0: traversal stack exhausted
     int       fast;       // 1: M2P/P2P in float with rsqrt (displacements formed in double, sums in double)
     const uint8_t* active; // nullable: targets with active[i] == 0 (outside the group view) get no gravity
+    unsigned long long* interactions; // nullable: [0] += P2P, [1] += M2P interactions summed over the targets (the
+                                      // reference's BhStats sumP2P / sumM2P, nbody/traversal.cuh:346-357, 614-620)
 };
 
 //! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi

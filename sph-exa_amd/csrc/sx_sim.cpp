@@ -1240,6 +1240,7 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     ga.egrav = &s->sc->egrav;
     ga.err   = &s->sc->gravErr;
     ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
+    ga.interactions = s->work.get<unsigned long long>("grav.inter", 2);
     SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
     ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(ga, st));
@@ -1266,6 +1267,7 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     fa.egrav = &s->sc->egrav;
     fa.err   = &s->sc->gravErr;
     fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
+    fa.interactions = ga.interactions;
     SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
     fa.waveE = s->work.get<double>("grav.waveE", (fa.last - fa.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(fa, st));
@@ -1560,6 +1562,15 @@ extern "C"
         return SX_OK;
     }
 
+    int sx_sim_gravity_interactions(sx_sim* s, uint64_t out[2])
+    {
+        if (!s || s->p.g == 0.0) return SX_ERR_ARG;
+        hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        SIM_HIP(hipMemcpyAsync(out, s->work.get<unsigned long long>("grav.inter", 2), 16, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        return SX_OK;
+    }
+
     int sx_sim_gravity_stats(sx_sim* s, uint64_t out[3])
     {
         out[0] = s->gravHalos;
@@ -1816,6 +1827,8 @@ extern "C"
         SIM_HIP(hipEventRecord(s->kev[12], st));
         if (s->p.g != 0.0)
         {
+            auto* inter = s->work.get<unsigned long long>("grav.inter", 2); // P2P, M2P of this step (BhStats)
+            SIM_HIP(hipMemsetAsync(inter, 0, 2 * sizeof(unsigned long long), st));
             if (dist)
             {
                 if (int e = distributedGravity(s, st, nullptr)) return e;
@@ -1842,6 +1855,7 @@ extern "C"
             ga.egrav = &s->sc->egrav;
             ga.err   = &s->sc->gravErr;
             ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
+            ga.interactions = inter;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
             ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
             SIM_HIP(gravityTraverse(ga, st));

@@ -189,6 +189,7 @@ def lib():
         "sx_sim_kernel_times": (C.c_int, [vp, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_char_p)]),
         "sx_sim_set_comm": (C.c_int, [vp, vp]),
         "sx_sim_gravity_stats": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_sim_gravity_interactions": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_sim_conserved": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sx_conserved_quantities": (C.c_int, [vp, C.POINTER(SxFields), u32, u32, C.c_float, C.c_double,
                                               C.POINTER(C.c_double)]),
@@ -681,6 +682,12 @@ class Sim:
         out = (C.c_uint64 * 3)()
         self.L.sx_sim_gravity_stats(self.h, out)
         return dict(halos=out[0], far_cells=out[1], remote_cells=out[2])
+
+    def gravity_interactions(self):
+        """P2P and M2P interactions of the last step (sx_sim_gravity_interactions; the reference's BhStats)"""
+        out = (C.c_uint64 * 2)()
+        self.ctx.check(self.L.sx_sim_gravity_interactions(self.h, out), "gravity_interactions")
+        return dict(p2p=out[0], m2p=out[1])
 
     def close(self):
         if self.h:

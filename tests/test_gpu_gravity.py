@@ -175,3 +175,28 @@ def test_traverse_group_view(ctx):
         assert np.all(got[~inview] == marker), k
         assert np.array_equal(got[inview], full[k][inview]), k
     assert 0 > eg.value > full["egrav"]  # part of the sum, same sign
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_interaction_counts(ctx, exact):
+    """sx_sim_gravity_interactions counts per target like the reference's BhStats (traversal.cuh:346-357): with an
+    opening angle so small that every node violates the MAC, every target interacts by P2P with every particle
+    (sumP2P = N^2, sumM2P = 0); at theta = 0.5 both kinds occur and far fewer sources than N^2 are visited"""
+    from sphexa_amd import ic
+
+    arrays, lim, bnd, dt0 = ic.evrard(12)
+    n = arrays["x"].size
+    counts = {}
+    for theta in (1e-6, 0.5):
+        ctx.set_exact(exact)
+        sim = sx.Sim(ctx, n, sx.make_box(lim, bnd), params=sx.default_params(g=1.0, theta=theta))
+        try:
+            sim.set_state(arrays, dt0, dt0)
+            sim.step()
+            counts[theta] = sim.gravity_interactions()
+        finally:
+            sim.close()
+            ctx.set_exact(False)
+    assert counts[1e-6] == {"p2p": n * n, "m2p": 0}, (n, counts)
+    c = counts[0.5]
+    assert c["m2p"] > 0 and 0 < c["p2p"] < n * n // 2, (n, c)

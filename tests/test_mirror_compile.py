@@ -5,7 +5,12 @@ headers, on the CPU (no GPU call is made):
   15-89) is defined by the mirror, so the whole reference header can be swapped for it (INTEGRATION.md);
 * tests/mirror_ref_compile.cpp instantiates each of them with the reference's cstone::Box, GroupView, GroupData,
   OctreeNsView and util::array<float, Timestep::maxNumRungs> types and a DeviceParticlesData-shaped dataset, and
-  links against libsphexa_hip.so.
+  links against libsphexa_hip.so (g++, a minimal thrust::device_vector stand-in);
+* the same file compiled by hipcc against the image's real rocThrust (/opt/rocm/include/thrust): every dataset field
+  and GroupData<GpuTag>::data a real thrust::device_vector, the mirror's rawPtr through device_ptr::get().  Host
+  pass only, to an object: the reference headers read under __HIPCC__ include <cuda_runtime.h> (its HIP build
+  hipifies them first), so they are read in their host configuration (see the file); the object's undefined
+  symbols are exactly sx_* functions of include/sphexa_hip.h.
 
 Runs where /root/reference exists (this container); skipped on the GPU box.
 """
@@ -49,3 +54,21 @@ def test_mirror_compiles_and_links_with_reference_types(tmp_path):
            "-o", str(exe), f"-L{LIBDIR}", "-lsphexa_hip", f"-Wl,-rpath,{LIBDIR}"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+@needs_ref
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/include/thrust/device_vector.h") or shutil.which("hipcc") is None
+                    and not os.path.exists("/opt/rocm/bin/hipcc"), reason="rocThrust / hipcc not present")
+def test_mirror_compiles_against_rocthrust(tmp_path):
+    import sphexa_amd as sx
+
+    obj = tmp_path / "mirror_thrust.o"
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-host-only", "--offload-arch=gfx950", "-std=c++20", "-O0", "-w",
+           "-DSX_REAL_THRUST", f"-I{REF}/domain/include", f"-I{REF}/sph/include", f"-I{ROOT}/include",
+           f"-I{ROOT}/sph-exa_amd/host", "-c", os.path.join(ROOT, "tests", "mirror_ref_compile.cpp"), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    nm = subprocess.run(["nm", "-C", str(obj)], capture_output=True, text=True, check=True).stdout
+    assert "thrust" in nm and "device_vector" in nm  # the real rocThrust types were instantiated
+    undefined_sx = {ln.split()[-1] for ln in nm.splitlines() if " U sx_" in ln}
+    assert undefined_sx and undefined_sx <= set(sx.header_symbols()), undefined_sx - set(sx.header_symbols())
