@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--gravity", action="store_true", help="only the multi-rank gravity of the IC (G = 1)")
     ap.add_argument("--overlap", action="store_true", help="interior clusters before each halo exchange")
+    ap.add_argument("--converge-h", action="store_true", help="h after the first search's h iteration (pyoracle)")
     args = ap.parse_args()
     import torch.distributed as dist
 
@@ -36,6 +37,8 @@ def main():
 
     ic = {"sedov": po.sedov_state, "noh": po.noh_state, "evrard": po.evrard_state}[args.ic]
     st, box = ic(args.side)
+    if args.converge_h:
+        po.converge_h(po.load_oracle(), st, box)
     f, l = st.n * args.rank // args.size, st.n * (args.rank + 1) // args.size
     local = po.HostState(l - f)
     for k in po.CONSERVED:

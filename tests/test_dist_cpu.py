@@ -155,3 +155,22 @@ def test_overlapped_exchanges_classification(tmp_path, ic, side):
                 assert np.array_equal(x, y), (s, q, k)
                 assert not np.any(np.isnan(y.astype(np.float64)))
             assert np.array_equal(a[q][f"s{s}_scalars"], b[q][f"s{s}_scalars"])
+
+
+def test_decomposed_gravity_matches_reference_two_ranks(tmp_path):
+    """the same restatement on the IC of tests/golden/evrard20_grav_mpi.npz against the reference's own 2-rank
+    gravity (Domain::syncGrav + computeGlobalMultipoles + computeGravity under MPICH, oracle/gen_grav_mpi.py): two
+    Barnes-Hut trees of theta = 0.5, within the opening-angle error; the reference's 2-rank result equals its
+    1-rank result bit for bit (its focus tree is independent of the decomposition; egrav to the order of its sum)"""
+    import golden_util as gu
+
+    fx = gu.load("evrard20_grav_mpi.npz")
+    assert np.array_equal(fx["acc_p1"], fx["acc_p2"]) and abs(fx["egrav_p1"][0] / fx["egrav_p2"][0] - 1) < 1e-14
+    ranks = run_ranks(tmp_path, 2, 20, 1, "evrard", ("--gravity", "--converge-h"))
+    ids = np.concatenate([d["id"] for d in ranks]).astype(np.int64)
+    acc = np.concatenate([d["acc"] for d in ranks])
+    a_ref = fx["acc_p2"].astype(np.float64)[ids]
+    err = np.linalg.norm(acc - a_ref, axis=1) / np.linalg.norm(a_ref, axis=1)
+    assert np.median(err) < 1e-3 and np.max(err) < 1e-2, (np.median(err), np.max(err))
+    eg = sum(float(d["egrav"][0]) for d in ranks)  # each rank's share of 0.5 sum G m phi
+    assert abs(eg / fx["egrav_p2"][0] - 1) < 1e-3, (eg, fx["egrav_p2"][0])

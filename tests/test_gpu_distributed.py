@@ -14,6 +14,7 @@ import sys
 import numpy as np
 import pytest
 
+import golden_util as gu
 import pyoracle as po
 
 pytestmark = pytest.mark.gpu
@@ -150,6 +151,18 @@ def test_distributed_gravity_matches_direct_sum(tmp_path, nproc, port):
     a_h = np.stack([hydro.ax[oh], hydro.ay[oh], hydro.az[oh]], 1).astype(np.float64)
     err = np.linalg.norm(a_gpu - a_h - ag, axis=1) / np.linalg.norm(ag, axis=1)
     assert np.median(err) < 1e-3 and np.max(err) < 1e-2, (np.median(err), np.max(err))
+    # the reference's own multi-rank gravity on the same IC (Domain::syncGrav + computeGlobalMultipoles +
+    # computeGravity under MPICH with 2 ranks, oracle/gen_grav_mpi.py): two Barnes-Hut trees of theta = 0.5 (the
+    # reference's focus tree vs this library's local + level-6 far tree), so within the opening-angle error
+    fx = gu.load("evrard20_grav_mpi.npz")
+    assert np.array_equal(fx["x"], st.x) and np.array_equal(fx["h"], st.h)
+    a_ref = fx["acc_p2"].astype(np.float64)
+    err_ref = np.linalg.norm(a_gpu - a_h - a_ref, axis=1) / np.linalg.norm(a_ref, axis=1)
+    egrav_gpu = ranks[0]["s0_conserved"][2]
+    print(f"{nproc} ranks vs the reference's 2-rank gravity: median {np.median(err_ref):.2g}, max {err_ref.max():.2g}; "
+          f"egrav {egrav_gpu:.8g} vs {fx['egrav_p2'][0]:.8g}")
+    assert np.median(err_ref) < 1e-3 and np.max(err_ref) < 1e-2, (np.median(err_ref), err_ref.max())
+    assert abs(egrav_gpu / fx["egrav_p2"][0] - 1) < 1e-3
     # both source paths were exercised: some remote cells far (multipoles), some near (gravity halos)
     for d in ranks:
         halos, far_cells, remote_cells = d["s0_gravity"]

@@ -180,14 +180,14 @@ def test_traverse_group_view(ctx):
 @pytest.mark.parametrize("exact", [False, True])
 def test_interaction_counts(ctx, exact):
     """sx_sim_gravity_interactions counts per target like the reference's BhStats (traversal.cuh:346-357): with an
-    opening angle so small that every node violates the MAC, every target interacts by P2P with every particle
+    opening angle so small that every node violates the MAC (mac = 2 size / theta + |com - center| beyond the box even for level-21 nodes), every target interacts by P2P with every particle
     (sumP2P = N^2, sumM2P = 0); at theta = 0.5 both kinds occur and far fewer sources than N^2 are visited"""
     from sphexa_amd import ic
 
     arrays, lim, bnd, dt0 = ic.evrard(12)
     n = arrays["x"].size
     counts = {}
-    for theta in (1e-6, 0.5):
+    for theta in (1e-20, 0.5):
         ctx.set_exact(exact)
         sim = sx.Sim(ctx, n, sx.make_box(lim, bnd), params=sx.default_params(g=1.0, theta=theta))
         try:
@@ -197,6 +197,6 @@ def test_interaction_counts(ctx, exact):
         finally:
             sim.close()
             ctx.set_exact(False)
-    assert counts[1e-6] == {"p2p": n * n, "m2p": 0}, (n, counts)
+    assert counts[1e-20] == {"p2p": n * n, "m2p": 0}, (n, counts)
     c = counts[0.5]
     assert c["m2p"] > 0 and 0 < c["p2p"] < n * n // 2, (n, c)
