@@ -611,13 +611,69 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
     }
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+//! kernelWt on two arguments at once (packed FP32: v_pk_fma / v_pk_mul)
+__device__ __forceinline__ v2f kernelWt2(v2f t)
+{
+    t     = v2f{fminf(t.x, 4.0f), fminf(t.y, 4.0f)};
+    v2f s = v2f{3.08339593857454e-08f, 3.08339593857454e-08f};
+    s     = __builtin_elementwise_fma(s, t, v2f{-2.262898533444968e-06f, -2.262898533444968e-06f});
+    s     = __builtin_elementwise_fma(s, t, v2f{0.00010206655861111358f, 0.00010206655861111358f});
+    s     = __builtin_elementwise_fma(s, t, v2f{-0.0029803994111716747f, -0.0029803994111716747f});
+    s     = __builtin_elementwise_fma(s, t, v2f{0.050733841955661774f, 0.050733841955661774f});
+    s     = __builtin_elementwise_fma(s, t, v2f{-0.411233514547348f, -0.411233514547348f});
+    s     = __builtin_elementwise_fma(s, t, v2f{1.0f, 1.0f});
+    const v2f s2 = s * s;
+    return s2 * s2 * s2;
+}
+
+/*! Packed-FP32 walk over this lane's share of its list (resident union, field-major LDS records sf[k * CH + slot]):
+ *  per list word both neighbors at once, field k of the two as one register pair (two ds_read_b32, no packing
+ *  moves).  body(F, two) gets F(k) -> v2f {field k of the first neighbor, of the second} and whether the second
+ *  exists (a missing second neighbor reads slot 0).  Field bases every 9 fields keep ds_read's 16-bit offsets. */
+template<int CH, int NF, class Body>
+__device__ __forceinline__ void packedLoop(const Clu& cu, const float* sf, Body&& body)
+{
+    const uint32_t  wLast = cu.wEnd - 1;
+    const uint32_t* nl    = cu.nl;
+    auto            ld    = [&](uint32_t w) { return nl[(size_t)min(w, wLast) * kWave]; };
+    uint32_t        q0 = ld(cu.wBeg + 1), q1 = ld(cu.wBeg + 2);
+    uint32_t        wd = nl[(size_t)cu.wBeg * kWave];
+    constexpr int   NB = (NF + 8) / 9;
+    for (uint32_t w = cu.wBeg;;)
+    {
+        const bool two = 2 * w + 1 < cu.cnt;
+        uint32_t   i0[NB], i1[NB];
+        i0[0] = wd & 0xffffu, i1[0] = wd >> 16;
+#pragma unroll
+        for (int b = 1; b < NB; ++b)
+        {
+            i0[b] = i0[0] + 9 * b * CH, i1[b] = i1[0] + 9 * b * CH;
+            asm volatile("" : "+v"(i0[b]));
+            asm volatile("" : "+v"(i1[b]));
+        }
+        auto F = [&](int k) { return v2f{sf[i0[k / 9] + (k % 9) * CH], sf[i1[k / 9] + (k % 9) * CH]}; };
+        wd = q0, q0 = q1, q1 = ld(w + 3);
+        body(F, two);
+        if (++w >= cu.wEnd) break;
+    }
+}
+
+#ifndef SX_AV_PK
+#define SX_AV_PK 0 // AV switches: packed FP32 over field-major LDS records
+#endif
+
 // ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
 template<int CH, int SPLIT, int UMIN = 0, int UMAX = 0>
 __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
 {
-    __shared__ float4 sP[CH]; // x, y, z, vol
-    __shared__ float4 sV[CH]; // vx, vy, vz, c
-    __shared__ float  sD[CH]; // divv
+    constexpr bool    SOA = SX_AV_PK;
+    constexpr int     CA  = SOA ? 1 : CH;
+    __shared__ float4 sP[CA]; // x, y, z, vol
+    __shared__ float4 sV[CA]; // vx, vy, vz, c
+    __shared__ float  sD[CA]; // divv
+    __shared__ float  sF[SOA ? 9 * CH : 1]; // SOA: the same 9 fields, field-major
     __shared__ float  s_red[kClusterWaves * SPLIT];
     if constexpr (UMIN > 0 || UMAX > 0)
     {
@@ -637,18 +693,71 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
     float       vijsignal_i = 1.e-40f * ci;
     float       gx = 0, gy = 0, gz = 0;
     bool        res = false;
+    auto        stage = [&](uint32_t j, uint32_t slot) {
+        const RecX r = a.rx[j];
+        const RecV v = a.rv[j];
+        const RecT t = a.rt[j];
+        if constexpr (SOA)
+        {
+            const float f[9] = {relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
+                                t.xm / t.kx, v.vx, v.vy, v.vz, v.c, a.rc[j].divv};
+#pragma unroll
+            for (int k = 0; k < 9; ++k)
+                sF[k * CH + slot] = f[k];
+            return;
+        }
+        sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
+                               t.xm / t.kx);
+        sV[slot] = make_float4(v.vx, v.vy, v.vz, v.c);
+        sD[slot] = a.rc[j].divv;
+    };
+    auto loadRec = [&](uint32_t p) {
+        if constexpr (SOA)
+            return Rec9{make_float4(sF[p], sF[CH + p], sF[2 * CH + p], sF[3 * CH + p]),
+                        make_float4(sF[4 * CH + p], sF[5 * CH + p], sF[6 * CH + p], sF[7 * CH + p]), sF[8 * CH + p]};
+        else return Rec9{sP[p], sV[p], sD[p]};
+    };
+#if SX_AV_PK
+    if (cu.U <= (uint32_t)CH)
+    {
+        // stage the resident union (neighborLoop's fill), then both neighbors of a list word per packed instruction
+        constexpr int  NT = kB * SPLIT;
+        for (uint32_t u = threadIdx.x; u < cu.U; u += NT)
+            stage(cu.un[u], u);
+        __syncthreads();
+        if (cu.wBeg < cu.wEnd)
+        {
+            const v2f xi2 = {xi, xi}, yi2 = {yi, yi}, zi2 = {zi, zi}, vx2 = {vi.vx, vi.vx}, vy2 = {vi.vy, vi.vy},
+                      vz2 = {vi.vz, vi.vz}, hiInv2_2 = {hiInv2, hiInv2}, ci2 = {ci, ci}, dv2 = {divv_i, divv_i};
+            v2f       G[3] = {{0, 0}, {0, 0}, {0, 0}};
+            packedLoop<CH, 9>(cu, sF, [&](auto&& F, bool two) {
+                v2f rx = xi2 - F(0), ry = yi2 - F(1), rz = zi2 - F(2);
+                if (cu.pbc)
+                {
+                    float x0 = rx.x, y0 = ry.x, z0 = rz.x, x1 = rx.y, y1 = ry.y, z1 = rz.y;
+                    applyPBC(a.box, h2, x0, y0, z0);
+                    applyPBC(a.box, h2, x1, y1, z1);
+                    rx = v2f{x0, x1}, ry = v2f{y0, y1}, rz = v2f{z0, z1};
+                }
+                v2f r2 = rx * rx + ry * ry + rz * rz;
+                r2.y   = two ? r2.y : 1.0f; // slot 0 may be the target itself: keep the skipped term finite
+                const v2f rinv = {rsqrtf(r2.x), rsqrtf(r2.y)};
+                const v2f rv   = rx * (vx2 - F(4)) + ry * (vy2 - F(5)) + rz * (vz2 - F(6));
+                const v2f t    = ci2 + F(7) - v2f{3.0f, 3.0f} * rv * rinv;
+                const float s0 = rv.x < 0.0f ? t.x : 0.0f, s1 = (two && rv.y < 0.0f) ? t.y : 0.0f;
+                vijsignal_i    = fmaxf(vijsignal_i, fmaxf(s0, s1));
+                const v2f fw   = kernelWt2(r2 * hiInv2_2) * (F(3) * (dv2 - F(8))) * v2f{1.0f, two ? 1.0f : 0.0f};
+                G[0] += fw * rx;
+                G[1] += fw * ry;
+                G[2] += fw * rz;
+            });
+            gx = G[0].x + G[0].y, gy = G[1].x + G[1].y, gz = G[2].x + G[2].y;
+        }
+    }
+    else
+#endif
     neighborLoop<CH, SPLIT>(
-        cu,
-        [&](uint32_t j, uint32_t slot) {
-            const RecX r = a.rx[j];
-            const RecV v = a.rv[j];
-            const RecT t = a.rt[j];
-            sP[slot]     = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
-                                   relc(r.z, cu.oz, a.box, 2), t.xm / t.kx);
-            sV[slot]     = make_float4(v.vx, v.vy, v.vz, v.c);
-            sD[slot]     = a.rc[j].divv;
-        },
-        [&](uint32_t p) { return Rec9{sP[p], sV[p], sD[p]}; },
+        cu, stage, loadRec,
         [&](const Rec9& r) {
             const float4& q  = r.a;
             const float4& v  = r.b;
@@ -670,7 +779,7 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         res);
     {
         float v[4] = {gx, gy, gz, vijsignal_i};
-        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 8u, true);
+        combineShares<SPLIT>(cu, v, SOA ? sF : reinterpret_cast<float*>(sP), 8u, true);
         gx = v[0], gy = v[1], gz = v[2], vijsignal_i = v[3];
     }
     if (!cu.valid || cu.part != 0) return;
@@ -715,23 +824,6 @@ __device__ __forceinline__ void atwoodWeights(float Atwood, float Atmin, float A
         a_mom             = exp2f(fmaf(sigma, dl, 2.0f * lxi));
         b_mom             = exp2f(fmaf(-sigma, dl, 2.0f * lxj));
     }
-}
-
-typedef float v2f __attribute__((ext_vector_type(2)));
-
-//! kernelWt on two arguments at once (packed FP32: v_pk_fma / v_pk_mul)
-__device__ __forceinline__ v2f kernelWt2(v2f t)
-{
-    t     = v2f{fminf(t.x, 4.0f), fminf(t.y, 4.0f)};
-    v2f s = v2f{3.08339593857454e-08f, 3.08339593857454e-08f};
-    s     = __builtin_elementwise_fma(s, t, v2f{-2.262898533444968e-06f, -2.262898533444968e-06f});
-    s     = __builtin_elementwise_fma(s, t, v2f{0.00010206655861111358f, 0.00010206655861111358f});
-    s     = __builtin_elementwise_fma(s, t, v2f{-0.0029803994111716747f, -0.0029803994111716747f});
-    s     = __builtin_elementwise_fma(s, t, v2f{0.050733841955661774f, 0.050733841955661774f});
-    s     = __builtin_elementwise_fma(s, t, v2f{-0.411233514547348f, -0.411233514547348f});
-    s     = __builtin_elementwise_fma(s, t, v2f{1.0f, 1.0f});
-    const v2f s2 = s * s;
-    return s2 * s2 * s2;
 }
 
 #ifndef SX_ME_PK
@@ -1091,8 +1183,18 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
             for (uint32_t w = cu.wBeg;;)
             {
                 const bool     two = 2 * w + 1 < cu.cnt; // the word's second neighbor exists
-                const uint32_t j0 = wd & 0xffffu, j1 = wd >> 16;
-                auto           F  = [&](int k) { return v2f{sF[k][j0], sF[k][j1]}; };
+                // three bases per neighbor (fields 0-8, 9-17, 18-19) within ds_read's 16-bit offset: the bases are
+                // laundered so the compiler does not fold them back into one add per field
+                uint32_t i0[3] = {wd & 0xffffu, 0u, 0u}, i1[3] = {wd >> 16, 0u, 0u};
+#pragma unroll
+                for (int b = 1; b < 3; ++b)
+                {
+                    i0[b] = i0[0] + 9 * b * CH, i1[b] = i1[0] + 9 * b * CH;
+                    asm volatile("" : "+v"(i0[b]));
+                    asm volatile("" : "+v"(i1[b]));
+                }
+                const float* sf = &sF[0][0];
+                auto F = [&](int k) { return v2f{sf[i0[k / 9] + (k % 9) * CH], sf[i1[k / 9] + (k % 9) * CH]}; };
                 const v2f      PX = F(0), PY = F(1), PZ = F(2), PW = F(3), VX = F(4), VY = F(5), VZ = F(6), VW = F(7);
                 const v2f      TX = F(8), TY = F(9), TZ = F(10), TW = F(11), AX = F(12), AY = F(13), AZ = F(14);
                 const v2f      AW = F(15), BX = F(16), BY = F(17), BZ = F(18), BW = F(19);
