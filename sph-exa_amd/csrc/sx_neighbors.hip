@@ -30,7 +30,8 @@
  * divergent loop whose trip count is the MAX over the wave's lanes of the hits in that chunk; a chunk is a compact
  * region, so the lanes near it have many hits and the others few, and the sum of these maxima was ~3.9x a lane's
  * own hit count (Sedov lattice: 180 iterations per wave against 46).  The masks of the last h pass are therefore
- * kept (global scratch per resident workgroup, the chunk tables in LDS) and expanded once after the pass, each
+ * kept (global scratch per resident workgroup, only the nonzero ones, compacted per lane: zero masks, about half
+ * of them, cost no traffic; the chunk tables in LDS) and expanded once after the pass, each
  * lane walking its own nonzero masks: trip count = max over lanes of its own hits / 2.  A wave with more chunks
  * than its table holds expands the full batch early with candidate indices, which the final pass rewrites to union
  * positions.
@@ -73,6 +74,48 @@ constexpr int kCandWords = kCandSpace / 32;
 #endif
 constexpr int kBatch = SX_NS_BATCH; //!< chunks whose hit masks a wave keeps before expanding them into its lists
 static_assert(kBatch <= 32, "nonzero-chunk bits per lane");
+
+#ifndef SX_NS_PAIR
+#define SX_NS_PAIR 0
+#endif
+#ifndef SX_NS_EXP4
+#define SX_NS_EXP4 0
+#endif
+#ifndef SX_NS_NT_LIST
+#define SX_NS_NT_LIST 0
+#endif
+//! a u16-pair list word: the lists are read only by later kernels, a streaming store keeps them from evicting the
+//! hit-mask rows and candidate coordinates this kernel re-reads from L2 (variant SX_NS_NT_LIST)
+__device__ __forceinline__ void storeList(uint32_t* p, uint32_t w)
+{
+    if constexpr (SX_NS_NT_LIST) __builtin_nontemporal_store(w, p);
+    else *p = w;
+}
+
+#ifndef SX_NS_PROBE
+#define SX_NS_PROBE 0
+#endif
+#if SX_NS_PROBE
+//! phase cycle counters of the search (probe builds only): [0] regions, [1] tree walk, [2] scan + reach, [3] stream
+//! and test, [4] h-iteration vote, [5] union, [6] early-entry rewrite + final expansion, [7] tail; [8] waves;
+//! read from the host through the symbol (scripts/search_probe.py)
+__device__ unsigned long long g_nsProbe[16];
+#ifdef SX_NS_SMALL
+#define SX_PROBE_FN sx_debug_ns_probe_small
+#else
+#define SX_PROBE_FN sx_debug_ns_probe_large
+#endif
+//! probe builds only (not part of the C-ABI): copy the counters out (reset: and zero them)
+extern "C" __attribute__((visibility("default"))) int SX_PROBE_FN(unsigned long long* out, int reset);
+#define SX_PROBE(k)                                                                                                    \
+    {                                                                                                                  \
+        const unsigned long long t_ = __builtin_readcyclecounter();                                                    \
+        prAcc[k] += t_ - prT;                                                                                          \
+        prT = t_;                                                                                                      \
+    }
+#else
+#define SX_PROBE(k)
+#endif
 
 __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t* pre, uint32_t idx)
 {
@@ -247,14 +290,19 @@ findNeighborsKernel(NsArgs a)
         a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[0]) : (a.numGroups + kClusterWaves - 1) / kClusterWaves;
     if (numClusters == 0) return;
     if (a.redo && blockIdx.x == 0 && threadIdx.x == 0) a.stats[11] = 1u; // the compact build ran first
-    const int      wave        = threadIdx.x >> 6;
+    const int      wave        = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: scalar
     const int      lane        = threadIdx.x & 63;
     NsWaveLds&     wl          = s_str.w[wave];
     // this wave's hit-mask rows (kBatch x 64 lanes), one slot per workgroup of the persistent grid
     uint64_t* const maskRow = a.hitMasks + ((size_t)blockIdx.x * kClusterWaves + wave) * kBatch * kWave + lane;
     if (threadIdx.x == 0) s_next = grabCluster(a.work, numClusters);
     __syncthreads();
-    uint32_t ci = s_next; // this workgroup's work item: a cluster, or a position in the redo list
+    // this workgroup's work item: a cluster, or a position in the redo list (uniform: the cluster's origin, list and
+    // scratch addresses are then scalar)
+    uint32_t ci = __builtin_amdgcn_readfirstlane(s_next);
+#if SX_NS_PROBE
+    unsigned long long prAcc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prT = __builtin_readcyclecounter(), prWaves = 0;
+#endif
     while (ci < numClusters)
     {
     const uint32_t c = a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[1 + ci]) : ci;
@@ -300,10 +348,11 @@ findNeighborsKernel(NsArgs a)
         uint32_t nz = nzq;
         int      q  = nz ? __builtin_ctz(nz) : 0;
         nz &= nz - 1u;
-        uint64_t m  = __builtin_nontemporal_load(maskRow + (size_t)q * kWave);
+        uint64_t m  = __builtin_nontemporal_load(maskRow);
         bool     hn = nz != 0u;
         int      qn = hn ? __builtin_ctz(nz) : 0;
-        uint64_t mn = __builtin_nontemporal_load(maskRow + (size_t)qn * kWave);
+        int      kn = 1; // row of the next nonzero chunk
+        uint64_t mn = __builtin_nontemporal_load(maskRow + (size_t)(hn ? kn : 0) * kWave);
         nz &= nz - 1u;
         if (!nzq) m = 0ull;
         while (m)
@@ -317,7 +366,7 @@ findNeighborsKernel(NsArgs a)
             // one store site: odd parity completes the pending word, even parity writes a fresh pair
             const bool     odd = stored & 1u;
             const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
-            if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
+            if (odd || two) storeList(ll + (size_t)(stored >> 1) * kWave, w);
             pend = odd ? e2 : e1;
             stored += two ? 2u : 1u;
             if (!m)
@@ -325,7 +374,8 @@ findNeighborsKernel(NsArgs a)
                 m  = hn ? mn : 0ull, q = qn;
                 hn = nz != 0u;
                 qn = hn ? __builtin_ctz(nz) : 0;
-                mn = __builtin_nontemporal_load(maskRow + (size_t)qn * kWave);
+                kn += hn ? 1 : 0;
+                mn = __builtin_nontemporal_load(maskRow + (size_t)(hn ? kn : 0) * kWave);
                 nz &= nz - 1u;
             }
         }
@@ -335,62 +385,107 @@ findNeighborsKernel(NsArgs a)
         __builtin_amdgcn_wave_barrier(); // table reads precede the next chunk's staging writes
     };
 
-    /*! the final expansion with the masks in LDS: every thread's nonzero-chunk masks are loaded in one burst (all
-     *  loads in flight together) and parked in the candidate-space bytes and its wave's record slots (kMaskLds per
-     *  thread), so the per-lane cursor below reads only LDS: no load latency, and no wait on the list stores it
-     *  issues (vmcnt counts stores too, in order).  A thread with more nonzero chunks than slots (rare) reads the
-     *  rest from the scratch rows.  Called by every thread of the workgroup after the union and the early-entry
-     *  rewrite, when the candidate space is dead. */
+    /*! the final expansion with the masks in LDS: every thread's nonzero-chunk masks are loaded in bursts (all loads
+     *  of a burst in flight together) and parked in the candidate-space bytes and its wave's record slots (kMaskLds
+     *  per thread), then walked by a per-lane cursor that reads only LDS.  No global load may sit inside the walk:
+     *  vmcnt counts the list stores too, in order, so any load there (even one only a few lanes take, or a flat
+     *  access the compiler cannot place in LDS) makes every iteration wait for the previous iteration's stores to
+     *  complete.  A lane with more nonzero chunks than slots is served in further rounds of kMaskLds masks.  Called
+     *  by every thread of the workgroup after the union and the early-entry rewrite, when the candidate space is
+     *  dead. */
     auto expandFinal = [&]() {
         uint64_t* const slotsRec = reinterpret_cast<uint64_t*>(wl.rec); // [2][64] of this wave
-        auto slotAddr = [&](int k) -> uint64_t* {
-            return k < kMaskSlots ? &s_cm.mk[k][threadIdx.x] : slotsRec + (k - kMaskSlots) * kWave + lane;
+        auto slot = [&](int k) -> uint64_t& {
+            return k < kMaskSlots ? s_cm.mk[k][threadIdx.x] : slotsRec[(k - kMaskSlots) * kWave + lane];
         };
+        const int nnz = __popc(nzq);
+        uint32_t  nz  = nzq; // chunks of the masks not yet walked (bit q: chunk q of the batch)
+        for (int r0 = 0; __ballot(r0 < nnz) != 0ull; r0 += kMaskLds)
         {
-            // groups of 8 chunks: 8 loads in flight, then parked (16 VGPRs, not 2 kBatch)
-            int k = 0;
-            for (int q0 = 0; q0 < nq; q0 += 8)
+            // this round's rows r0 .. r0 + rn - 1 (the lane's nonzero masks, compacted) -> slots 0 .. rn - 1, groups
+            // of 8 loads in flight (16 VGPRs)
+            const int rn = max(0, min(nnz - r0, kMaskLds));
+            for (int k0 = 0; k0 < rn; k0 += 8)
             {
                 uint64_t v[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
-                    v[u] = q0 + u < nq ? __builtin_nontemporal_load(maskRow + (size_t)(q0 + u) * kWave) : 0ull;
+                    v[u] = k0 + u < rn ? __builtin_nontemporal_load(maskRow + (size_t)(r0 + k0 + u) * kWave) : 0ull;
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
-                    if ((nzq >> (q0 + u)) & 1u)
-                    {
-                        if (k < kMaskLds) *slotAddr(k) = v[u];
-                        ++k;
-                    }
+                    if (k0 + u < rn) slot(k0 + u) = v[u];
             }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): this thread's slots have landed (only it reads them)
-        uint32_t nz = nzq;
-        int      q  = nz ? __builtin_ctz(nz) : 0;
-        nz &= nz - 1u;
-        int      k  = 0;
-        uint64_t m  = nzq ? *slotAddr(0) : 0ull;
-        while (m)
-        {
-            const uint16_t* tq = wl.tab[q];
-            const uint32_t  e1 = tq[__builtin_ctzll(m)];
-            m &= m - 1ull;
-            const bool     two = m != 0ull;
-            const uint32_t e2  = two ? tq[__builtin_ctzll(m)] : 0u;
-            if (two) m &= m - 1ull;
-            // one store site: odd parity completes the pending word, even parity writes a fresh pair
-            const bool     odd = stored & 1u;
-            const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
-            if (odd || two) ll[(size_t)(stored >> 1) * kWave] = w;
-            pend = odd ? e2 : e1;
-            stored += two ? 2u : 1u;
-            if (!m && nz)
+            __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): this thread's slots have landed (only it reads them)
+            int q = rn > 0 ? __builtin_ctz(nz) : 0;
+            if (rn > 0) nz &= nz - 1u;
+#if SX_NS_EXP4
+            // four entries per iteration (four table reads in flight, up to two list words); the next mask is read
+            // ahead from an in-range slot and taken when the current one runs out
+            uint64_t m  = rn > 0 ? slot(0) : 0ull;
+            int      kn = 1;
+            bool     hn = kn < rn;
+            int      qn = hn ? __builtin_ctz(nz) : 0;
+            if (hn) nz &= nz - 1u;
+            uint64_t mn = slot(min(kn, kMaskLds - 1));
+            while (m || hn) // m may run out at the end of an iteration with masks left
             {
-                q = __builtin_ctz(nz);
-                nz &= nz - 1u;
-                ++k;
-                m = k < kMaskLds ? *slotAddr(k) : __builtin_nontemporal_load(maskRow + (size_t)q * kWave);
+                uint32_t e[4];
+                uint32_t c = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    if (!m && hn)
+                    {
+                        m  = mn;
+                        q  = qn;
+                        ++kn;
+                        hn = kn < rn;
+                        qn = hn ? __builtin_ctz(nz) : 0;
+                        if (hn) nz &= nz - 1u;
+                        mn = slot(min(kn, kMaskLds - 1));
+                    }
+                    const bool h = m != 0ull;
+                    e[u]         = wl.tab[q][h ? __builtin_ctzll(m) : 0];
+                    m &= m - 1ull;
+                    c += h ? 1u : 0u;
+                }
+                // the sequence [pend if odd] e0..e(c-1): its complete pairs are list words, an odd last one pends
+                const bool     odd = stored & 1u;
+                const uint32_t s0 = odd ? pend : e[0], s1 = odd ? e[0] : e[1], s2 = odd ? e[1] : e[2],
+                               s3 = odd ? e[2] : e[3];
+                const uint32_t len = c + (odd ? 1u : 0u);
+                uint32_t*      row = ll + (size_t)(stored >> 1) * kWave;
+                if (len >= 2u) storeList(row, s0 | (s1 << 16));
+                if (len >= 4u) storeList(row + kWave, s2 | (s3 << 16));
+                pend = len == 1u ? s0 : (len == 3u ? s2 : e[3]);
+                stored += c;
             }
+#else
+            int      k = 0;
+            uint64_t m = rn > 0 ? slot(0) : 0ull;
+            while (m)
+            {
+                const uint16_t* tq = wl.tab[q];
+                const uint32_t  e1 = tq[__builtin_ctzll(m)];
+                m &= m - 1ull;
+                const bool     two = m != 0ull;
+                const uint32_t e2  = two ? tq[__builtin_ctzll(m)] : 0u;
+                if (two) m &= m - 1ull;
+                // one store site: odd parity completes the pending word, even parity writes a fresh pair
+                const bool     odd = stored & 1u;
+                const uint32_t w   = odd ? (pend | (e1 << 16)) : (e1 | (e2 << 16));
+                if (odd || two) storeList(ll + (size_t)(stored >> 1) * kWave, w);
+                pend = odd ? e2 : e1;
+                stored += two ? 2u : 1u;
+                if (!m && k + 1 < rn)
+                {
+                    q = __builtin_ctz(nz);
+                    nz &= nz - 1u;
+                    ++k;
+                    m = slot(k);
+                }
+            }
+#endif
         }
         nq  = 0;
         nzq = 0;
@@ -400,6 +495,7 @@ findNeighborsKernel(NsArgs a)
     bool abandoned = false;
     while (true)
     {
+        SX_PROBE(7)
         // ---- 1./2. search regions, then the candidate leaves within reach of one, numbered into the candidate space
         if (threadIdx.x == 0) s_nreg = 0;
         __syncthreads();
@@ -476,6 +572,7 @@ findNeighborsKernel(NsArgs a)
             }
             return bits;
         };
+        SX_PROBE(0)
         bool      overflow = false;
         const int nCand    = clusterCollectLeaves(
             a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, s_bfsCnt, wave,
@@ -532,6 +629,7 @@ findNeighborsKernel(NsArgs a)
             abandoned = true; // nothing of this cluster is written: h, nc, lists and union stay for the redo
             break;
         }
+        SX_PROBE(1)
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
@@ -547,6 +645,7 @@ findNeighborsKernel(NsArgs a)
         }
         __syncthreads(); // the regions (aliasing the stream LDS) are no longer read
 
+        SX_PROBE(2)
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f    = 4.0f * hi * hi;
         const double radSq  = (double)r2f;
@@ -582,12 +681,16 @@ findNeighborsKernel(NsArgs a)
             }
             hw = fmaxf(hw, __shfl_xor(hw, o, kWave));
         }
-        const float bcx = 0.5f * (blo[0] + bhi[0]), bcy = 0.5f * (blo[1] + bhi[1]), bcz = 0.5f * (blo[2] + bhi[2]);
-        const float bsx = 0.5f * (bhi[0] - blo[0]), bsy = 0.5f * (bhi[1] - blo[1]), bsz = 0.5f * (bhi[2] - blo[2]);
+        // the wave box (identical in every lane after the butterfly): scalar registers
+        auto        rfl = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+        const float bcx = rfl(0.5f * (blo[0] + bhi[0])), bcy = rfl(0.5f * (blo[1] + bhi[1])),
+                    bcz = rfl(0.5f * (blo[2] + bhi[2]));
+        const float bsx = rfl(0.5f * (bhi[0] - blo[0])), bsy = rfl(0.5f * (bhi[1] - blo[1])),
+                    bsz = rfl(0.5f * (bhi[2] - blo[2]));
         const float bmag  = fmaxf(fabsf(blo[0]), fabsf(bhi[0])) + fmaxf(fabsf(blo[1]), fabsf(bhi[1])) +
                            fmaxf(fabsf(blo[2]), fabsf(bhi[2]));
         const float cullR = 2.0f * hw * (1.0f + 0x1p-12f) + 0x1p-16f * (bmag + 2.0f * hw);
-        const float cullR2 = (fastWave && hw > 0.0f) ? cullR * cullR : 3e38f;
+        const float cullR2 = rfl((fastWave && hw > 0.0f) ? cullR * cullR : 3e38f);
         // bound on |p| + |r| over every staged candidate and lane: the error scale of the packed test
         const float E   = bmag + cullR + sqrtf(xr * xr + yr * yr + zr * zr);
         const float tol = valid ? 0x1p-19f * fmaf(E, E, thr) : 0.0f;
@@ -719,8 +822,9 @@ findNeighborsKernel(NsArgs a)
                     const uint32_t ci = tq[lane];
                     atomicOr(&s_bits[ci >> 5], 1u << (ci & 31));
                 }
-                // the chunk joins the batch: this lane's mask row (coalesced 512-B store per wave)
-                maskRow[(size_t)nq * kWave] = hm;
+                // the chunk joins the batch: a nonzero mask goes to the lane's next row (rows compacted per lane: the
+                // k-th nonzero chunk of the batch, bit k of nzq, sits in row k; zero masks cost no traffic)
+                if (hm) maskRow[(size_t)__popc(nzq) * kWave] = hm;
                 nzq |= (hm != 0ull ? 1u : 0u) << nq;
                 if (++nq == kBatch) expandBatch(false);
             }
@@ -802,16 +906,8 @@ findNeighborsKernel(NsArgs a)
                 X = a.x[j], Y = a.y[j], Z = a.z[j];
             }
         };
-        Blk cur{-1, 0, 0, 0};
-        advance(cur);
-        double cx = 0, cy = 0, cz = 0;
-        load(cur, cx, cy, cz);
-        while (cur.cc < numCand)
-        {
-            Blk nxt = cur;
-            advance(nxt);
-            double nx = 0, ny = 0, nz = 0;
-            load(nxt, nx, ny, nz);
+        // cull, stage and (when the chunk fills, or after the last block) test one block; `last`: no block follows
+        auto block = [&](const Blk& cur, double cx, double cy, double cz, bool last) {
             const uint32_t j  = cur.s + lane;
             const bool     in = j < cur.p1;
             float          px = 0, py = 0, pz = 0;
@@ -840,10 +936,47 @@ findNeighborsKernel(NsArgs a)
             if (valid && i >= cur.s && i - cur.s < (uint32_t)kWave && i < cur.p1)
                 selfSeq = seq + (uint32_t)(fill + __popcll(bm & ((1ull << (i - cur.s)) - 1ull)));
             fill += n;
-            if (fill == kWave || (nxt.cc >= numCand && fill > 0)) testChunk();
+            if (fill == kWave || (last && fill > 0)) testChunk();
+        };
+        Blk cur{-1, 0, 0, 0};
+        advance(cur);
+        double cx = 0, cy = 0, cz = 0;
+        load(cur, cx, cy, cz);
+#if SX_NS_PAIR
+        // two blocks per iteration: both of the next pair are loaded while the current pair is processed, so one
+        // load round trip (the wait at the loop's end, where the prefetched registers become the current ones) is
+        // spent per two blocks
+        Blk    cu2 = cur;
+        advance(cu2);
+        double cx2 = 0, cy2 = 0, cz2 = 0;
+        load(cu2, cx2, cy2, cz2);
+        while (cur.cc < numCand)
+        {
+            Blk nxt = cu2;
+            advance(nxt);
+            Blk nx2 = nxt;
+            advance(nx2);
+            double nx = 0, ny = 0, nz = 0, nx_2 = 0, ny_2 = 0, nz_2 = 0;
+            load(nxt, nx, ny, nz);
+            load(nx2, nx_2, ny_2, nz_2);
+            block(cur, cx, cy, cz, cu2.cc >= numCand);
+            if (cu2.cc < numCand) block(cu2, cx2, cy2, cz2, nxt.cc >= numCand);
+            cur = nxt, cx = nx, cy = ny, cz = nz;
+            cu2 = nx2, cx2 = nx_2, cy2 = ny_2, cz2 = nz_2;
+        }
+#else
+        while (cur.cc < numCand)
+        {
+            Blk nxt = cur;
+            advance(nxt);
+            double nx = 0, ny = 0, nz = 0;
+            load(nxt, nx, ny, nz);
+            block(cur, cx, cy, cz, nxt.cc >= numCand);
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
+#endif
 
+        SX_PROBE(3)
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -868,6 +1001,7 @@ findNeighborsKernel(NsArgs a)
         int any = 0;
         for (int w = 0; w < kClusterWaves; ++w)
             any |= s_again[w];
+        SX_PROBE(4)
         if (!any) break;
         __syncthreads(); // s_again / candidate space / regions are rewritten by the next iteration
     }
@@ -933,6 +1067,7 @@ findNeighborsKernel(NsArgs a)
             }
         }
         __syncthreads(); // s_pre complete
+        SX_PROBE(5)
         // the last batch's chunk tables -> union positions
         for (int q = 0; q < nq; ++q)
         {
@@ -972,6 +1107,7 @@ findNeighborsKernel(NsArgs a)
         __syncthreads(); // the candidate space and the union bitmap are dead: the masks take their bytes
         // the last batch: union positions straight into the lists (the early entries' last pending half included)
         expandFinal();
+        SX_PROBE(6)
         if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
     }
 
@@ -1005,9 +1141,33 @@ findNeighborsKernel(NsArgs a)
         a.clStats[c] = t;
     }
     __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
-    ci = s_next;
+    ci = __builtin_amdgcn_readfirstlane(s_next);
+#if SX_NS_PROBE
+    ++prWaves;
+#endif
     }
+#if SX_NS_PROBE
+    SX_PROBE(7)
+    if (lane == 0)
+    {
+        for (int k = 0; k < 8; ++k)
+            atomicAdd(&g_nsProbe[k], prAcc[k]);
+        atomicAdd(&g_nsProbe[8], prWaves);
+    }
+#endif
 }
+
+#if SX_NS_PROBE
+extern "C" int SX_PROBE_FN(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsProbe), sizeof(g_nsProbe), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    const unsigned long long z[16] = {};
+    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_nsProbe), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return 1;
+    return 0;
+}
+#endif
 
 //! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]
 __global__ void exportKernel(NsArgs a, uint32_t* out)

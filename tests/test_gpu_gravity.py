@@ -181,10 +181,11 @@ def test_traverse_group_view(ctx):
 def test_interaction_counts(ctx, exact):
     """sx_sim_gravity_interactions counts per target like the reference's BhStats (traversal.cuh:346-357): with an
     opening angle so small that every node violates the MAC (mac = 2 size / theta + |com - center| beyond the box even for level-21 nodes), every target interacts by P2P with every particle
-    (sumP2P = N^2, sumM2P = 0); at theta = 0.5 both kinds occur and far fewer sources than N^2 are visited"""
+    (sumP2P = N^2, sumM2P = 0); at theta = 0.5 both kinds occur (at least one M2P node per target on average) and fewer sources than
+    N^2 are visited by P2P"""
     from sphexa_amd import ic
 
-    arrays, lim, bnd, dt0 = ic.evrard(12)
+    arrays, lim, bnd, dt0 = ic.evrard(24)  # ~7k particles: at theta 0.5 most sources are then far enough for M2P
     n = arrays["x"].size
     counts = {}
     for theta in (1e-20, 0.5):
@@ -199,4 +200,4 @@ def test_interaction_counts(ctx, exact):
             ctx.set_exact(False)
     assert counts[1e-20] == {"p2p": n * n, "m2p": 0}, (n, counts)
     c = counts[0.5]
-    assert c["m2p"] > 0 and 0 < c["p2p"] < n * n // 2, (n, c)
+    assert c["m2p"] >= n and 0 < c["p2p"] < 0.8 * n * n, (n, c)
