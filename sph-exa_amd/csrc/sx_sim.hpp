@@ -108,7 +108,7 @@ struct sx_sim
     uint32_t* stats;
     uint32_t* statsHost;
     int       sortBits{30};          // key bits the local sort orders first (sortLocals)
-    uint64_t  sortStats[3]{0, 0, 0}; // sorts requested, done (not the identity), redone on all bits
+    uint64_t  sortStats[4]{0, 0, 0, 0}; // sorts requested, done (not the identity), redone on all bits, moved-only
     Scalars*  sc;
     Scalars*  scHost;
 

@@ -458,6 +458,83 @@ hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hip
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void movedPositionsKernel(const uint32_t* __restrict__ order, size_t n,
+                                                            uint32_t* __restrict__ idx, uint32_t* count)
+{
+    const size_t   i  = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const bool     mv = i < n && order[i] != (uint32_t)i;
+    const uint64_t b  = __ballot(mv);
+    if (!b) return;
+    // one atomic per wave, lanes in order behind it
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
+    uint32_t  base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(b));
+    base = __shfl(base, leader);
+    if (mv) idx[base + __popcll(b & ((1ull << lane) - 1ull))] = (uint32_t)i;
+}
+
+hipError_t movedPositions(const uint32_t* order, size_t n, uint32_t* idx, uint32_t* count, hipStream_t s)
+{
+    if (!n) return hipSuccess;
+    movedPositionsKernel<<<grid(n), 256, 0, s>>>(order, n, idx, count);
+    return hipGetLastError();
+}
+
+//! field bytes of the set and the offset of field f's column in tmp (columns of `moved` elements, 8-byte aligned)
+struct MovedCols
+{
+    size_t off[kMaxGatherFields];
+};
+
+template<bool GATHER>
+__global__ __launch_bounds__(256) void movedCopyKernel(const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ idx, uint32_t moved, GatherSet set,
+                                                       MovedCols cols, char* __restrict__ tmp)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= moved) return;
+    const uint32_t i = idx[k];
+    const uint32_t o = GATHER ? order[i] : 0u;
+    for (int f = 0; f < set.count; ++f) // uniform
+    {
+        char* col = tmp + cols.off[f];
+        if (set.bytes[f] == 8)
+        {
+            if (GATHER) reinterpret_cast<uint64_t*>(col)[k] = static_cast<const uint64_t*>(set.src[f])[o];
+            else static_cast<uint64_t*>(set.dst[f])[i] = reinterpret_cast<const uint64_t*>(col)[k];
+        }
+        else if (set.bytes[f] == 4)
+        {
+            if (GATHER) reinterpret_cast<uint32_t*>(col)[k] = static_cast<const uint32_t*>(set.src[f])[o];
+            else static_cast<uint32_t*>(set.dst[f])[i] = reinterpret_cast<const uint32_t*>(col)[k];
+        }
+        else
+        {
+            if (GATHER) reinterpret_cast<uint8_t*>(col)[k] = static_cast<const uint8_t*>(set.src[f])[o];
+            else static_cast<uint8_t*>(set.dst[f])[i] = reinterpret_cast<const uint8_t*>(col)[k];
+        }
+    }
+}
+
+hipError_t permuteMoved(const uint32_t* order, const uint32_t* idx, uint32_t moved, const GatherSet& set, char* tmp,
+                        hipStream_t s)
+{
+    if (!moved || !set.count) return hipSuccess;
+    MovedCols cols{};
+    size_t    off = 0;
+    for (int f = 0; f < set.count; ++f)
+    {
+        if (set.bytes[f] != 1 && set.bytes[f] != 4 && set.bytes[f] != 8) return hipErrorInvalidValue;
+        if (set.src[f] != set.dst[f]) return hipErrorInvalidValue; // in place only
+        cols.off[f] = off;
+        off += ((size_t)moved * set.bytes[f] + 7) & ~size_t(7);
+    }
+    const unsigned g = (moved + 255) / 256;
+    movedCopyKernel<true><<<g, 256, 0, s>>>(order, idx, moved, set, cols, tmp);
+    movedCopyKernel<false><<<g, 256, 0, s>>>(order, idx, moved, set, cols, tmp);
+    return hipGetLastError();
+}
+
 template<class T>
 static hipError_t exclusiveScan(Arena& arena, const char* tag, const T* in, T* out, int n, hipStream_t s)
 {
