@@ -698,32 +698,30 @@ int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
     s->sortStats[1]++;
     SIM_HIP(hipMemcpyAsync(s->keys, kOut, nl * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     // a nearly stationary state moves few positions per step (Sedov 64M: ~10 %): then only those are rewritten, in
-    // place (two passes through a compact buffer), instead of gathering every field into its spare buffer
+    // place (read into a scratch copy, then written back), instead of gathering every field into its spare buffer
     {
-        uint32_t* idx = s->work.get<uint32_t>("sort.moved", nl);
         SIM_HIP(hipMemsetAsync(cnt, 0, 4, st));
-        SIM_HIP(movedPositions(s->order, nl, idx, cnt, st));
+        SIM_HIP(movedCount(s->order, nl, cnt, st));
         SIM_HIP(hipMemcpyAsync(cntH, cnt, 4, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
-        const uint32_t moved = *cntH;
-        if (moved <= nl / 4)
+        if (*cntH <= nl / 4)
         {
-            size_t rowBytes = 0;
+            size_t colBytes = 0;
             for (auto& sp : s->spares)
-                rowBytes += (size_t)sp.elemBytes;
-            char*     tmp = s->work.get<char>("sort.movedtmp", (nl / 4 + 1) * (rowBytes + 8 * kMaxGatherFields));
+                colBytes += ((size_t)nl * sp.elemBytes + 255) & ~size_t(255);
+            char*     tmp = s->work.get<char>("sort.movedtmp", colBytes);
             GatherSet set{};
             for (auto& sp : s->spares)
             {
                 if (set.count == kMaxGatherFields)
                 {
-                    SIM_HIP(permuteMoved(s->order, idx, moved, set, tmp, st));
+                    SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
                     set.count = 0;
                 }
                 set.src[set.count] = *sp.field, set.dst[set.count] = *sp.field, set.bytes[set.count] = sp.elemBytes;
                 ++set.count;
             }
-            SIM_HIP(permuteMoved(s->order, idx, moved, set, tmp, st));
+            SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
             s->sortStats[3]++;
             return SX_OK;
         }

@@ -458,80 +458,74 @@ hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hip
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void movedPositionsKernel(const uint32_t* __restrict__ order, size_t n,
-                                                            uint32_t* __restrict__ idx, uint32_t* count)
+//! number of positions i < n with order[i] != i (added to *count): a capped grid, one atomic per block
+__global__ __launch_bounds__(256) void movedCountKernel(const uint32_t* __restrict__ order, size_t n, uint32_t* count)
 {
-    const size_t   i  = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const bool     mv = i < n && order[i] != (uint32_t)i;
-    const uint64_t b  = __ballot(mv);
-    if (!b) return;
-    // one atomic per wave, lanes in order behind it
-    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
-    uint32_t  base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(b));
-    base = __shfl(base, leader);
-    if (mv) idx[base + __popcll(b & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    uint32_t c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c += order[i] != (uint32_t)i ? 1u : 0u;
+    c = waveSum(c);
+    __shared__ uint32_t s_c[4];
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        const uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        if (t) atomicAdd(count, t);
+    }
 }
 
-hipError_t movedPositions(const uint32_t* order, size_t n, uint32_t* idx, uint32_t* count, hipStream_t s)
+hipError_t movedCount(const uint32_t* order, size_t n, uint32_t* count, hipStream_t s)
 {
     if (!n) return hipSuccess;
-    movedPositionsKernel<<<grid(n), 256, 0, s>>>(order, n, idx, count);
+    movedCountKernel<<<(unsigned)std::min<size_t>(2048, (n + 255) / 256), 256, 0, s>>>(order, n, count);
     return hipGetLastError();
 }
 
-//! field bytes of the set and the offset of field f's column in tmp (columns of `moved` elements, 8-byte aligned)
-struct MovedCols
-{
-    size_t off[kMaxGatherFields];
-};
-
+//! GATHER: tmp_f[i] = field_f[order[i]]; else field_f[i] = tmp_f[i]; both only where order[i] != i
 template<bool GATHER>
-__global__ __launch_bounds__(256) void movedCopyKernel(const uint32_t* __restrict__ order,
-                                                       const uint32_t* __restrict__ idx, uint32_t moved, GatherSet set,
-                                                       MovedCols cols, char* __restrict__ tmp)
+__global__ __launch_bounds__(256) void movedCopyKernel(const uint32_t* __restrict__ order, size_t n, GatherSet set,
+                                                       GatherSet tmp)
 {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= moved) return;
-    const uint32_t i = idx[k];
-    const uint32_t o = GATHER ? order[i] : 0u;
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = order[i];
+    if (o == (uint32_t)i) return;
     for (int f = 0; f < set.count; ++f) // uniform
     {
-        char* col = tmp + cols.off[f];
+        void* t = tmp.dst[f];
         if (set.bytes[f] == 8)
         {
-            if (GATHER) reinterpret_cast<uint64_t*>(col)[k] = static_cast<const uint64_t*>(set.src[f])[o];
-            else static_cast<uint64_t*>(set.dst[f])[i] = reinterpret_cast<const uint64_t*>(col)[k];
+            if (GATHER) static_cast<uint64_t*>(t)[i] = static_cast<const uint64_t*>(set.src[f])[o];
+            else static_cast<uint64_t*>(set.dst[f])[i] = static_cast<const uint64_t*>(t)[i];
         }
         else if (set.bytes[f] == 4)
         {
-            if (GATHER) reinterpret_cast<uint32_t*>(col)[k] = static_cast<const uint32_t*>(set.src[f])[o];
-            else static_cast<uint32_t*>(set.dst[f])[i] = reinterpret_cast<const uint32_t*>(col)[k];
+            if (GATHER) static_cast<uint32_t*>(t)[i] = static_cast<const uint32_t*>(set.src[f])[o];
+            else static_cast<uint32_t*>(set.dst[f])[i] = static_cast<const uint32_t*>(t)[i];
         }
         else
         {
-            if (GATHER) reinterpret_cast<uint8_t*>(col)[k] = static_cast<const uint8_t*>(set.src[f])[o];
-            else static_cast<uint8_t*>(set.dst[f])[i] = reinterpret_cast<const uint8_t*>(col)[k];
+            if (GATHER) static_cast<uint8_t*>(t)[i] = static_cast<const uint8_t*>(set.src[f])[o];
+            else static_cast<uint8_t*>(set.dst[f])[i] = static_cast<const uint8_t*>(t)[i];
         }
     }
 }
 
-hipError_t permuteMoved(const uint32_t* order, const uint32_t* idx, uint32_t moved, const GatherSet& set, char* tmp,
-                        hipStream_t s)
+hipError_t permuteMoved(const uint32_t* order, size_t n, const GatherSet& set, char* tmp, hipStream_t s)
 {
-    if (!moved || !set.count) return hipSuccess;
-    MovedCols cols{};
-    size_t    off = 0;
+    if (!n || !set.count) return hipSuccess;
+    GatherSet cols = set;
+    size_t    off  = 0;
     for (int f = 0; f < set.count; ++f)
     {
         if (set.bytes[f] != 1 && set.bytes[f] != 4 && set.bytes[f] != 8) return hipErrorInvalidValue;
         if (set.src[f] != set.dst[f]) return hipErrorInvalidValue; // in place only
-        cols.off[f] = off;
-        off += ((size_t)moved * set.bytes[f] + 7) & ~size_t(7);
+        cols.dst[f] = tmp + off;
+        off += (n * set.bytes[f] + 255) & ~size_t(255);
     }
-    const unsigned g = (moved + 255) / 256;
-    movedCopyKernel<true><<<g, 256, 0, s>>>(order, idx, moved, set, cols, tmp);
-    movedCopyKernel<false><<<g, 256, 0, s>>>(order, idx, moved, set, cols, tmp);
+    movedCopyKernel<true><<<grid(n), 256, 0, s>>>(order, n, set, cols);
+    movedCopyKernel<false><<<grid(n), 256, 0, s>>>(order, n, set, cols);
     return hipGetLastError();
 }
 

@@ -264,13 +264,12 @@ struct GatherSet
     int         bytes[kMaxGatherFields];
 };
 hipError_t gatherMany(const uint32_t* order, size_t n, const GatherSet& set, hipStream_t s);
-//! the positions i < n with order[i] != i, in any order, into idx[0 .. *count) (*count zeroed by the caller)
-hipError_t movedPositions(const uint32_t* order, size_t n, uint32_t* idx, uint32_t* count, hipStream_t s);
-/*! in-place reorder of the fields set.src[f] (== set.dst[f]) at the `moved` positions idx[0 .. moved): field[i] =
- *  old field[order[i]] for every listed i (the others are fixed points of order), through tmp (>= moved x the set's
- *  bytes per particle): every moved value is read before any is written (two kernels) */
-hipError_t permuteMoved(const uint32_t* order, const uint32_t* idx, uint32_t moved, const GatherSet& set, char* tmp,
-                        hipStream_t s);
+//! number of positions i < n with order[i] != i, added to *count
+hipError_t movedCount(const uint32_t* order, size_t n, uint32_t* count, hipStream_t s);
+/*! in-place reorder of the fields set.src[f] (== set.dst[f]) where order moves them: field[i] = old field[order[i]]
+ *  for every i with order[i] != i, through tmp (n x the set's bytes per particle, columns 256-byte aligned): every
+ *  moved value is read before any is written (two kernels); the fixed points of order are not touched */
+hipError_t permuteMoved(const uint32_t* order, size_t n, const GatherSet& set, char* tmp, hipStream_t s);
 hipError_t buildTree(Arena& arena, const uint64_t* keys, size_t n, uint32_t bucket, const DevBox& box, DevTree& t,
                      hipStream_t s);
 hipError_t nodeCenters(const uint64_t* prefixes, int numNodes, const DevBox& b, double* centers, double* sizes,
