@@ -1115,6 +1115,7 @@ findNeighborsKernel(NsArgs a)
     {
         a.nc[i] = count + 1;
         if (a.iterateH) a.h[i] = hi;
+        if (a.rxOut) a.rxOut[i] = RecX{xi, yi, zi, hi, a.m[i]};
     }
     // statistics (NcStats-like): per wave, then per cluster into clStats (reduced after the launch)
     const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;

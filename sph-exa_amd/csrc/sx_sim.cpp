@@ -769,6 +769,15 @@ __global__ void classifyClustersKernel(const uint32_t* uni, const uint32_t* ucou
     }
 }
 
+//! RecX of the halos [0, first) and [last, n): the search wrote the locals' records (NsArgs::rxOut)
+void packXHalos(sx_sim* s, hipStream_t st)
+{
+    if (s->first) packX(s->first, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+    if (s->n > s->last)
+        packX(s->n - s->last, s->x + s->last, s->y + s->last, s->z + s->last, s->h + s->last, s->m + s->last,
+              s->rx + s->last, st);
+}
+
 //! exchange one set of fields for the halos of this step (send lists built by discoverHalos)
 int haloExchange(sx_sim* s, std::initializer_list<std::pair<void*, int>> fields, hipStream_t st)
 {
@@ -1672,6 +1681,8 @@ extern "C"
             na.clStats        = s->mem.get<uint4>("ns.clstats", (na.numGroups + kClusterWaves - 1) / kClusterWaves);
             na.work           = s->mem.get<uint32_t>("ns.work", 16);
             na.hitMasks       = s->mem.get<uint64_t>("ns.masks", searchScratchBytes() / sizeof(uint64_t));
+            na.rxOut          = s->rx; // the locals' RecX: packed by the search itself (packXHalos below)
+            na.m              = s->m;
             if (!na.hSave || !na.clStats || !na.work || !na.hitMasks) return SX_ERR_NOMEM;
             if (const char* reps = getenv("SX_SEARCH_REPS"); reps && attempt == 0)
             {
@@ -1742,7 +1753,7 @@ extern "C"
             // ---- HydroProp::computeForces (std_hydro.hpp:124-166): density, EOS, [v,rho,p,c] halos, IAD,
             //      [c_ij] halos, momentum + energy.  The stage/kernel event slots follow the VE order:
             //      density in "xmass", IAD in "iadDivvCurlv", momentumEnergySTD in "momentumEnergy".
-            packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+            packXHalos(s, st);
             SIM_HIP(hipEventRecord(s->kev[2], st));
             PairArgs da = pa;
             da.xm       = s->rho; // computeDensity: xmass written to rho (xmass_gpu.cu:151-153)
@@ -1788,7 +1799,7 @@ extern "C"
         else
         {
             // ---- XMass
-            packX(n, s->x, s->y, s->z, s->h, s->m, s->rx, st);
+            packXHalos(s, st);
             SIM_HIP(hipEventRecord(s->kev[2], st));
             H.xmass(pa, st);
             SIM_HIP(hipEventRecord(s->kev[3], st));

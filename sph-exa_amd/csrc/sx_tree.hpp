@@ -234,6 +234,10 @@ struct NsArgs
     // per-workgroup hit-mask scratch, searchScratchBytes() bytes
     uint32_t*       work;
     uint64_t*       hitMasks;
+    // optional: the targets' final neighbor records {x, y, z, h, m} (the pair kernels' RecX), written by the search
+    // for every target it completes, so no separate packing pass is needed for [first, last)
+    RecX*           rxOut;
+    const float*    m;
 
     void setLists(const NbLists& L)
     {
