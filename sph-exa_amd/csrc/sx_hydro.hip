@@ -423,10 +423,13 @@ __global__ void eosKernel(EosArgs a)
     double tmp = (double)idealGasCv(a.mui, a.gamma) * a.temp[i] * (a.gamma - 1.0);
     double pi  = (double)rho * tmp;
     double ci  = sqrt(tmp);
-    a.prho[i]  = (float)(pi / (double)(a.kx[i] * a.m[i] * a.m[i] * a.gradh[i]));
-    a.c[i]     = (float)ci;
+    const float prho = (float)(pi / (double)(a.kx[i] * a.m[i] * a.m[i] * a.gradh[i]));
+    a.prho[i]        = prho;
+    a.c[i]           = (float)ci;
     if (a.rho) a.rho[i] = rho;
     if (a.p) a.p[i] = (float)pi;
+    if (a.rvOut) a.rvOut[i] = RecV{a.vx[i], a.vy[i], a.vz[i], (float)ci};
+    if (a.rtOut) a.rtOut[i] = RecT{a.xm[i], a.kx[i], prho, a.alpha[i]};
 }
 
 // ---- std propagator (HydroProp, std_hydro.hpp:124-184) ----------------------------------------------------------

@@ -64,6 +64,11 @@ struct PairArgs
     const uint8_t* active;
     // nullable: each computed target's Courant time-step (momentum kernels), for the per-view-group minimum
     float* dtOut;
+    // nullable (cluster kernels, full views): the producing kernel also writes the targets' records for the next
+    // kernels, so only the halos need a packing pass: XMass rtOut = {xm, 0, 0, 0}, IAD rcOut = {c_ij, divv},
+    // AV switches rtOut = the target's record with the new alpha
+    RecT* rtOut;
+    RecC* rcOut;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent
@@ -125,6 +130,10 @@ struct EosArgs
     const double* temp;
     const float * m, *kx, *xm, *gradh;
     float *       prho, *c, *rho, *p;
+    // nullable: also write the records {vx, vy, vz, c} and {xm, kx, prho, alpha} of [first, last)
+    const float * vx, *vy, *vz, *alpha;
+    RecV*         rvOut;
+    RecT*         rtOut;
 };
 
 struct PosArgs

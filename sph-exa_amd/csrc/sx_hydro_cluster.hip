@@ -328,7 +328,9 @@ __global__ __launch_bounds__(kB * SPLIT) void xmassKernel(PairArgs a)
     if (cu.valid && cu.part == 0)
     {
         const float h3Inv = hInv * hInv * hInv;
-        a.xm[cu.i]        = (float)((double)ri.m / ((double)v[0] * a.K * (double)h3Inv));
+        const float xm    = (float)((double)ri.m / ((double)v[0] * a.K * (double)h3Inv));
+        a.xm[cu.i]        = xm;
+        if (a.rtOut) a.rtOut[cu.i] = RecT{xm, 0.0f, 0.0f, 0.0f};
     }
 }
 
@@ -488,7 +490,9 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         const uint32_t i = cu.i;
         a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
         const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
-        a.divv[i]            = norm_kxi * (dVx0 + dVy1 + dVz2);
+        const float divv_i   = norm_kxi * (dVx0 + dVy1 + dVz2);
+        a.divv[i]            = divv_i;
+        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, 0.0f};
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
@@ -593,7 +597,9 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
         const uint32_t i = cu.i;
         a.c11[i] = c11i, a.c12[i] = c12i, a.c13[i] = c13i, a.c22[i] = c22i, a.c23[i] = c23i, a.c33[i] = c33i;
         const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
-        a.divv[i]            = norm_kxi * (dVx0 + dVy1 + dVz2);
+        const float divv_i   = norm_kxi * (dVx0 + dVy1 + dVz2);
+        a.divv[i]            = divv_i;
+        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, 0.0f};
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
@@ -806,6 +812,13 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         alpha_i              = (float)((double)alpha_i + (double)alphadot * dt);
     }
     a.alpha[cu.i] = alpha_i;
+    if (a.rtOut)
+    {
+        // xm, kx and prho as they are (a concurrent reader of this record sees them unchanged either way)
+        RecT t       = a.rt[cu.i];
+        t.alpha      = alpha_i;
+        a.rtOut[cu.i] = t;
+    }
 }
 
 // ---- momentum + energy: momentumAndEnergyJLoop<avClean> (momentum_energy_kern.hpp:65-222) -------------------

@@ -75,12 +75,6 @@ constexpr int kCandWords = kCandSpace / 32;
 constexpr int kBatch = SX_NS_BATCH; //!< chunks whose hit masks a wave keeps before expanding them into its lists
 static_assert(kBatch <= 32, "nonzero-chunk bits per lane");
 
-#ifndef SX_NS_PAIR
-#define SX_NS_PAIR 0
-#endif
-#ifndef SX_NS_EXP4
-#define SX_NS_EXP4 0
-#endif
 #ifndef SX_NS_NT_LIST
 #define SX_NS_NT_LIST 0
 #endif
@@ -418,49 +412,6 @@ findNeighborsKernel(NsArgs a)
             __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): this thread's slots have landed (only it reads them)
             int q = rn > 0 ? __builtin_ctz(nz) : 0;
             if (rn > 0) nz &= nz - 1u;
-#if SX_NS_EXP4
-            // four entries per iteration (four table reads in flight, up to two list words); the next mask is read
-            // ahead from an in-range slot and taken when the current one runs out
-            uint64_t m  = rn > 0 ? slot(0) : 0ull;
-            int      kn = 1;
-            bool     hn = kn < rn;
-            int      qn = hn ? __builtin_ctz(nz) : 0;
-            if (hn) nz &= nz - 1u;
-            uint64_t mn = slot(min(kn, kMaskLds - 1));
-            while (m || hn) // m may run out at the end of an iteration with masks left
-            {
-                uint32_t e[4];
-                uint32_t c = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                {
-                    if (!m && hn)
-                    {
-                        m  = mn;
-                        q  = qn;
-                        ++kn;
-                        hn = kn < rn;
-                        qn = hn ? __builtin_ctz(nz) : 0;
-                        if (hn) nz &= nz - 1u;
-                        mn = slot(min(kn, kMaskLds - 1));
-                    }
-                    const bool h = m != 0ull;
-                    e[u]         = wl.tab[q][h ? __builtin_ctzll(m) : 0];
-                    m &= m - 1ull;
-                    c += h ? 1u : 0u;
-                }
-                // the sequence [pend if odd] e0..e(c-1): its complete pairs are list words, an odd last one pends
-                const bool     odd = stored & 1u;
-                const uint32_t s0 = odd ? pend : e[0], s1 = odd ? e[0] : e[1], s2 = odd ? e[1] : e[2],
-                               s3 = odd ? e[2] : e[3];
-                const uint32_t len = c + (odd ? 1u : 0u);
-                uint32_t*      row = ll + (size_t)(stored >> 1) * kWave;
-                if (len >= 2u) storeList(row, s0 | (s1 << 16));
-                if (len >= 4u) storeList(row + kWave, s2 | (s3 << 16));
-                pend = len == 1u ? s0 : (len == 3u ? s2 : e[3]);
-                stored += c;
-            }
-#else
             int      k = 0;
             uint64_t m = rn > 0 ? slot(0) : 0ull;
             while (m)
@@ -485,7 +436,6 @@ findNeighborsKernel(NsArgs a)
                     m = slot(k);
                 }
             }
-#endif
         }
         nq  = 0;
         nzq = 0;
@@ -942,29 +892,6 @@ findNeighborsKernel(NsArgs a)
         advance(cur);
         double cx = 0, cy = 0, cz = 0;
         load(cur, cx, cy, cz);
-#if SX_NS_PAIR
-        // two blocks per iteration: both of the next pair are loaded while the current pair is processed, so one
-        // load round trip (the wait at the loop's end, where the prefetched registers become the current ones) is
-        // spent per two blocks
-        Blk    cu2 = cur;
-        advance(cu2);
-        double cx2 = 0, cy2 = 0, cz2 = 0;
-        load(cu2, cx2, cy2, cz2);
-        while (cur.cc < numCand)
-        {
-            Blk nxt = cu2;
-            advance(nxt);
-            Blk nx2 = nxt;
-            advance(nx2);
-            double nx = 0, ny = 0, nz = 0, nx_2 = 0, ny_2 = 0, nz_2 = 0;
-            load(nxt, nx, ny, nz);
-            load(nx2, nx_2, ny_2, nz_2);
-            block(cur, cx, cy, cz, cu2.cc >= numCand);
-            if (cu2.cc < numCand) block(cu2, cx2, cy2, cz2, nxt.cc >= numCand);
-            cur = nxt, cx = nx, cy = ny, cz = nz;
-            cu2 = nx2, cx2 = nx_2, cy2 = ny_2, cz2 = nz_2;
-        }
-#else
         while (cur.cc < numCand)
         {
             Blk nxt = cur;
@@ -974,7 +901,6 @@ findNeighborsKernel(NsArgs a)
             block(cur, cx, cy, cz, nxt.cc >= numCand);
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
-#endif
 
         SX_PROBE(3)
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------

@@ -1800,15 +1800,31 @@ extern "C"
         {
             // ---- XMass
             packXHalos(s, st);
+            // the cluster kernels write the locals' records as they produce them (PairArgs::rtOut / rcOut, EosArgs):
+            // the packing passes below then cover only the halos (halo()); the exact kernels leave it to them
+            const bool fused = H.clusterLists && !pa.active;
+            auto       halo  = [&](size_t a, size_t b, auto&& fn) {
+                if (!fused) return fn(a, b);
+                if (a < s->first) fn(a, std::min(b, (size_t)s->first));
+                if (b > s->last) fn(std::max(a, (size_t)s->last), b);
+            };
             SIM_HIP(hipEventRecord(s->kev[2], st));
-            H.xmass(pa, st);
+            {
+                PairArgs xa = pa;
+                xa.rtOut    = fused ? s->rt : nullptr;
+                H.xmass(xa, st);
+            }
             SIM_HIP(hipEventRecord(s->kev[3], st));
             // ---- [xm] halos, VeDefGradh (overlapped: interior clusters while the halos are in flight)
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             SIM_HIP(hipEventRecord(s->kev[4], st));
             if (int e = exchangeThen(
                     s, H, {{s->xm, 4}},
-                    [&](size_t a, size_t b) { packT(b - a, s->xm + a, nullptr, nullptr, nullptr, s->rt + a, st); },
+                    [&](size_t a, size_t b)
+                    {
+                        halo(a, b, [&](size_t u, size_t v)
+                             { packT(v - u, s->xm + u, nullptr, nullptr, nullptr, s->rt + u, st); });
+                    },
                     [&](const PairArgs& p) { H.veDefGradh(p, st); }, pa, st))
                 return e;
             SIM_HIP(hipEventRecord(s->kev[5], st));
@@ -1816,14 +1832,24 @@ extern "C"
             // ---- EOS, then the v/prho/c/kx halo exchange
             EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
                        s->gradh, s->prho, s->c, nullptr, nullptr};
+            if (fused)
+            {
+                ea.vx = s->vx, ea.vy = s->vy, ea.vz = s->vz, ea.alpha = s->alpha;
+                ea.rvOut = s->rv, ea.rtOut = s->rt; // the locals' {v, c} and {xm, kx, prho, alpha} records
+            }
             H.eos(ea, st);
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             // ---- [v, prho, c, kx] halos, IAD + divv/curlv, rho time-step
             auto packVT = [&](size_t a, size_t b)
             {
-                packV(b - a, s->vx + a, s->vy + a, s->vz + a, s->c + a, s->rv + a, st);
-                packT(b - a, s->xm + a, s->kx + a, s->prho + a, s->alpha + a, s->rt + a, st);
+                halo(a, b,
+                     [&](size_t u, size_t v)
+                     {
+                         packV(v - u, s->vx + u, s->vy + u, s->vz + u, s->c + u, s->rv + u, st);
+                         packT(v - u, s->xm + u, s->kx + u, s->prho + u, s->alpha + u, s->rt + u, st);
+                     });
             };
+            pa.rcOut = fused ? s->rc : nullptr; // IAD writes the locals' {c_ij, divv}
             SIM_HIP(hipEventRecord(s->kev[6], st));
             if (int e = exchangeThen(s, H, {{s->vx, 4}, {s->vy, 4}, {s->vz, 4}, {s->prho, 4}, {s->c, 4}, {s->kx, 4}},
                                      packVT, [&](const PairArgs& p) { H.iadDivvCurlv(p, st); }, pa, st))
@@ -1837,18 +1863,33 @@ extern "C"
                     s, H, {{s->c11, 4}, {s->c12, 4}, {s->c13, 4}, {s->c22, 4}, {s->c23, 4}, {s->c33, 4}, {s->divv, 4}},
                     [&](size_t a, size_t b)
                     {
-                        packC(b - a, s->c11 + a, s->c12 + a, s->c13 + a, s->c22 + a, s->c23 + a, s->c33 + a,
-                              s->divv + a, s->rc + a, st);
+                        halo(a, b,
+                             [&](size_t u, size_t v)
+                             {
+                                 packC(v - u, s->c11 + u, s->c12 + u, s->c13 + u, s->c22 + u, s->c23 + u, s->c33 + u,
+                                       s->divv + u, s->rc + u, st);
+                             });
                     },
-                    [&](const PairArgs& p) { H.avSwitches(p, st); }, pa, st))
+                    [&](const PairArgs& p)
+                    {
+                        PairArgs q = p;
+                        q.rcOut    = nullptr;
+                        q.rtOut    = fused ? s->rt : nullptr; // AV writes the locals' records with the new alpha
+                        H.avSwitches(q, st);
+                    },
+                    pa, st))
                 return e;
+            pa.rcOut = nullptr;
             SIM_HIP(hipEventRecord(s->kev[9], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             // ---- [alpha (+ dV)] halos, momentum + energy.  With avClean the reference exchanges dV11,dV12,dV22,
             //      dV23,dV33 + alpha (ve_hydro.hpp:182-185) and leaves the halo dV13 undefined; all six are exchanged
             //      here so the result does not depend on the decomposition
             auto packTa = [&](size_t a, size_t b)
-            { packT(b - a, s->xm + a, s->kx + a, s->prho + a, s->alpha + a, s->rt + a, st); };
+            {
+                halo(a, b, [&](size_t u, size_t v)
+                     { packT(v - u, s->xm + u, s->kx + u, s->prho + u, s->alpha + u, s->rt + u, st); });
+            };
             auto launchMe = [&](const PairArgs& p) { H.momentumEnergy(p, st); };
             SIM_HIP(hipEventRecord(s->kev[10], st));
             if (s->p.avClean)
