@@ -440,9 +440,13 @@ int    sx_sim_last_stats(sx_sim* sim, sx_nbstats* stats);
 /*! multi-rank self-gravity of the last step: {gravity halos received, remote level-6 cells used as far-field
  *  multipoles, remote cells in total} (zeros on one rank) */
 int    sx_sim_gravity_stats(sx_sim* sim, uint64_t out[3]);
-/*! self-gravity interactions of the last VE step on this rank, counted per target as the reference's BhStats
- *  (nbody/traversal.cuh:346-357, 614-620): {sumP2P (source particles), sumM2P (multipole nodes)}; synchronises.
- *  SX_ERR_ARG without gravity. */
+/*! count the self-gravity interactions of the following steps (the reference's BhStats, collected only when its
+ *  stats are requested, traversal.cuh:346-357): off by default -- the counting traversal is a separate kernel
+ *  instantiation, ~8 % slower.  SX_ERR_ARG without gravity. */
+int    sx_sim_set_gravity_counting(sx_sim* sim, int enable);
+/*! self-gravity interactions of the last VE step on this rank (zeros when counting was off), counted per target as
+ *  the reference's BhStats (nbody/traversal.cuh:346-357, 614-620): {sumP2P (source particles), sumM2P (multipole
+ *  nodes)}; synchronises.  SX_ERR_ARG without gravity. */
 int    sx_sim_gravity_interactions(sx_sim* sim, uint64_t out[2]);
 /*! computeConservedQuantities (conserved_quantities.hpp:110-179) of the current state, summed over the ranks of the
  *  communicator: {ecin, eint, egrav, etot, |linmom|, |angmom|, totalNeighbors, linmom x y z, angmom x y z}

@@ -243,7 +243,9 @@ struct __attribute__((aligned(16))) GSrc
 #ifndef SX_GRAV_WPE
 #define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
 #endif
-template<bool FAST>
+//! COUNT: the per-target interaction counts (GravArgs::interactions, BhStats) -- a separate instantiation because the
+//! counters' registers cost the traversal 9 SGPR and 4 VGPR spills and 3.6 ms at Evrard n=300 (A/B)
+template<bool FAST, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE))) void gravityTraverseKernel(GravArgs args)
 {
     // the fields the traversal reads, as scalars: with the many closures below capturing the kernel argument by
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const uint64_t W    = __ballot(mine);
                     const int      cnt  = __popcll(W);
                     if (cnt == 0) continue;
-                    numM2P += (unsigned long long)cnt * qn[qq];
+                    if constexpr (COUNT) numM2P += (unsigned long long)cnt * qn[qq];
                     SX_LOAD_QUARTER(qq)
                     __builtin_amdgcn_wave_barrier(); // the previous quarter's reads of s_idx are done
                     if (mine) s_idx[wave][__popcll(W & ltMask)] = (uint8_t)lane;
@@ -440,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             {
                 const int e    = __builtin_amdgcn_readfirstlane(s_m2p[wave][k]);
                 const int node = e >> 4;
-                numM2P += targetsOf((unsigned)(e & 15));
+                if constexpr (COUNT) numM2P += targetsOf((unsigned)(e & 15));
                 if (valid && (((e & 15) >> q) & 1))
                     m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
             }
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         {
             const uint32_t cn = jn;
             const unsigned cm = jm;
-            numP2P += (unsigned long long)cn * targetsOf(cm);
+            if constexpr (COUNT) numP2P += (unsigned long long)cn * targetsOf(cm);
             __builtin_amdgcn_wave_barrier();
             {
                 // source l goes to pair P = 4 (l / 8) + l % 4 as half (l / 4) % 2: the lane of sub s evaluates sources
@@ -579,7 +581,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             const bool     mine = valid && (((e & 15) >> q) & 1);
             const int      lidx = a.internalToLeaf[node];
             const uint32_t s0 = a.layout[lidx], s1 = a.layout[lidx + 1];
-            numP2P += (unsigned long long)(s1 - s0) * targetsOf((unsigned)(e & 15));
+            if constexpr (COUNT) numP2P += (unsigned long long)(s1 - s0) * targetsOf((unsigned)(e & 15));
             for (uint32_t c0 = s0; c0 < s1; c0 += kWave)
             {
                 const uint32_t cnt = min((uint32_t)kWave, s1 - c0);
@@ -666,7 +668,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         a.ay[i]        = (float)((double)a.ay[i] + G * acc[2]);
         a.az[i]        = (float)((double)a.az[i] + G * acc[3]);
     }
-    if (lane == 0 && a.inter)
+    if (COUNT && lane == 0 && a.inter)
     {
         atomicAdd(a.inter, numP2P);
         atomicAdd(a.inter + 1, numM2P);
@@ -865,8 +867,14 @@ hipError_t gravityTraverse(const GravArgs& a, hipStream_t s)
 {
     if (a.last <= a.first) return hipSuccess;
     const uint32_t waves = (a.last - a.first + kWave - 1) / kWave;
-    if (a.fast) gravityTraverseKernel<true><<<(waves + 3) / 4, 256, 0, s>>>(a);
-    else gravityTraverseKernel<false><<<(waves + 3) / 4, 256, 0, s>>>(a);
+    const unsigned g = (waves + 3) / 4;
+    if (a.interactions)
+    {
+        if (a.fast) gravityTraverseKernel<true, true><<<g, 256, 0, s>>>(a);
+        else gravityTraverseKernel<false, true><<<g, 256, 0, s>>>(a);
+    }
+    else if (a.fast) gravityTraverseKernel<true, false><<<g, 256, 0, s>>>(a);
+    else gravityTraverseKernel<false, false><<<g, 256, 0, s>>>(a);
     if (a.waveE && a.egrav) reduceWaveEnergyKernel<<<1, 1024, 0, s>>>(a.waveE, waves, a.egrav);
     return hipGetLastError();
 }

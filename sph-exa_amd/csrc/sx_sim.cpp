@@ -1278,7 +1278,7 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     ga.egrav = &s->sc->egrav;
     ga.err   = &s->sc->gravErr;
     ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
-    ga.interactions = s->work.get<unsigned long long>("grav.inter", 2);
+    ga.interactions = s->gravCount ? s->work.get<unsigned long long>("grav.inter", 2) : nullptr;
     SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
     ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(ga, st));
@@ -1600,9 +1600,27 @@ extern "C"
         return SX_OK;
     }
 
+    int sx_sim_set_gravity_counting(sx_sim* s, int enable)
+    {
+        if (!s || s->p.g == 0.0) return SX_ERR_ARG;
+        s->gravCount = enable != 0;
+        if (s->gravCount)
+        {
+            // counts of a step without counting read as zeros, not as stale values
+            hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+            SIM_HIP(hipMemsetAsync(s->work.get<unsigned long long>("grav.inter", 2), 0, 16, st));
+        }
+        return SX_OK;
+    }
+
     int sx_sim_gravity_interactions(sx_sim* s, uint64_t out[2])
     {
         if (!s || s->p.g == 0.0) return SX_ERR_ARG;
+        if (!s->gravCount)
+        {
+            out[0] = out[1] = 0;
+            return SX_OK;
+        }
         hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
         SIM_HIP(hipMemcpyAsync(out, s->work.get<unsigned long long>("grav.inter", 2), 16, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
@@ -1908,8 +1926,9 @@ extern "C"
         SIM_HIP(hipEventRecord(s->kev[12], st));
         if (s->p.g != 0.0)
         {
-            auto* inter = s->work.get<unsigned long long>("grav.inter", 2); // P2P, M2P of this step (BhStats)
-            SIM_HIP(hipMemsetAsync(inter, 0, 2 * sizeof(unsigned long long), st));
+            // P2P, M2P of this step (BhStats), counted only on request (sx_sim_set_gravity_counting)
+            auto* inter = s->gravCount ? s->work.get<unsigned long long>("grav.inter", 2) : nullptr;
+            if (inter) SIM_HIP(hipMemsetAsync(inter, 0, 2 * sizeof(unsigned long long), st));
             if (dist)
             {
                 if (int e = distributedGravity(s, st, nullptr)) return e;

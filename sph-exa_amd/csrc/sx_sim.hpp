@@ -108,6 +108,7 @@ struct sx_sim
     uint32_t* stats;
     uint32_t* statsHost;
     int       sortBits{30};          // key bits the local sort orders first (sortLocals)
+    bool      gravCount = false; // count the gravity interactions (sx_sim_set_gravity_counting)
     uint64_t  sortStats[4]{0, 0, 0, 0}; // sorts requested, done (not the identity), redone on all bits, moved-only
     Scalars*  sc;
     Scalars*  scHost;

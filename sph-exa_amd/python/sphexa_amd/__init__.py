@@ -190,6 +190,7 @@ def lib():
         "sx_sim_set_comm": (C.c_int, [vp, vp]),
         "sx_sim_gravity_stats": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "sx_sim_gravity_interactions": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_sim_set_gravity_counting": (C.c_int, [vp, C.c_int]),
         "sx_sim_conserved": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sx_conserved_quantities": (C.c_int, [vp, C.POINTER(SxFields), u32, u32, C.c_float, C.c_double,
                                               C.POINTER(C.c_double)]),
@@ -682,6 +683,10 @@ class Sim:
         out = (C.c_uint64 * 3)()
         self.L.sx_sim_gravity_stats(self.h, out)
         return dict(halos=out[0], far_cells=out[1], remote_cells=out[2])
+
+    def set_gravity_counting(self, enable=True):
+        """count the gravity interactions of the following steps (sx_sim_set_gravity_counting; off by default)"""
+        self.ctx.check(self.L.sx_sim_set_gravity_counting(self.h, 1 if enable else 0), "set_gravity_counting")
 
     def gravity_interactions(self):
         """P2P and M2P interactions of the last step (sx_sim_gravity_interactions; the reference's BhStats)"""

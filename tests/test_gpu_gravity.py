@@ -194,6 +194,9 @@ def test_interaction_counts(ctx, exact):
         try:
             sim.set_state(arrays, dt0, dt0)
             sim.step()
+            assert sim.gravity_interactions() == {"p2p": 0, "m2p": 0}  # counting is off by default
+            sim.set_gravity_counting(True)
+            sim.step()
             counts[theta] = sim.gravity_interactions()
         finally:
             sim.close()
