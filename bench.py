@@ -334,7 +334,7 @@ def main():
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
     inter = None
-    if kern_sum.get("gravity", 0.0) / args.steps > 0.01:  # self-gravity on (its empty event pair reads ~0.005 ms)
+    if args.init == "evrard":  # self-gravity on (g = 1); the same decision on every rank: the extra step is collective
         # the interaction counts (BhStats) of one more step after the timed region: counting is a separate, slower
         # instantiation of the traversal, so the timed steps run without it
         sim.set_gravity_counting(True)
