@@ -373,10 +373,14 @@ def main():
                             if (dom.get("frac") or 0) < 0.5 else "hbm"),
                 "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) if pmc else None,
                 "definition": "achieved = rocprofv3 PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, same "
-                              "workload; the x2 is measured for coalesced 4/8/16-B, leaf-run and random 16-B/4-B "
-                              "gathers alike, profiles/r3_fetch_calib.json) / avg launch time measured live with HIP "
-                              "events; frac = achieved / 8 TB/s; "
-                              "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s); valu_frac = SURVEY 8(d) flop "
+                              "workload; FETCH_SIZE x2 equals the bytes read for coalesced 4/8/16-B streams and "
+                              "leaf-run record gathers, profiles/r3_fetch_calib.json; for random 16-B/4-B gathers "
+                              "the calibration only shows FETCH_SIZE x2 at 3.3x/8.2x the useful bytes, i.e. whole "
+                              "lines, so the x2 reading is inferred there, not measured) / avg launch time measured "
+                              "live with HIP events; frac = achieved / 8 TB/s; "
+                              "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s: 2 cycles per "
+                              "instruction per SIMD-32 at 2.4 GHz, the chip's rate; one wave alone issues at most "
+                              "half of it, profiles/r4_issue_calib.jsonl); valu_frac = SURVEY 8(d) flop "
                               "per pair x pairs / time / 157.3 TF (FP32 peak at 2.4 GHz); gravity: flop_frac = "
                               "(23 P2P + 54 M2P) / time / 157.3 TF; lds_conflict_frac = "
                               "SQ_LDS_BANK_CONFLICT / 256 CUs / (time x 2.4 GHz); effective_gbs = SURVEY 8(d) edge "
