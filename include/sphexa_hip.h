@@ -427,7 +427,9 @@ int    sx_sim_set_state(sx_sim* sim, size_t n, const double* x, const double* y,
                         const float* m, const double* temp, const float* vx, const float* vy, const float* vz,
                         const float* x_m1, const float* y_m1, const float* z_m1, const float* du_m1,
                         const float* alpha, const uint64_t* id, double minDt, double minDt_m1);
-/*! device field pointers of the current state (valid until the next step) */
+/*! device field pointers of the current state (valid until the next step).  After a one-rank VE or std step the
+ *  keys are those of the updated coordinates (computed by the position update for the next sync), not of the
+ *  step's tree; writing x, y or z through these pointers between steps is not supported on that path */
 int    sx_sim_fields(sx_sim* sim, sx_fields* f, uint64_t** id);
 size_t sx_sim_size(sx_sim* sim);
 /*! one VE step; the time-step scalars stay on the device (no host sync unless stats are requested) */

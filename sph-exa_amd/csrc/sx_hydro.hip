@@ -14,6 +14,7 @@
  * LDS-staged cluster kernels of sx_hydro_cluster.hip.
  */
 #include "sx_hydro.hpp"
+#include "sx_sfc.hpp"
 
 #ifndef SX_VARIANT
 #error "SX_VARIANT must be exact or fast"
@@ -642,7 +643,9 @@ __global__ void positionsKernel(PosArgs a)
         a.vx[i]   = (float)Vn1[0];
         a.vy[i]   = (float)Vn1[1];
         a.vz[i]   = (float)Vn1[2];
+        if (a.keys) a.keys[i] = sfcKey(Xn[0], Xn[1], Xn[2], b);
     }
+    else if (a.keys) a.keys[i] = sfcKey(a.x[i], a.y[i], a.z[i], b);
     double u_old = (double)a.constCv * a.temp[i];
     double du = a.du[i], du_m1 = (double)a.du_m1[i];
     double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;

@@ -150,6 +150,8 @@ struct PosArgs
     float*        du_m1;
     const float*  h;
     float         constCv;
+    // nullable: the next sync's SFC keys of the updated coordinates (sfcKey, box `box`), written in the same pass
+    uint64_t*     keys;
 };
 
 struct HydroLaunch

@@ -936,12 +936,22 @@ findNeighborsKernel(NsArgs a)
     uint32_t ucnt = 0;
     if (local && !abandoned)
     {
-        const uint32_t nw  = (s_cOff[numCand] + 31) / 32;
-        const uint32_t per = (nw + kCluster - 1) / kCluster; // words per thread, consecutive
-        const uint32_t w0  = min(nw, threadIdx.x * per), w1 = min(nw, w0 + per);
-        uint32_t       sum = 0;
-        for (uint32_t w = w0; w < w1; ++w)
-            sum += __popc(s_bits[w]);
+        // every thread takes a run of B consecutive candidate bits (not whole words: ~100 words for 256 threads
+        // left most threads idle and gave the others 32-bit serial chains)
+        const uint32_t nbits = s_cOff[numCand];
+        const uint32_t B     = (nbits + kCluster - 1) / kCluster;
+        const uint32_t b0 = min(nbits, threadIdx.x * B), b1 = min(nbits, b0 + B);
+        const uint32_t wb = b0 >> 5, we = b1 > b0 ? ((b1 - 1) >> 5) + 1 : wb; // words touched: [wb, we)
+        auto           mine = [&](uint32_t w) -> uint32_t { // word w's bits within [b0, b1)
+            uint32_t       v    = s_bits[w];
+            const uint32_t base = w * 32;
+            if (b0 > base) v &= ~0u << (b0 - base);
+            if (b1 < base + 32) v &= (1u << (b1 - base)) - 1u;
+            return v;
+        };
+        uint32_t sum = 0;
+        for (uint32_t w = wb; w < we; ++w)
+            sum += __popc(mine(w));
         // workgroup exclusive scan of the per-thread sums
         uint32_t incl = sum;
 #pragma unroll
@@ -957,30 +967,31 @@ findNeighborsKernel(NsArgs a)
             off += s_wsum[w];
         for (int w = 0; w < kClusterWaves; ++w)
             ucnt += s_wsum[w];
+        // per-word prefix (bitRank): set by the thread whose run holds the word's first bit
         uint32_t run = off + incl - sum;
-        for (uint32_t w = w0; w < w1; ++w)
+        for (uint32_t w = wb; w < we; ++w)
         {
-            s_pre[w] = run;
-            run += __popc(s_bits[w]);
+            if (w * 32 >= b0) s_pre[w] = run;
+            run += __popc(mine(w));
         }
         // union entries: candidate index -> global index, through the leaf it belongs to
         uint32_t* uni = a.uni + (size_t)c * a.ucap;
         run           = off + incl - sum;
-        // first candidate leaf of this thread's words by binary search (s_cOff ascending), then walk forward
+        // first candidate leaf of this thread's run by binary search (s_cOff ascending), then walk forward
         int cc = 0;
         {
-            int lo = 0, hi = numCand; // last cc with s_cOff[cc] <= w0 * 32
+            int lo = 0, hi = numCand; // last cc with s_cOff[cc] <= b0
             while (lo < hi)
             {
                 const int mid = (lo + hi + 1) >> 1;
-                if (s_cOff[mid] <= w0 * 32) lo = mid;
+                if (s_cOff[mid] <= b0) lo = mid;
                 else hi = mid - 1;
             }
             cc = lo;
         }
-        for (uint32_t w = w0; w < w1; ++w)
+        for (uint32_t w = wb; w < we; ++w)
         {
-            uint32_t bits = s_bits[w];
+            uint32_t bits = mine(w);
             while (bits)
             {
                 const uint32_t idx = w * 32 + __builtin_ctz(bits);

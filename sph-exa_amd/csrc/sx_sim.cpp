@@ -1360,7 +1360,9 @@ void maxAccSq(sx_sim* s, hipStream_t st)
 int localSync(sx_sim* s, hipStream_t st)
 {
     const size_t n = s->n;
-    SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, n, s->dbox, st));
+    // keys written by the last position update (PosArgs::keys) are those of the current coordinates
+    if (!s->keysFresh) SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, n, s->dbox, st));
+    s->keysFresh = false;
     if (int e = sortLocals(s, n, st)) return e;
     SIM_HIP(buildTree(s->work, s->keys, n, s->bucket, s->dbox, s->tree, st));
     s->first = 0;
@@ -1430,6 +1432,7 @@ extern "C"
 
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
+        s->keysFresh  = false;
         s->comm       = sx_comm_transport_internal(c);
         s->commHandle = c;
         return SX_OK;
@@ -1461,6 +1464,7 @@ extern "C"
 
     int sx_sim_init_sedov_rank(sx_sim* s, uint32_t side, int rank, int size)
     {
+        s->keysFresh = false;
         size_t N  = (size_t)side * side * side;
         size_t f  = N * rank / size, l = N * (rank + 1) / size;
         size_t n  = l - f;
@@ -1493,6 +1497,7 @@ extern "C"
                          const float* x_m1, const float* y_m1, const float* z_m1, const float* du_m1,
                          const float* alpha, const uint64_t* id, double minDt, double minDt_m1)
     {
+        s->keysFresh = false;
         if (n > s->cap) return SX_ERR_ARG;
         if (s->p.propagator == 2)
         {   // ve-bdt carries the rung in the id's top byte through the particle exchange (PRec): ids must fit 56 bits
@@ -1991,7 +1996,10 @@ extern "C"
         qa.du_m1   = s->dum1;
         qa.h       = s->h;
         qa.constCv = idealGasCv(s->p.muiConst, s->p.gamma);
+        // one rank: the next localSync's keys come from this pass (the coordinates are in registers here)
+        qa.keys    = (!dist && s->p.propagator != 2) ? s->keys : nullptr;
         H.positions(qa, st);
+        s->keysFresh = qa.keys != nullptr;
         H.updateH((uint32_t)s->first, (uint32_t)s->last, s->p.ng0, s->nc, s->h, na.powTab, st);
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
         SIM_HIP(hipGetLastError());

@@ -109,6 +109,8 @@ struct sx_sim
     uint32_t* statsHost;
     int       sortBits{30};          // key bits the local sort orders first (sortLocals)
     bool      gravCount = false; // count the gravity interactions (sx_sim_set_gravity_counting)
+    bool      keysFresh = false; // keys[0, n) hold the current coordinates' SFC keys (set by the position update,
+                                 // consumed by the next localSync; cleared by every entry point that sets state)
     uint64_t  sortStats[4]{0, 0, 0, 0}; // sorts requested, done (not the identity), redone on all bits, moved-only
     Scalars*  sc;
     Scalars*  scHost;

@@ -16,6 +16,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "sx_tree.hpp"
+#include "sx_sfc.hpp"
 
 namespace sx
 {
@@ -59,49 +60,6 @@ __device__ __forceinline__ size_t lowerBound(const uint64_t* a, size_t n, uint64
     return lo;
 }
 
-//! iHilbert<uint64_t> (sfc/hilbert.hpp:60-105), branch-free: per Morton octant one byte of a 64-bit constant holds the
-//! Hilbert digit, the x/y/z reflections and the axis permutation the reference applies at that level (built from the
-//! reference's expressions at compile time), and the digits go straight to their bit positions (32-bit halves).
-//! Checked equal to the reference's loop on 2e7 random coordinates; keys are bit-exact in tests/test_gpu_parity.py.
-__device__ __forceinline__ uint64_t iHilbert(unsigned px, unsigned py, unsigned pz)
-{
-    constexpr uint64_t T = [] {
-        constexpr unsigned m2h[8] = {0, 1, 3, 2, 7, 6, 4, 5}; // mortonToHilbert
-        uint64_t           t      = 0;
-        for (unsigned o = 0; o < 8; ++o)
-        {
-            const unsigned xi = o >> 2, yi = (o >> 1) & 1u, zi = o & 1u;
-            const unsigned fx = xi & ((!yi) | zi), fy = (xi & (yi | zi)) | (yi & (!zi)), fz = (xi & (!yi) & (!zi)) | (yi & (!zi));
-            const unsigned perm = zi ? 1u : (!yi ? 2u : 0u); // 1: (x,y,z) <- (y,z,x), 2: x <-> z
-            t |= (uint64_t)(m2h[o] | (fx << 3) | (fy << 4) | (fz << 5) | (perm << 6)) << (8 * o);
-        }
-        return t;
-    }();
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int level = kMaxLevel - 1; level >= 0; --level)
-    {
-        const unsigned o = (((px >> level) & 1u) << 2) | (((py >> level) & 1u) << 1) | ((pz >> level) & 1u);
-        const unsigned e = (unsigned)(T >> (8 * o)) & 0xffu;
-        const int      s = 3 * level;
-        if (s >= 32) hi |= (e & 7u) << (s - 32);
-        else
-        {
-            lo |= (e & 7u) << s;
-            if (s > 29) hi |= (e & 7u) >> (32 - s);
-        }
-        px ^= 0u - ((e >> 3) & 1u);
-        py ^= 0u - ((e >> 4) & 1u);
-        pz ^= 0u - ((e >> 5) & 1u);
-        const unsigned perm = e >> 6;
-        const unsigned nx = perm == 1u ? py : (perm == 2u ? pz : px);
-        const unsigned ny = perm == 1u ? pz : py;
-        const unsigned nz = perm == 0u ? pz : px;
-        px = nx, py = ny, pz = nz;
-    }
-    return ((uint64_t)hi << 32) | lo;
-}
-
 //! decodeHilbert<uint64_t> (sfc/hilbert.hpp:145-190)
 __device__ __forceinline__ void decodeHilbert(uint64_t key, unsigned& ox, unsigned& oy, unsigned& oz)
 {
@@ -143,16 +101,7 @@ __global__ void sfcKeysKernel(const double* x, const double* y, const double* z,
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    constexpr unsigned cubeLength = 1u << kMaxLevel;
-    constexpr int      mcoord     = (1 << kMaxLevel) - 1;
-    double             mx = cubeLength * b.il[0], my = cubeLength * b.il[1], mz = cubeLength * b.il[2];
-    int                ix = (int)(floor(x[i] * mx) - b.lim[0] * mx);
-    int                iy = (int)(floor(y[i] * my) - b.lim[2] * my);
-    int                iz = (int)(floor(z[i] * mz) - b.lim[4] * mz);
-    ix                    = ix < mcoord ? ix : mcoord;
-    iy                    = iy < mcoord ? iy : mcoord;
-    iz                    = iz < mcoord ? iz : mcoord;
-    keys[i]               = iHilbert((unsigned)ix, (unsigned)iy, (unsigned)iz);
+    keys[i] = sfcKey(x[i], y[i], z[i], b);
 }
 
 __global__ void iotaKernel(uint32_t* a, size_t n)
