@@ -40,5 +40,7 @@ for name, f in FNS.items():
     for k, p in enumerate(PHASES):
         print(f"  {p:15s} {float(v[k]) / waves / 1e3:10.1f}  ({float(v[k]) / max(1.0, float(v[:8].sum())):.3f})")
     print(f"  {'total':15s} {tot:10.1f}")
+    for k, c in enumerate(["blocks", "streamed", "staged", "chunks", "exact chunks", "test kcycles"]):
+        print(f"  per wave: {c:13s} {float(v[9 + k]) / waves / (1e3 if k == 5 else 1):10.1f}")
 sim.close()
 ctx.close()

@@ -296,6 +296,7 @@ findNeighborsKernel(NsArgs a)
     uint32_t ci = __builtin_amdgcn_readfirstlane(s_next);
 #if SX_NS_PROBE
     unsigned long long prAcc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prT = __builtin_readcyclecounter(), prWaves = 0;
+    unsigned long long prCnt[6] = {0, 0, 0, 0, 0, 0}; // blocks, streamed, staged, chunks, exact chunks, test cycles
 #endif
     while (ci < numClusters)
     {
@@ -696,6 +697,9 @@ findNeighborsKernel(NsArgs a)
 
         // test the fill staged slots of table row nq: hit mask -> count, union bitmap, the batch (or global lists)
         auto testChunk = [&]() {
+#if SX_NS_PROBE
+            const unsigned long long tc0_ = __builtin_readcyclecounter();
+#endif
             const int m = fill;
             candTested += m;
             uint16_t* tq = wl.tab[nq];
@@ -746,6 +750,10 @@ findNeighborsKernel(NsArgs a)
                 }
             }
             if (exact) hm = exactChunk(m, tq);
+#if SX_NS_PROBE
+            prCnt[3]++;
+            prCnt[4] += exact ? 1 : 0;
+#endif
             const uint32_t sd = selfSeq - seq;
             if (sd < (uint32_t)m) hm &= ~(1ull << sd); // j != i
             const unsigned nh = __popcll(hm);
@@ -791,6 +799,9 @@ findNeighborsKernel(NsArgs a)
             seq += m;
             fill = 0;
             __builtin_amdgcn_wave_barrier(); // every lane's slot reads precede the next staging writes
+#if SX_NS_PROBE
+            prCnt[5] += __builtin_readcyclecounter() - tc0_;
+#endif
         };
 
         // blocks of up to 64 consecutive particles of the reachable candidate leaves, in candidate order; the next
@@ -873,6 +884,11 @@ findNeighborsKernel(NsArgs a)
             }
             const uint64_t bm = __ballot(pass);
             const int      n  = __popcll(bm);
+#if SX_NS_PROBE
+            prCnt[0]++;
+            prCnt[1] += __popcll(__ballot(in));
+            prCnt[2] += n;
+#endif
             if (fill + n > kWave) testChunk();
             if (pass)
             {
@@ -1091,6 +1107,8 @@ findNeighborsKernel(NsArgs a)
         for (int k = 0; k < 8; ++k)
             atomicAdd(&g_nsProbe[k], prAcc[k]);
         atomicAdd(&g_nsProbe[8], prWaves);
+        for (int k = 0; k < 6; ++k)
+            atomicAdd(&g_nsProbe[9 + k], prCnt[k]);
     }
 #endif
 }

@@ -663,82 +663,116 @@ double quantMargin(const DevBox& b)
  *  - else a stable radix sort of the top sortBits key bits, accepted when the result is ascending in the full keys
  *    (then keys equal in the sorted bits kept their input order AND that order is ascending in the lower bits, which
  *    is what the full stable sort gives); otherwise the full sort, and more bits from the next step on.
- *  Lattice-like states separate every particle within the top 10 levels (30 bits), so 4 of the 8 radix passes. */
+ *  Lattice-like states separate every particle within the top 10 levels (30 bits), so 4 of the 8 radix passes.
+ *  Up to 32 bits the sort moves 32-bit keys (the top bits, extracted by the descent count) and an implicit identity
+ *  permutation: 8 instead of 12 bytes per element and pass; the full keys are then reordered with the other fields
+ *  (only the moved positions), instead of being copied back from the sort's output. */
 int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
 {
-    uint32_t* cnt  = s->work.get<uint32_t>("sort.desc", 1);
-    uint32_t* cntH = s->work.pinned<uint32_t>("sort.desch", 1);
-    auto descents = [&](const uint64_t* k, uint32_t& out) -> int {
-        SIM_HIP(hipMemsetAsync(cnt, 0, 4, st));
-        SIM_HIP(countDescents(k, nl, cnt, st));
-        SIM_HIP(hipMemcpyAsync(cntH, cnt, 4, hipMemcpyDeviceToHost, st));
+    uint32_t* cnt  = s->work.get<uint32_t>("sort.desc", 2);
+    uint32_t* cntH = s->work.pinned<uint32_t>("sort.desch", 2);
+    auto      read = [&]() -> int {
+        SIM_HIP(hipMemcpyAsync(cntH, cnt, 8, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
-        out = *cntH;
         return SX_OK;
     };
-    uint32_t d = 0;
-    if (int e = descents(s->keys, d)) return e;
+    const int bits = std::clamp(s->sortBits, 1, 63);
+    uint32_t* top  = bits <= 32 ? s->work.get<uint32_t>("sort.top", nl) : nullptr;
+    SIM_HIP(hipMemsetAsync(cnt, 0, 8, st));
+    if (top) SIM_HIP(countDescentsTop(s->keys, nl, 63 - bits, top, cnt, st));
+    else SIM_HIP(countDescents(s->keys, nl, cnt, st));
+    if (int e = read()) return e;
     s->sortStats[0]++;
-    if (d == 0) return SX_OK;
-    hipError_t he   = hipSuccess;
-    const int  bits = std::clamp(s->sortBits, 1, 63);
-    uint64_t*  kOut = sortKeysBits(s->work, s->keys, s->order, nl, 63 - bits, st, he);
-    SIM_HIP(he);
-    if (bits < 63)
+    if (cntH[0] == 0) return SX_OK;
+    hipError_t he          = hipSuccess;
+    bool       permuteKeys = false; // the order is final and the keys are reordered with the fields
+    uint32_t   moved       = 0;
+    if (top)
     {
-        if (int e = descents(kOut, d)) return e;
-        if (d)
+        SIM_HIP(sortTopBits(s->work, top, s->order, nl, bits, st));
+        SIM_HIP(hipMemsetAsync(cnt, 0, 8, st));
+        SIM_HIP(checkSorted(s->keys, s->order, nl, cnt, st));
+        if (int e = read()) return e;
+        permuteKeys = cntH[0] == 0;
+        moved       = cntH[1];
+    }
+    if (!permuteKeys)
+    {
+        uint64_t* kOut = nullptr;
+        if (!top && bits < 63)
+        {
+            kOut = sortKeysBits(s->work, s->keys, s->order, nl, 63 - bits, st, he);
+            SIM_HIP(he);
+            SIM_HIP(hipMemsetAsync(cnt, 0, 8, st));
+            SIM_HIP(countDescents(kOut, nl, cnt, st));
+            if (int e = read()) return e;
+            if (cntH[0]) kOut = nullptr;
+        }
+        if (!kOut)
         {
             kOut = sortKeysBits(s->work, s->keys, s->order, nl, 0, st, he);
             SIM_HIP(he);
-            s->sortBits = std::min(63, bits + 9);
-            s->sortStats[2]++;
+            if (bits < 63)
+            {
+                s->sortBits = std::min(63, bits + 9);
+                s->sortStats[2]++;
+            }
         }
+        SIM_HIP(hipMemcpyAsync(s->keys, kOut, nl * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+        SIM_HIP(hipMemsetAsync(cnt, 0, 8, st));
+        SIM_HIP(movedCount(s->order, nl, cnt, st));
+        if (int e = read()) return e;
+        moved = cntH[0];
     }
     s->sortStats[1]++;
-    SIM_HIP(hipMemcpyAsync(s->keys, kOut, nl * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     // a nearly stationary state moves few positions per step (Sedov 64M: ~10 %): then only those are rewritten, in
     // place (read into a scratch copy, then written back), instead of gathering every field into its spare buffer
+    if (moved <= nl / 4)
     {
-        SIM_HIP(hipMemsetAsync(cnt, 0, 4, st));
-        SIM_HIP(movedCount(s->order, nl, cnt, st));
-        SIM_HIP(hipMemcpyAsync(cntH, cnt, 4, hipMemcpyDeviceToHost, st));
-        SIM_HIP(hipStreamSynchronize(st));
-        if (*cntH <= nl / 4)
-        {
-            size_t colBytes = 0;
-            for (auto& sp : s->spares)
-                colBytes += ((size_t)nl * sp.elemBytes + 255) & ~size_t(255);
-            char*     tmp = s->work.get<char>("sort.movedtmp", colBytes);
-            GatherSet set{};
-            for (auto& sp : s->spares)
+        size_t colBytes = permuteKeys ? ((size_t)nl * sizeof(uint64_t) + 255) & ~size_t(255) : 0;
+        for (auto& sp : s->spares)
+            colBytes += ((size_t)nl * sp.elemBytes + 255) & ~size_t(255);
+        char*     tmp = s->work.get<char>("sort.movedtmp", colBytes);
+        GatherSet set{};
+        auto      add = [&](void* field, int bytes) -> int {
+            if (set.count == kMaxGatherFields)
             {
-                if (set.count == kMaxGatherFields)
-                {
-                    SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
-                    set.count = 0;
-                }
-                set.src[set.count] = *sp.field, set.dst[set.count] = *sp.field, set.bytes[set.count] = sp.elemBytes;
-                ++set.count;
+                SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
+                set.count = 0;
             }
-            SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
-            s->sortStats[3]++;
+            set.src[set.count] = field, set.dst[set.count] = field, set.bytes[set.count] = bytes;
+            ++set.count;
             return SX_OK;
-        }
+        };
+        if (permuteKeys)
+            if (int e = add(s->keys, sizeof(uint64_t))) return e;
+        for (auto& sp : s->spares)
+            if (int e = add(*sp.field, sp.elemBytes)) return e;
+        SIM_HIP(permuteMoved(s->order, nl, set, tmp, st));
+        s->sortStats[3]++;
+        return SX_OK;
     }
     GatherSet set{};
-    for (auto& sp : s->spares)
-    {
+    auto      add = [&](const void* src, void* dst, int bytes) -> int {
         if (set.count == kMaxGatherFields)
         {
             SIM_HIP(gatherMany(s->order, nl, set, st));
             set.count = 0;
         }
-        set.src[set.count] = *sp.field, set.dst[set.count] = sp.alt, set.bytes[set.count] = sp.elemBytes;
+        set.src[set.count] = src, set.dst[set.count] = dst, set.bytes[set.count] = bytes;
         ++set.count;
+        return SX_OK;
+    };
+    uint64_t* kOut = permuteKeys ? s->work.get<uint64_t>("sort.kout", nl) : nullptr;
+    if (kOut)
+        if (int e = add(s->keys, kOut, sizeof(uint64_t))) return e;
+    for (auto& sp : s->spares)
+    {
+        if (int e = add(*sp.field, sp.alt, sp.elemBytes)) return e;
         std::swap(*sp.field, sp.alt);
     }
     SIM_HIP(gatherMany(s->order, nl, set, st));
+    if (kOut) SIM_HIP(hipMemcpyAsync(s->keys, kOut, nl * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     return SX_OK;
 }
 

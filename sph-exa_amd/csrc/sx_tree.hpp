@@ -257,6 +257,12 @@ hipError_t sortKeys(Arena& arena, uint64_t* keys, uint32_t* order, size_t n, hip
 hipError_t countDescents(const uint64_t* keys, size_t n, uint32_t* out, hipStream_t s);
 uint64_t*  sortKeysBits(Arena& arena, const uint64_t* keys, uint32_t* order, size_t n, int beginBit, hipStream_t s,
                         hipError_t& e);
+//! countDescents, and top[i] = keys[i] >> shift in the same pass
+hipError_t countDescentsTop(const uint64_t* keys, size_t n, int shift, uint32_t* top, uint32_t* out, hipStream_t s);
+//! stable radix sort of the 32-bit keys top on bits [0, bits): order = the permutation (values 0..n-1)
+hipError_t sortTopBits(Arena& arena, const uint32_t* top, uint32_t* order, size_t n, int bits, hipStream_t s);
+//! out[0] += descents of keys[order[i]] over i, out[1] += positions with order[i] != i
+hipError_t checkSorted(const uint64_t* keys, const uint32_t* order, size_t n, uint32_t* out, hipStream_t s);
 hipError_t gather(const uint32_t* order, size_t n, const void* src, void* dst, int elemBytes, hipStream_t s);
 //! up to kMaxGatherFields fields of 4 or 8 bytes reordered by one kernel (the index is read once per particle)
 constexpr int kMaxGatherFields = 16;

@@ -297,6 +297,44 @@ def test_full_steps_vs_oracle(ctx, ora, ic, side, steps):
     run_checked_steps(ctx, ora, st, obox, steps).close()
 
 
+@pytest.mark.parametrize("pairs", [0, 24])
+def test_local_sort_order(ctx, ora, pairs):
+    """the step's local sort (sortLocals) orders the particles exactly like the reference's stable sort of the full
+    keys (Domain::sync): a shuffled lattice (every position moves: the gather path), then two more steps (few moves:
+    the in-place path).  With `pairs` particles moved next to others (the same level-10 cell, so their top 30 key
+    bits tie) in shuffled order, the 32-bit sort of the top bits leaves descents in the low bits and the full sort
+    must take over."""
+    st, obox = po.sedov_state(16)
+    rng = np.random.default_rng(11)
+    perm = rng.permutation(st.n)
+    for k in po.CONSERVED:
+        st.arrays[k][:] = st.arrays[k][perm]
+    if pairs:
+        src = rng.choice(st.n, pairs, replace=False)
+        dst = rng.choice(np.setdiff1d(np.arange(st.n), src), pairs, replace=False)
+        for d, s in zip(dst, src):
+            for c, off in zip(("x", "y", "z"), (1.5e-4, 2.5e-4, 3.5e-4)):
+                st.arrays[c][d] = st.arrays[c][s] + off
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    conserved = list(gutil.StepChecker.CONSERVED)
+    cur = {k: st.arrays[k].copy() for k in conserved}
+    for step in range(3):
+        hs = po.HostState(st.n)
+        for k in conserved:
+            hs.arrays[k][:] = cur[k]
+        keys = ora.sfc_keys(hs, obox).copy()
+        expect = cur["id"][np.argsort(keys, kind="stable")]
+        if pairs and step == 0:
+            top = keys >> np.uint64(33)
+            o = np.argsort(top, kind="stable")
+            assert np.any(np.diff(keys[o].astype(np.int64)) < 0)  # the top-bit order alone is not the answer
+        sim.step()
+        cur = sim.get(conserved)
+        assert np.array_equal(cur["id"], expect), step
+    sim.close()
+
+
 def test_golden_fixture_steps(ctx, ora):
     """the oracle reproduces the reference's own steps (sedov10.npz, from oracle/_ref) bit for bit, and the GPU's
     steps from the fixture state are checked per particle against it"""
