@@ -98,6 +98,9 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     const uint32_t nw = (cu.cnt + 1) >> 1;
     cu.wBeg           = nw * cu.part / SPLIT;
     cu.wEnd           = nw * (cu.part + 1) / SPLIT;
+#ifdef SX_PAIR_NOLOOP
+    cu.wEnd = cu.wBeg; // measurement builds only: setup, staging and output without the neighbor loops
+#endif
     cu.U              = a.ucount[cu.c];
     cu.un             = a.uni + (size_t)cu.c * a.ucap;
     cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
@@ -166,12 +169,21 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             const uint32_t u = b0 + threadIdx.x + s * NT;
             js[s]            = u < b1 ? cu.un[u] : 0u;
         }
+#ifndef SX_PAIR_NOSTAGE
 #pragma unroll
         for (int s = 0; s < S; ++s)
         {
             const uint32_t u = b0 + threadIdx.x + s * NT;
             if (u < b1) stage(js[s], u - b0);
         }
+#else
+        // measurement builds only: the union indices are read, no record is gathered or staged
+        uint32_t x = 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            x ^= js[s];
+        asm volatile("" ::"v"(x));
+#endif
     };
 
     if (cu.U <= (uint32_t)CH)
@@ -1008,6 +1020,9 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         const uint32_t nw = (cu.cnt + 1) >> 1;
         cu.wBeg           = nw * cu.part / SPLIT;
         cu.wEnd           = nw * (cu.part + 1) / SPLIT;
+#ifdef SX_PAIR_NOLOOP
+        cu.wEnd = cu.wBeg;
+#endif
         cu.U              = cur.U;
         cu.un             = a.uni + (size_t)cu.c * a.ucap;
         cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
