@@ -69,6 +69,9 @@ struct PairArgs
     // AV switches rtOut = the target's record with the new alpha
     RecT* rtOut;
     RecC* rcOut;
+    // cluster kernels, 0 = unknown: an upper bound of every cluster's union size (the search's statistics, read by
+    // the host once the search has finished); AV switches skips its large-union launch when no union needs it
+    uint32_t unionMax;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent

@@ -1508,7 +1508,8 @@ void avSwitches(const PairArgs& a, hipStream_t s)
 {
     if (!a.numGroups || !clusters(a)) return;
     avSwitchesKernel<kChAv, SX_SPLIT_AV, 0, kChAv><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
-    avSwitchesKernel<kChAvLarge, SX_SPLIT_AV, kChAv + 1, 0><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
+    if (a.unionMax == 0 || a.unionMax > (uint32_t)kChAv) // else every workgroup of it would exit after one load
+        avSwitchesKernel<kChAvLarge, SX_SPLIT_AV, kChAv + 1, 0><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
 }
 //! min over the per-workgroup Courant time-steps of one launch -> *minDt (one atomic)
 __global__ __launch_bounds__(1024) void reduceBlockDtKernel(const float* v, uint32_t n, float* minDt)

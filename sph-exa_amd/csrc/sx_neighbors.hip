@@ -1197,27 +1197,31 @@ size_t     searchScratchWords();
 
 size_t searchScratchBytes() { return std::max(searchScratchWords(), small::searchScratchWords()) * sizeof(uint64_t); }
 
-//! per-cluster statistics -> stats[2] (max count), u64 stats[4] (stored), [6] (tested), [8] (union entries)
+//! per-cluster statistics -> stats[2] (max count), u64 stats[4] (stored), [6] (tested), [8] (union entries),
+//! stats[12] (largest union)
 __global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
 {
-    __shared__ uint32_t           s_max[16];
+    __shared__ uint32_t           s_max[2][16];
     __shared__ unsigned long long s_sum[3][16];
-    uint32_t                      mx = 0;
+    uint32_t                      mx = 0, mu = 0;
     unsigned long long            st = 0, te = 0, un = 0;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     {
         const uint4 v = cl[i];
-        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w;
+        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w, mu = max(mu, v.w);
     }
-    mx = waveMax(mx), st = waveSum(st), te = waveSum(te), un = waveSum(un);
+    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un);
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) s_max[w] = mx, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
+    if ((threadIdx.x & 63) == 0)
+        s_max[0][w] = mx, s_max[1][w] = mu, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
     __syncthreads();
     if (threadIdx.x == 0)
     {
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            mx = max(mx, s_max[k]), st += s_sum[0][k], te += s_sum[1][k], un += s_sum[2][k];
+            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), st += s_sum[0][k], te += s_sum[1][k],
+            un += s_sum[2][k];
         stats[2]                                            = mx;
+        stats[12]                                           = mu;
         *reinterpret_cast<unsigned long long*>(stats + 4) = st;
         *reinterpret_cast<unsigned long long*>(stats + 6) = te;
         *reinterpret_cast<unsigned long long*>(stats + 8) = un;

@@ -1444,6 +1444,7 @@ extern "C"
         if (hipStreamCreateWithFlags(&s->commStream, hipStreamNonBlocking) != hipSuccess) s->commStream = nullptr;
         (void)hipEventCreateWithFlags(&s->evProd, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evComm, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&s->evStats, hipEventDisableTiming);
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
@@ -1460,6 +1461,7 @@ extern "C"
             (void)hipEventDestroy(e);
         if (s->evProd) (void)hipEventDestroy(s->evProd);
         if (s->evComm) (void)hipEventDestroy(s->evComm);
+        if (s->evStats) (void)hipEventDestroy(s->evStats);
         if (s->commStream) (void)hipStreamDestroy(s->commStream);
         delete s;
     }
@@ -1769,6 +1771,7 @@ extern "C"
             SIM_HIP(findNeighbors(na, st));
             SIM_HIP(hipEventRecord(s->kev[1], st));
             SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
+            if (s->evStats) SIM_HIP(hipEventRecord(s->evStats, st));
             if (!dist) break;
             // halo sufficiency: every local particle's final h within its chunk's request margin
             const size_t nl  = s->last - s->first;
@@ -1932,6 +1935,9 @@ extern "C"
                         PairArgs q = p;
                         q.rcOut    = nullptr;
                         q.rtOut    = fused ? s->rt : nullptr; // AV writes the locals' records with the new alpha
+                        // the largest union of this step's search: the host waits here for the search to finish
+                        // (long done on the device when the kernels queued before AV still run, so nothing idles)
+                        if (s->evStats && hipEventSynchronize(s->evStats) == hipSuccess) q.unionMax = s->statsHost[12];
                         H.avSwitches(q, st);
                     },
                     pa, st))

@@ -135,6 +135,7 @@ struct sx_sim
     bool        overlap{true};
     hipStream_t commStream{nullptr};
     hipEvent_t  evProd{nullptr}, evComm{nullptr};
+    hipEvent_t  evStats{nullptr}; // the search's statistics have reached statsHost
     uint32_t*   clsList{nullptr}; // [interior | boundary] cluster indices (2 x numClusters)
     uint32_t*   clsCount{nullptr};
     uint32_t*   clsHost{nullptr}; // pinned copy of clsCount
