@@ -176,7 +176,7 @@ typedef struct sx_nbstats
     uint64_t sumCandidates;  /* candidate particles tested (per target, summed) */
     uint64_t sumUnion;       /* cluster neighbor-union entries, summed over 256-particle clusters */
     uint32_t build;          /* search build used: 0 compact, 1 large, 2 compact overflowed and redone by the large */
-    uint32_t reserved;
+    uint32_t maxUnion;       /* largest cluster neighbor union (local lists; 0 otherwise) */
 } sx_nbstats;
 
 typedef struct sx_ctx sx_ctx;

@@ -455,7 +455,7 @@ extern "C"
             stats->sumCandidates = *reinterpret_cast<uint64_t*>(c->statsHost + 6);
             stats->sumUnion      = *reinterpret_cast<uint64_t*>(c->statsHost + 8);
             stats->build         = c->nsPolicy.lastBuild;
-            stats->reserved      = 0;
+            stats->maxUnion      = c->statsHost[12];
         }
         if (c->statsHost[0] & 1u) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in neighbor search");
         if (iterate_h && c->statsHost[1]) return fail(c, SX_ERR_NOT_CONVERGED, "coupled nc/h-updated failed to converge");

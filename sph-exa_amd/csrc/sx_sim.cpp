@@ -2054,6 +2054,7 @@ extern "C"
         s->lastStats.sumNeighbors  = *reinterpret_cast<uint64_t*>(s->statsHost + 4);
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
+        s->lastStats.maxUnion      = s->statsHost[12];
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         s->lastStats.build         = s->nsPolicy.lastBuild;
         if (s->statsHost[0] & 1u)

@@ -75,7 +75,7 @@ class SxOctree(C.Structure):
 class SxNbStats(C.Structure):
     _fields_ = [("sumNeighbors", C.c_uint64), ("maxNeighbors", C.c_uint32), ("numFailed", C.c_uint32),
                 ("sumCandidates", C.c_uint64), ("sumUnion", C.c_uint64), ("build", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("maxUnion", C.c_uint32)]
 
 
 # field dtypes (sph::SphTypes, sph/types.hpp:39-46)
@@ -661,7 +661,7 @@ class Sim:
         s = SxNbStats()
         self.L.sx_sim_last_stats(self.h, C.byref(s))
         return dict(sumNeighbors=s.sumNeighbors, maxNeighbors=s.maxNeighbors, numFailed=s.numFailed,
-                    sumCandidates=s.sumCandidates, sumUnion=s.sumUnion, build=s.build)
+                    sumCandidates=s.sumCandidates, sumUnion=s.sumUnion, build=s.build, maxUnion=s.maxUnion)
 
     def conserved(self):
         """computeConservedQuantities over all ranks (sx_sim_conserved)"""

@@ -335,6 +335,17 @@ def test_local_sort_order(ctx, ora, pairs):
     sim.close()
 
 
+def test_large_union_step(ctx, ora):
+    """h 15 % above the lattice's (~140 neighbors): cluster unions beyond AV switches' three-workgroup capacity (1470
+    records), so the step needs AV's large-union launch, which the step skips only when the search's largest union
+    fits; the step is checked per particle against the oracle (alpha is AV's output)"""
+    st, obox = po.sedov_state(24)
+    st.h[:] *= np.float32(1.15)
+    sim = run_checked_steps(ctx, ora, st, obox, 1)
+    assert sim.stats()["maxUnion"] > 1470
+    sim.close()
+
+
 def test_golden_fixture_steps(ctx, ora):
     """the oracle reproduces the reference's own steps (sedov10.npz, from oracle/_ref) bit for bit, and the GPU's
     steps from the fixture state are checked per particle against it"""
