@@ -377,6 +377,10 @@ findNeighborsKernel(NsArgs a)
         if (!final) nEarly = stored;
         nq  = 0;
         nzq = 0;
+        // the last (unused) next-mask load completes here: left outstanding, its registers are reused by the stream's
+        // staging code, and the wait the compiler must then put there (vmcnt(0), on every path through the merge)
+        // would also wait for the next block's prefetched coordinates
+        __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
         __builtin_amdgcn_wave_barrier(); // table reads precede the next chunk's staging writes
     };
 
@@ -683,6 +687,9 @@ findNeighborsKernel(NsArgs a)
                 }
                 if (valid && (dx * dx + dy * dy + dz * dz < radSq)) hm |= 1ull << k;
             }
+            // the coordinate loads complete inside this rare path (m = 0 skips the loop): otherwise their registers,
+            // reused by the common path, make it wait for every outstanding load, the next block's prefetch included
+            __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
             return hm;
         };
 
