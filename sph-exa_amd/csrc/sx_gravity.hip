@@ -496,14 +496,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             }
             return false;
         };
-        float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
-        float  ph = 0.f;
+        // the next chunk's sources stay raw (double coordinates) until they are staged: a conversion right after
+        // the loads would wait for them there, before the current chunk's evaluation they are meant to overlap
+        double px = 0.0, py = 0.0, pz = 0.0;
+        float  pm = 0.f, ph = 0.f;
         auto   loadRegs = [&]() {
             if ((uint32_t)lane < jn)
             {
                 const uint32_t j = js + lane;
-                pv = make_float4((float)(a.x[j] - ox), (float)(a.y[j] - oy), (float)(a.z[j] - oz), a.m[j]);
-                ph = a.h[j];
+                px = a.x[j], py = a.y[j], pz = a.z[j], pm = a.m[j], ph = a.h[j];
             }
         };
         bool have = nextChunk();
@@ -524,8 +525,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const bool  in = (uint32_t)lane < cn;
                     const int   P = (lane >> 3) * 4 + (lane & 3), hf = (lane >> 2) & 1;
                     float*      d = reinterpret_cast<float*>(&s_srcF[wave][buf][0]) + P * 8 + hf;
-                    d[0] = in ? pv.x : 1e18f, d[2] = in ? pv.y : 1e18f, d[4] = in ? pv.z : 1e18f;
-                    d[6] = in ? pv.w : 0.0f;
+                    d[0] = in ? (float)(px - ox) : 1e18f, d[2] = in ? (float)(py - oy) : 1e18f;
+                    d[4] = in ? (float)(pz - oz) : 1e18f, d[6] = in ? pm : 0.0f;
                     s_hF[wave][buf][P * 2 + hf] = in ? ph : 0.0f;
                 }
             }
