@@ -959,6 +959,9 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         Pre p;
         p.c = c;
         p.U = 0, p.nc = 1, p.act = 1;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            p.js[s] = 0u;
         if (c == kNone) return p;
         const uint32_t c0 = __builtin_amdgcn_readfirstlane(a.first + c * kCluster), i = c0 + tid;
         const bool     in = c * kClusterWaves + sub < a.numGroups && i < a.last;
@@ -982,15 +985,16 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         }
         return p;
     };
-    // every slot is assigned (zeros where nothing is staged), so the records are dead between staging and reload
+    // every slot is loaded (particle 0's records where nothing is staged): a load under a branch is merged with the
+    // branch's alternative right after it, and that merge waited for the load there -- before the share combination
+    // it is meant to overlap -- instead of at the next cluster's staging
     auto loadRecords = [&](const Pre& p, MeRaw<AVC> (&rr)[SP]) {
         const bool use = p.c != kNone && p.U <= (uint32_t)CH;
 #pragma unroll
         for (int s = 0; s < SP; ++s)
         {
-            MeRaw<AVC> r{};
-            if (use && threadIdx.x + s * NT < p.U) r = meLoadRaw<AVC>(a, p.js[s]);
-            rr[s] = r;
+            const bool ok = use && threadIdx.x + s * NT < p.U;
+            rr[s]         = meLoadRaw<AVC>(a, ok ? p.js[s] : 0u);
         }
     };
 
