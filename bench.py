@@ -47,8 +47,8 @@ EDGE_MODEL = {"findNeighbors": (32, 28), "xmass": (44, 32), "veDefGradh": (48, 3
               "avSwitches": (88, 52), "momentumEnergy": (108, 92)}
 # compulsory (unique-field) HBM bytes per target as implemented: packed own records + outputs, plus
 # 2 B per stored neighbor (u16 union positions) and 4 B per union entry; the search reads x,y,z,h (28 B) and the
-# tree, writes h, nc and the lists
-COMPULSORY_OWN = {"findNeighbors": 28 + 8, "xmass": 32 + 4 + 4, "veDefGradh": 48 + 4 + 8,
+# tree, writes h, nc, the lists and the targets' 32-B RecX records (NsArgs::rxOut)
+COMPULSORY_OWN = {"findNeighbors": 28 + 8 + 32, "xmass": 32 + 4 + 4, "veDefGradh": 48 + 4 + 8,
                   "iadDivvCurlv": 80 + 4 + 28, "avSwitches": 96 + 4 + 4, "momentumEnergy": 96 + 4 + 20}
 # kernel-time slot -> rocprofv3 kernel-name fragments it launches (sx_sim.cpp kev slots)
 PMC_KERNELS = {"findNeighbors": ("findNeighborsKernel", "leafFrameKernel"), "xmass": ("xmassKernel",),
@@ -147,6 +147,8 @@ def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
         r["traffic"] = r["achieved"] = r["frac"] = None
     if c and "SQ_INSTS_VALU" in c:
         r["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (ms * 1e-3 * VALU_ISSUE_PEAK)
+        if slot in FLOP_PER_PAIR:  # lane-instructions per neighbor pair (wave64 instructions x 64 / pairs)
+            r["valu_lane_ops_per_pair"] = c["SQ_INSTS_VALU"] * 64 / max(1.0, n_local * ng)
     if c and "SQ_LDS_BANK_CONFLICT" in c:
         r["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / NUM_CU / (ms * 1e-3 * CLOCK_HZ)
     if c and "profiled_ms" in c:
@@ -167,7 +169,9 @@ def gravity_roofline(ms, n_local, inter, pmc):
     flop_ref = GRAV_FLOP_REF[0] * p2p + GRAV_FLOP_REF[1] * m2p
     r = {"avg_launch_ms": ms, "p2p_per_target": p2p / max(1, n_local), "m2p_per_target": m2p / max(1, n_local),
          "tflops": flop_impl / (ms * 1e-3) / 1e12, "tflops_reference_model": flop_ref / (ms * 1e-3) / 1e12}
-    r["flop_frac"] = r["tflops"] / FP32_PEAK_TFLOPS
+    # headline: the reference's own flop accounting (traversal.cuh:632); the implementation's count is secondary
+    r["flop_frac"] = r["tflops_reference_model"] / FP32_PEAK_TFLOPS
+    r["flop_frac_impl_model"] = r["tflops"] / FP32_PEAK_TFLOPS
     c = pmc_slot(pmc, "gravity")
     if c and "SQ_INSTS_VALU" in c:
         r["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (ms * 1e-3 * VALU_ISSUE_PEAK)
@@ -361,14 +365,14 @@ def main():
     dom = per_kernel.get(dominant, {})
     grav_dom = dominant == "gravity"
     roofline = {"bound": "valu" if grav_dom else "hbm", "kernel": dominant,
-                "achieved": dom.get("tflops") if grav_dom else dom.get("achieved"),
+                "achieved": dom.get("tflops_reference_model") if grav_dom else dom.get("achieved"),
                 "peak": FP32_PEAK_TFLOPS if grav_dom else HBM_PEAK_GBS,
                 "unit": "TFLOP/s" if grav_dom else "GB/s",
                 "frac": dom.get("flop_frac") if grav_dom else dom.get("frac"), "traffic": dom.get("traffic"),
                 "avg_launch_ms": dom.get("avg_launch_ms"),
                 "share_of_step": dom.get("avg_launch_ms", 0.0) / ms_step,
                 "binding": ("FP32 VALU / latency: flop roofline from the per-target P2P/M2P counts (see "
-                            "tflops_reference_model, valu_issue_frac, hbm_frac)" if grav_dom else
+                            "tflops (this kernel's own count), valu_issue_frac, hbm_frac)" if grav_dom else
                             "valu-issue/latency (HBM frac < 0.5; see valu_issue_frac, lds_conflict_frac)"
                             if (dom.get("frac") or 0) < 0.5 else "hbm"),
                 "traffic_source": os.path.relpath(pmc_file(pmc_key), ROOT) if pmc else None,
@@ -381,13 +385,16 @@ def main():
                               "valu_issue_frac = SQ_INSTS_VALU / (time x 1.23e12 wave64 ops/s: 2 cycles per "
                               "instruction per SIMD-32 at 2.4 GHz, the chip's rate; one wave alone issues at most "
                               "half of it, profiles/r4_issue_calib.jsonl); valu_frac = SURVEY 8(d) flop "
-                              "per pair x pairs / time / 157.3 TF (FP32 peak at 2.4 GHz); gravity: flop_frac = "
-                              "(23 P2P + 54 M2P) / time / 157.3 TF; lds_conflict_frac = "
+                              "per pair x pairs / time / 157.3 TF (FP32 peak at 2.4 GHz); gravity: achieved and "
+                              "flop_frac = the reference's accounting (traversal.cuh:632: 20 per P2P + 16 per M2P) / "
+                              "time / 157.3 TF, flop_frac_impl_model = this kernel's (23 P2P + 54 M2P); "
+                              "lds_conflict_frac = "
                               "SQ_LDS_BANK_CONFLICT / 256 CUs / (time x 2.4 GHz); effective_gbs = SURVEY 8(d) edge "
                               "model (neighbor records served from LDS/L2, not a roofline)",
                 **{k: dom[k] for k in ("valu_issue_frac", "lds_conflict_frac", "effective_gbs",
                                        "algorithmic_bytes_per_launch", "algorithmic_frac", "hbm_frac",
-                                       "tflops_reference_model", "p2p_per_target", "m2p_per_target") if k in dom},
+                                       "tflops", "flop_frac_impl_model", "p2p_per_target", "m2p_per_target",
+                                       "valu_lane_ops_per_pair") if k in dom},
                 "per_kernel": per_kernel}
     st_bytes = step_traffic(pmc)
     if st_bytes:

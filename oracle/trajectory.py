@@ -18,12 +18,16 @@ import numpy as np
 import pyoracle as po
 
 
-def eos_rho_p(f, mui=np.float32(10.0), gamma=5.0 / 3.0):
-    """rho = kx*m/xm (float), p = rho * (cv*T*(gamma-1)) (idealGasEOS, sph/eos.hpp:31-40: double since T is double)"""
-    kx = np.asarray(f["kx"], np.float32)
-    m = np.asarray(f["m"], np.float32)
-    xm = np.asarray(f["xm"], np.float32)
-    rho = (kx * m / xm).astype(np.float32)
+def eos_rho_p(f, mui=np.float32(10.0), gamma=5.0 / 3.0, std=False):
+    """rho = kx*m/xm (float), p = rho * (cv*T*(gamma-1)) (idealGasEOS, sph/eos.hpp:31-40: double since T is double).
+    std: the std propagator's own density field (computeDensity, hydro_std/density.hpp:41-60) instead of kx m / xm"""
+    if std:
+        rho = np.asarray(f["rho"], np.float32)
+    else:
+        kx = np.asarray(f["kx"], np.float32)
+        m = np.asarray(f["m"], np.float32)
+        xm = np.asarray(f["xm"], np.float32)
+        rho = (kx * m / xm).astype(np.float32)
     cv = np.float64(po.ideal_gas_cv(mui, gamma))
     tmp = cv * np.asarray(f["temp"], np.float64) * (gamma - 1.0)
     return rho, (rho.astype(np.float64) * tmp).astype(np.float32)
@@ -34,11 +38,11 @@ def radii(f):
     return np.sqrt(x * x + y * y + z * z)
 
 
-def profiles(f, rmax, nbins):
+def profiles(f, rmax, nbins, std=False):
     """mean rho, p, |v|, u per radial shell [r_b, r_b+1) of width rmax/nbins; particles beyond rmax are ignored.
     Returns (edges, {name: mean per bin}, count per bin)."""
     r = radii(f)
-    rho, p = eos_rho_p(f)
+    rho, p = eos_rho_p(f, std=std)
     v = np.sqrt(sum(np.asarray(f[k], np.float64) ** 2 for k in ("vx", "vy", "vz")))
     u = np.float64(po.ideal_gas_cv()) * np.asarray(f["temp"], np.float64)
     edges = np.linspace(0.0, rmax, nbins + 1)
@@ -76,10 +80,50 @@ def energies(f, mui=np.float32(10.0), gamma=5.0 / 3.0):
     return ekin + eint, mom
 
 
-FIELDS = ["x", "y", "z", "vx", "vy", "vz", "temp", "m", "kx", "xm"]
+def noh_rho(r, t, gamma=5.0 / 3.0, rho0=1.0, vel0=-1.0, xgeom=3):
+    """analytic Noh density (compare_noh.py:49-60, nohShockFront + nohRho, vectorised): behind the shock front
+    r2 = (gamma - 1)/2 |vel0| t the density is rho0 ((gamma + 1)/(gamma - 1))^xgeom, ahead of it
+    rho0 (1 - vel0 t / r)^(xgeom - 1)"""
+    r = np.asarray(r, np.float64)
+    r2 = 0.5 * (gamma - 1) * abs(vel0) * t
+    with np.errstate(divide="ignore"):
+        pre = rho0 * (1.0 - vel0 * t / np.maximum(r, 1e-300)) ** (xgeom - 1)
+    return np.where(r > r2, pre, rho0 * ((gamma + 1) / (gamma - 1)) ** xgeom)
 
-# the two trajectory cases: (fixture name, IC, side, steps, profile steps, profile radius, bins)
+
+# the reference's Noh attributes (noh_init.hpp:46-56): r1 = 0.5, mTotal = 1, rho0 = 1.  compare_noh.py evaluates the
+# solution with the rho0 attribute, although mTotal = 1 in a sphere of radius 0.5 is a density of 1/(pi/6) = 1.91;
+# both are reported: NOH_RHO0_ATTR (the reference's number) and NOH_RHO0_IC (the IC's own density)
+NOH_RHO0_ATTR = 1.0
+NOH_RHO0_IC = 1.0 / (4.0 / 3.0 * np.pi * 0.5 ** 3)
+
+
+def noh_l1(f, t, rho0, std=False):
+    """createDensityPlot's L1 (compare_noh.py:141-148): mean |nohRho(r_i, t) - rho_i| over the particles"""
+    rho, _ = eos_rho_p(f, std=std)
+    return float(np.sum(np.abs(noh_rho(radii(f), t, rho0=rho0) - rho.astype(np.float64))) / rho.size)
+
+
+def energies_grav(f, egrav, mui=np.float32(10.0), gamma=5.0 / 3.0):
+    """ekin + eint + egrav (conserved_quantities.hpp with self-gravity: etot includes the potential energy)"""
+    return energies(f, mui, gamma)[0] + egrav
+
+
+FIELDS = ["x", "y", "z", "vx", "vy", "vz", "temp", "m", "kx", "xm"]
+FIELDS_STD = ["x", "y", "z", "vx", "vy", "vz", "temp", "m", "rho"]
+
+# the trajectory cases: (fixture name, IC, side, steps, profile steps, profile radius, bins)
 CASES = {
     "sedov": ("traj_sedov50.npz", "sedov", 50, 200, (50, 100, 200), 0.5, 25),
     "noh": ("traj_noh30.npz", "noh", 30, 100, (25, 50, 100), 0.5, 15),
+    # the std propagator (HydroProp, std_hydro.hpp:124-184) on the CI's Sedov case: its analytic L1 next to VE's
+    "sedov_std": ("traj_sedov50_std.npz", "sedov", 50, 200, (50, 100, 200), 0.5, 25),
+    # Evrard with self-gravity (G = 1): the energy budget including egrav of the reference's run
+    "evrard": ("traj_evrard30.npz", "evrard", 30, 100, (50, 100), 1.0, 20),
+    # BASELINE configs 3 and 5 at full size (14.1M particles each), the reference's run at the configured length
+    # (made with the -O3 build of the reference, libsphexa_ref_fast.so: ~1 h each on 8 cores)
+    "noh300": ("traj_noh300.npz", "noh", 300, 100, (25, 50, 100), 0.5, 50),
+    "evrard300": ("traj_evrard300.npz", "evrard", 300, 100, (50, 100), 1.0, 50),
 }
+# propagator / physics options of a case (pyoracle.default_params keywords; both the reference run and the GPU run)
+CASE_PARAMS = {"sedov_std": {"std": True}, "evrard": {"g": 1.0}, "evrard300": {"g": 1.0}}

@@ -879,6 +879,20 @@ int exchangeThen(sx_sim* s, const HydroLaunch& H, std::initializer_list<std::pai
  *  On entry the local particles are [first,last); on exit [first,last) again with halos around them. */
 int anyRank(sx_sim* s, bool bad, hipStream_t st, bool& out);
 
+//! a count exchange that doubles as a collective abort: a rank that cannot go on (capacity, scratch) sends
+//! kAbortCount to every peer, so all ranks leave the sync at the same exchange (SX_ERR_NOMEM) instead of the others
+//! waiting in the next collective; no extra host round trip
+constexpr uint64_t kAbortCount = ~0ull;
+int countsOrAbort(sx_sim* s, std::vector<uint64_t>& send, std::vector<uint64_t>& recv, bool fail, hipStream_t st)
+{
+    if (fail) send.assign(send.size(), kAbortCount);
+    SIM_COMM(s->comm->exchangeCounts(send, recv, st, s->cntBuf));
+    bool abort = fail;
+    for (uint64_t c : recv)
+        abort |= c == kAbortCount;
+    return abort ? SX_ERR_NOMEM : SX_OK;
+}
+
 int distributedSync(sx_sim* s, hipStream_t st, double margin)
 {
     sx::Transport* T  = s->comm;
@@ -931,7 +945,19 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     for (int q = 0; q < P; ++q)
         sendCnt[q] = seg[q + 1] - seg[q];
     s->cntBuf = s->work.get<uint64_t>("dom.cnt", 2 * P);
-    SIM_COMM(T->exchangeCounts(sendCnt, recvCnt, st, s->cntBuf));
+    if (!s->cntBuf) return SX_ERR_NOMEM; // 16 B per rank, kept from the first sync on
+    // the new local count is this rank's histogram bins (nlOf[r], the sum of the receive counts); the exchange
+    // buffers are sized by it before the count exchange, so a failure is decided there on every rank
+    PRec* sbuf = nullptr;
+    PRec* rbuf = nullptr;
+    bool  noRoom = nlOf[r] > s->cap;
+    if (!noRoom)
+    {
+        sbuf   = s->work.get<PRec>("dom.psend", nl);
+        rbuf   = s->work.get<PRec>("dom.precv", nlOf[r]);
+        noRoom = !sbuf || !rbuf;
+    }
+    if (int e = countsOrAbort(s, sendCnt, recvCnt, noRoom, st)) return e;
     bool moved = false;
     for (int q = 0; q < P; ++q)
         moved |= (q != r) && (sendCnt[q] || recvCnt[q]);
@@ -940,9 +966,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         uint64_t nNew = 0;
         for (int q = 0; q < P; ++q)
             nNew += recvCnt[q];
-        if (nNew > s->cap) return SX_ERR_NOMEM;
-        PRec* sbuf = s->work.get<PRec>("dom.psend", nl);
-        PRec* rbuf = s->work.get<PRec>("dom.precv", nNew);
+        if (nNew != nlOf[r]) return SX_ERR_ARG; // cannot happen: the splitters are histogram-bin boundaries
         if (nl) packPRecKernel<<<grid(nl), 256, 0, st>>>(s->fields(), nl, sbuf);
         std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
         uint64_t              acc = 0;
@@ -962,11 +986,10 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     }
 
     // --- 4. halo discovery: request boxes, exchange, mark, send lists
-    {   // the exchange must deliver exactly this rank's bins; the peers size their box receives from nlOf
-        bool bad = false;
-        if (int e = anyRank(s, nl != nlOf[r], st, bad)) return e;
-        if (bad) return SX_ERR_ARG;
-    }
+    // the exchange delivers exactly this rank's bins (the peers size their box receives from nlOf): the splitters
+    // are bin boundaries of the histogram of these same keys, so this holds on every rank by construction (checked
+    // after the exchange above); no agreement round trip
+    if (nl != nlOf[r]) return SX_ERR_ARG;
     const size_t nChunks = (nl + kChunk - 1) / kChunk;
     ReqBox*      myBoxes = s->work.get<ReqBox>("dom.mybox", nChunks);
     if (nChunks) chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
@@ -1005,18 +1028,24 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     constexpr size_t kFlagCap = size_t(1) << 27;
     const int        Pb       = (int)std::max<size_t>(1, std::min<size_t>(P, kFlagCap / (nl + 1)));
     const size_t     nf       = (size_t)Pb * (nl + 1);
-    if (nf > (size_t)INT32_MAX) return SX_ERR_NOMEM; // one peer's segment alone beyond the scan's range
-    uint32_t* flag = s->work.get<uint32_t>("dom.flag", nf);
-    uint32_t* scan = s->work.get<uint32_t>("dom.scan", nf);
+    // scratch failures are not returned here (the peers would wait in the count exchange below): they skip the
+    // send-list work and abort every rank at that exchange (countsOrAbort)
+    bool      fail = nf > (size_t)INT32_MAX; // one peer's segment alone beyond the scan's range
+    uint32_t* flag = fail ? nullptr : s->work.get<uint32_t>("dom.flag", nf);
+    uint32_t* scan = fail ? nullptr : s->work.get<uint32_t>("dom.scan", nf);
     uint32_t* segs = s->work.get<uint32_t>("dom.segs", Pb + 1);
     uint32_t* hseg = s->work.pinned<uint32_t>("dom.hseg", Pb + 1);
-    if (!flag || !scan || !segs || !hseg) return SX_ERR_NOMEM;
+    fail |= !flag || !scan || !segs || !hseg;
     s->haloSend.assign(P, 0);
     s->haloSendOff.assign(P, 0);
     size_t tmpB = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nf, st);
-    void* tmp = s->work.get<char>("dom.scantmp", tmpB);
-    if (!tmp) return SX_ERR_NOMEM;
+    void*  tmp  = nullptr;
+    if (!fail)
+    {
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nf, st);
+        tmp  = s->work.get<char>("dom.scantmp", tmpB);
+        fail = !tmp;
+    }
     // flags + scan of one batch; with scatter, the batch's send indices go to sendIdx[base, ...)
     auto batch = [&](int q0, int nb, bool scatter, uint64_t base) -> int
     {
@@ -1037,16 +1066,16 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     // the send list is sized by what the peers request (a local may go to several peers): with one batch the scan
     // is read before the scatter; with several, a counting pass first (the arena's growth does not keep contents)
     uint64_t total = 0;
-    for (int q0 = 0; q0 < P; q0 += Pb)
+    for (int q0 = 0; q0 < P && !fail; q0 += Pb)
     {
         const int nb = std::min(Pb, P - q0);
         if (int e = batch(q0, nb, false, total)) return e;
         total += hseg[nb];
     }
-    s->sendIdx = s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
-    if (!s->sendIdx) return SX_ERR_NOMEM;
-    if (Pb >= P) scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, 0, s->sendIdx);
-    else
+    s->sendIdx = fail ? nullptr : s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
+    fail |= !s->sendIdx;
+    if (!fail && Pb >= P) scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, 0, s->sendIdx);
+    else if (!fail)
     {
         uint64_t base = 0;
         for (int q0 = 0; q0 < P; q0 += Pb)
@@ -1057,7 +1086,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         }
     }
     s->numSend = total;
-    SIM_COMM(T->exchangeCounts(s->haloSend, s->haloRecv, st, s->cntBuf));
+    if (int e = countsOrAbort(s, s->haloSend, s->haloRecv, fail, st)) return e;
     s->haloRecv[r] = 0;
     uint64_t nLow = 0, nHigh = 0;
     for (int q = 0; q < P; ++q)
@@ -1644,6 +1673,8 @@ extern "C"
     int sx_sim_set_gravity_counting(sx_sim* s, int enable)
     {
         if (!s || s->p.g == 0.0) return SX_ERR_ARG;
+        // the ve-bdt substeps (sx_bdt.cpp) do not count: refusing beats zeros that read as valid counts
+        if (enable && s->p.propagator == 2) return SX_ERR_ARG;
         s->gravCount = enable != 0;
         if (s->gravCount)
         {
@@ -1862,7 +1893,9 @@ extern "C"
             packXHalos(s, st);
             // the cluster kernels write the locals' records as they produce them (PairArgs::rtOut / rcOut, EosArgs):
             // the packing passes below then cover only the halos (halo()); the exact kernels leave it to them
-            const bool fused = H.clusterLists && !pa.active;
+            // only the cluster kernels write records; they run when the lists are in the local (union) format, and
+            // ngmax > 256 keeps the global format, whose gather kernels read packed records of every particle
+            const bool fused = H.clusterLists && pa.localLists && !pa.active;
             auto       halo  = [&](size_t a, size_t b, auto&& fn) {
                 if (!fused) return fn(a, b);
                 if (a < s->first) fn(a, std::min(b, (size_t)s->first));

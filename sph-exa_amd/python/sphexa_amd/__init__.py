@@ -603,11 +603,15 @@ class Sim:
         self.set_state(st, float(d["minDt"]), float(d["minDt_m1"]))
         if self.params.propagator == 2 and "ts::numRungs" in d:
             # HydroVeBdtProp::load (ve_hydro_bdt.hpp:155-168): Timestep numRungs + dt_m1, substep 0, and the rungs
+            if "rung" not in d:
+                raise ValueError("restart file has ts::numRungs but no 'rung' field")
+            rung = np.ascontiguousarray(d["rung"], dtype=np.uint8)
+            if rung.shape != (len(st["x"]),):
+                raise ValueError(f"restart file's 'rung' has {rung.size} entries for {len(st['x'])} particles")
             ts = SxTimestep()
             ts.numRungs = int(d["ts::numRungs"])
             for k, v in enumerate(np.asarray(d["ts::dt_m1"], np.float32)):
                 ts.dt_m1[k] = float(v)
-            rung = np.ascontiguousarray(d["rung"], dtype=np.uint8)
             self._keep_rung = rung
             self.ctx.check(self.L.sx_sim_set_timestep(self.h, C.byref(ts), rung.ctypes.data), "set_timestep")
         self.iteration = int(d["iteration"]) if "iteration" in d else 0

@@ -346,6 +346,21 @@ def test_large_union_step(ctx, ora):
     sim.close()
 
 
+@pytest.mark.parametrize("ic", ["sedov", "noh"])
+def test_global_list_format_steps(ctx, ora, ic):
+    """ngmax > 256: the lists cannot be u16 union positions (NbLists::localPossible), so the step runs the gather
+    kernels over global lists, which read the packed records of every particle.  The cluster kernels' record
+    writes then do not happen and every record must come from the packing passes (reading the previous
+    step's records went unnoticed); three steps, each checked per particle against the oracle"""
+    st, obox = (po.sedov_state if ic == "sedov" else po.noh_state)(16)
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox), params=sx.default_params(ngmax=300))
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    op = ora.params()
+    op.ngmax = 300
+    gutil.shadow_steps(ctx, ora, sim, obox, 3, op, FLOATS)
+    sim.close()
+
+
 def test_golden_fixture_steps(ctx, ora):
     """the oracle reproduces the reference's own steps (sedov10.npz, from oracle/_ref) bit for bit, and the GPU's
     steps from the fixture state are checked per particle against it"""
