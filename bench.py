@@ -51,7 +51,8 @@ EDGE_MODEL = {"findNeighbors": (32, 28), "xmass": (44, 32), "veDefGradh": (48, 3
 COMPULSORY_OWN = {"findNeighbors": 28 + 8 + 32, "xmass": 32 + 4 + 4, "veDefGradh": 48 + 4 + 8,
                   "iadDivvCurlv": 80 + 4 + 28, "avSwitches": 96 + 4 + 4, "momentumEnergy": 96 + 4 + 20}
 # kernel-time slot -> rocprofv3 kernel-name fragments it launches (sx_sim.cpp kev slots)
-PMC_KERNELS = {"findNeighbors": ("findNeighborsKernel", "leafFrameKernel"), "xmass": ("xmassKernel",),
+PMC_KERNELS = {"findNeighbors": ("findNeighborsKernel", "leafFrameKernel", "skinFilterKernel", "dispGridKernel",
+                                  "leafBoxKernel", "innerBoxKernel"), "xmass": ("xmassKernel",),
                "veDefGradh": ("veDefGradhKernel",), "iadDivvCurlv": ("iadDivvCurlv",),
                "avSwitches": ("avSwitchesKernel",), "momentumEnergy": ("momentumEnergyKernel",),
                "gravity": ("gravityTraverseKernel",)}
@@ -199,6 +200,10 @@ def parse():
     ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
     ap.add_argument("--prop", default="ve", choices=["ve", "std"],
                     help="ve (HydroVeProp, the BASELINE metric) or std (HydroProp, std_hydro.hpp)")
+    ap.add_argument("--skin", type=float, default=0.08,
+                    help="neighbor lists behind a skin 2h(1+s) between full builds (sx_sim_set_skin; 0: sync + "
+                         "search every step, the reference's flow)")
+    ap.add_argument("--skin-reuse", type=int, default=24, help="steps between full builds at most")
     return ap.parse_args()
 
 
@@ -282,6 +287,7 @@ def main():
     params = sx.default_params(av_clean=args.av_clean, g=1.0 if args.init == "evrard" else 0.0,
                                std=args.prop == "std")
     sim = sx.Sim(ctx, cap, box, params=params, bucket=args.bucket)
+    sim.set_skin(args.skin, args.skin_reuse)
     comm = None
     transport = args.backend
     if world > 1:
@@ -317,6 +323,7 @@ def main():
 
     ctx.sync()
     barrier()
+    skin0 = sim.skin_stats()
     stage_sum, kern_sum = {}, {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -335,6 +342,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = sim.stats()
+    skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters") else v)
+            for k, v in sim.skin_stats().items()}  # the timed steps'
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
     inter = None
@@ -437,7 +446,11 @@ def main():
                    **({"gravity_halos_per_gpu": sim.gravity_stats()["halos"],
                        "gravity_far_cells": sim.gravity_stats()["far_cells"]} if world > 1 and args.init == "evrard"
                       else {}),
-                   "kernels": "exact (no FMA)" if args.exact else "fast (FMA)"},
+                   "kernels": "exact (no FMA)" if args.exact else "fast (FMA)",
+                   "neighbor_skin": {"factor": args.skin, "max_reuse": args.skin_reuse,
+                                     "note": "one rank without gravity: steps between full builds filter the last "
+                                             "build's lists within 2h(1+s) (sx_skin.hpp); same neighbor sets, nc, h",
+                                     **skin}},
         "roofline": roofline,
         "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_ms.items()
                        if not std_prop or k in STD_KERNEL_NAMES},

@@ -206,6 +206,57 @@ __device__ __forceinline__ double readfirstlaneD(double v)
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+//! uniform grid over the box (skin lists, sx_skin.hpp: per-step displacement maxima by cell of the end-of-step position)
+struct DispGrid
+{
+    double lo[3];
+    double inv[3]; // cells per unit length
+    int    n;      // cells per axis
+    int    pbc[3];
+};
+
+//! cell index of coordinate v on axis d: clamped on open axes, unwrapped (callers wrap) on periodic ones
+__host__ __device__ inline int gridCell(double v, const DispGrid& g, int d)
+{
+    const double f = (v - g.lo[d]) * g.inv[d];
+    int          k = (int)floor(f);
+    if (g.pbc[d]) return k;
+    return k < 0 ? 0 : (k >= g.n ? g.n - 1 : k);
+}
+
+__host__ __device__ inline int wrapCell(int k, int n)
+{
+    k %= n;
+    return k < 0 ? k + n : k;
+}
+
+/*! cells[cell of (x, y, z)] = max(., d) for every lane with d > 0, called by every lane of the wave.  SFC-ordered
+ *  particles: a wave's moving particles share one or two cells, so the first moving lane's cell takes one atomic with
+ *  the wave's maximum over it and lanes in other cells add their own */
+__device__ inline void gridMaxAtomic(uint32_t* cells, const DispGrid& g, double x, double y, double z, float d)
+{
+    uint32_t cell = 0;
+    if (d > 0.0f)
+    {
+        const double p[3] = {x, y, z};
+        int          k[3];
+        for (int e = 0; e < 3; ++e)
+            k[e] = g.pbc[e] ? wrapCell(gridCell(p[e], g, e), g.n) : gridCell(p[e], g, e);
+        cell = ((uint32_t)k[2] * g.n + (uint32_t)k[1]) * g.n + (uint32_t)k[0];
+    }
+    const uint64_t mv = __ballot(d > 0.0f);
+    if (!mv) return;
+    const int      l0   = __builtin_ctzll(mv);
+    const uint32_t c0   = __builtin_amdgcn_readlane(cell, l0);
+    const bool     same = d > 0.0f && cell == c0;
+    float          m    = same ? d : 0.0f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        m = fmaxf(m, __shfl_xor(m, o, kWave));
+    if ((int)(threadIdx.x & 63) == l0) atomicMax(&cells[c0], __float_as_uint(m));
+    if (d > 0.0f && !same) atomicMax(&cells[cell], __float_as_uint(d));
+}
+
 //! float atomic min for non-negative values via the ordered int representation
 __device__ __forceinline__ void atomicMinPos(float* addr, float v)
 {

@@ -599,59 +599,76 @@ __global__ __launch_bounds__(kBlock) void momentumStdKernel(PairArgs a)
 __global__ void positionsKernel(PosArgs a)
 {
     uint32_t i = a.first + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.last) return;
-    const DevBox& b    = a.box;
-    bool          skip = false;
-    if ((b.fbc[0] || b.fbc[1] || b.fbc[2]) && a.vx[i] == 0.0f && a.vy[i] == 0.0f && a.vz[i] == 0.0f)
+    float    dcell = 0.0f; // this step's displacement for the grid (every lane reaches the grid update below)
+    double   pc[3] = {0.0, 0.0, 0.0};
+    if (i < a.last)
     {
-        double X[3] = {a.x[i], a.y[i], a.z[i]};
-        for (int d = 0; d < 3; ++d)
+        const DevBox& b    = a.box;
+        bool          skip = false;
+        if ((b.fbc[0] || b.fbc[1] || b.fbc[2]) && a.vx[i] == 0.0f && a.vy[i] == 0.0f && a.vz[i] == 0.0f)
         {
-            double top = b.lim[2 * d + 1], bot = b.lim[2 * d];
-            if (b.fbc[d] && (fabs(top - X[d]) < 2.0f * a.h[i] || fabs(bot - X[d]) < 2.0f * a.h[i])) skip = true;
+            double X[3] = {a.x[i], a.y[i], a.z[i]};
+            for (int d = 0; d < 3; ++d)
+            {
+                double top = b.lim[2 * d + 1], bot = b.lim[2 * d];
+                if (b.fbc[d] && (fabs(top - X[d]) < 2.0f * a.h[i] || fabs(bot - X[d]) < 2.0f * a.h[i])) skip = true;
+            }
         }
+        const double dt = a.dtPtr ? a.dtPtr[0] : a.dt, dt_m1 = a.dtPtr ? a.dtPtr[1] : a.dt_m1;
+        if (!skip)
+        {
+            double A[3]  = {a.ax[i], a.ay[i], a.az[i]};
+            double X[3]  = {a.x[i], a.y[i], a.z[i]};
+            double dX[3] = {a.x_m1[i], a.y_m1[i], a.z_m1[i]};
+            double Xn[3], Vn1[3], dXn1[3];
+            double inv = 1.0 / dt_m1, hdm1 = 0.5 * dt_m1, adt = fabs(dt);
+    #pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+                double Vnmhalf = dX[k] * inv;
+                double Vn      = Vnmhalf + A[k] * hdm1;
+                Vn1[k]         = Vn + A[k] * dt;
+                dXn1[k]        = (Vn + (A[k] * 0.5) * adt) * dt;
+                Xn[k]          = X[k] + dXn1[k];
+            }
+    #pragma unroll
+            for (int d = 0; d < 3; ++d)
+            {
+                if (b.pbc[d] && Xn[d] > b.lim[2 * d + 1]) Xn[d] -= b.l[d];
+                else if (b.pbc[d] && Xn[d] < b.lim[2 * d]) Xn[d] += b.l[d];
+            }
+            a.x[i]    = Xn[0];
+            a.y[i]    = Xn[1];
+            a.z[i]    = Xn[2];
+            a.x_m1[i] = (float)dXn1[0];
+            a.y_m1[i] = (float)dXn1[1];
+            a.z_m1[i] = (float)dXn1[2];
+            a.vx[i]   = (float)Vn1[0];
+            a.vy[i]   = (float)Vn1[1];
+            a.vz[i]   = (float)Vn1[2];
+            if (a.keys) a.keys[i] = sfcKey(Xn[0], Xn[1], Xn[2], b);
+            if (a.disp)
+            {
+                // an upper bound of the move (the periodic wrap above does not count): float rounding pushed upwards
+                const float d = (float)(sqrt(dXn1[0] * dXn1[0] + dXn1[1] * dXn1[1] + dXn1[2] * dXn1[2]) * (1.0 + 0x1p-20));
+                a.disp[i]     = d;
+                a.odo[i] += d;
+                dcell = d, pc[0] = Xn[0], pc[1] = Xn[1], pc[2] = Xn[2];
+            }
+        }
+        else
+        {
+            if (a.keys) a.keys[i] = sfcKey(a.x[i], a.y[i], a.z[i], b);
+            if (a.disp) a.disp[i] = 0.0f;
+        }
+        double u_old = (double)a.constCv * a.temp[i];
+        double du = a.du[i], du_m1 = (double)a.du_m1[i];
+        double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;
+        if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
+        a.temp[i]  = u_new / (double)a.constCv;
+        a.du_m1[i] = (float)du;
     }
-    const double dt = a.dtPtr ? a.dtPtr[0] : a.dt, dt_m1 = a.dtPtr ? a.dtPtr[1] : a.dt_m1;
-    if (!skip)
-    {
-        double A[3]  = {a.ax[i], a.ay[i], a.az[i]};
-        double X[3]  = {a.x[i], a.y[i], a.z[i]};
-        double dX[3] = {a.x_m1[i], a.y_m1[i], a.z_m1[i]};
-        double Xn[3], Vn1[3], dXn1[3];
-        double inv = 1.0 / dt_m1, hdm1 = 0.5 * dt_m1, adt = fabs(dt);
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-        {
-            double Vnmhalf = dX[k] * inv;
-            double Vn      = Vnmhalf + A[k] * hdm1;
-            Vn1[k]         = Vn + A[k] * dt;
-            dXn1[k]        = (Vn + (A[k] * 0.5) * adt) * dt;
-            Xn[k]          = X[k] + dXn1[k];
-        }
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-        {
-            if (b.pbc[d] && Xn[d] > b.lim[2 * d + 1]) Xn[d] -= b.l[d];
-            else if (b.pbc[d] && Xn[d] < b.lim[2 * d]) Xn[d] += b.l[d];
-        }
-        a.x[i]    = Xn[0];
-        a.y[i]    = Xn[1];
-        a.z[i]    = Xn[2];
-        a.x_m1[i] = (float)dXn1[0];
-        a.y_m1[i] = (float)dXn1[1];
-        a.z_m1[i] = (float)dXn1[2];
-        a.vx[i]   = (float)Vn1[0];
-        a.vy[i]   = (float)Vn1[1];
-        a.vz[i]   = (float)Vn1[2];
-        if (a.keys) a.keys[i] = sfcKey(Xn[0], Xn[1], Xn[2], b);
-    }
-    else if (a.keys) a.keys[i] = sfcKey(a.x[i], a.y[i], a.z[i], b);
-    double u_old = (double)a.constCv * a.temp[i];
-    double du = a.du[i], du_m1 = (double)a.du_m1[i];
-    double u_new = u_old + du * dt + 0.5 * (du - du_m1) / dt_m1 * fabs(dt) * dt;
-    if (u_new < 0.) { u_new = u_old * exp(u_new * dt / u_old); }
-    a.temp[i]  = u_new / (double)a.constCv;
-    a.du_m1[i] = (float)du;
+    if (a.cells) gridMaxAtomic(a.cells, a.grid, pc[0], pc[1], pc[2], dcell);
 }
 
 //! updateSmoothingLengthGpuKernel (update_h_gpu.cu:39-46)

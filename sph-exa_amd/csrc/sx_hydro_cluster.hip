@@ -98,9 +98,6 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     const uint32_t nw = (cu.cnt + 1) >> 1;
     cu.wBeg           = nw * cu.part / SPLIT;
     cu.wEnd           = nw * (cu.part + 1) / SPLIT;
-#ifdef SX_PAIR_NOLOOP
-    cu.wEnd = cu.wBeg; // measurement builds only: setup, staging and output without the neighbor loops
-#endif
     cu.U              = a.ucount[cu.c];
     cu.un             = a.uni + (size_t)cu.c * a.ucap;
     cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
@@ -169,21 +166,12 @@ __device__ __forceinline__ void neighborLoop(const Clu& cu, Stage&& stage, Load&
             const uint32_t u = b0 + threadIdx.x + s * NT;
             js[s]            = u < b1 ? cu.un[u] : 0u;
         }
-#ifndef SX_PAIR_NOSTAGE
 #pragma unroll
         for (int s = 0; s < S; ++s)
         {
             const uint32_t u = b0 + threadIdx.x + s * NT;
             if (u < b1) stage(js[s], u - b0);
         }
-#else
-        // measurement builds only: the union indices are read, no record is gathered or staged
-        uint32_t x = 0;
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-            x ^= js[s];
-        asm volatile("" ::"v"(x));
-#endif
     };
 
     if (cu.U <= (uint32_t)CH)
@@ -629,69 +617,13 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
     }
 }
 
-typedef float v2f __attribute__((ext_vector_type(2)));
-
-//! kernelWt on two arguments at once (packed FP32: v_pk_fma / v_pk_mul)
-__device__ __forceinline__ v2f kernelWt2(v2f t)
-{
-    t     = v2f{fminf(t.x, 4.0f), fminf(t.y, 4.0f)};
-    v2f s = v2f{3.08339593857454e-08f, 3.08339593857454e-08f};
-    s     = __builtin_elementwise_fma(s, t, v2f{-2.262898533444968e-06f, -2.262898533444968e-06f});
-    s     = __builtin_elementwise_fma(s, t, v2f{0.00010206655861111358f, 0.00010206655861111358f});
-    s     = __builtin_elementwise_fma(s, t, v2f{-0.0029803994111716747f, -0.0029803994111716747f});
-    s     = __builtin_elementwise_fma(s, t, v2f{0.050733841955661774f, 0.050733841955661774f});
-    s     = __builtin_elementwise_fma(s, t, v2f{-0.411233514547348f, -0.411233514547348f});
-    s     = __builtin_elementwise_fma(s, t, v2f{1.0f, 1.0f});
-    const v2f s2 = s * s;
-    return s2 * s2 * s2;
-}
-
-/*! Packed-FP32 walk over this lane's share of its list (resident union, field-major LDS records sf[k * CH + slot]):
- *  per list word both neighbors at once, field k of the two as one register pair (two ds_read_b32, no packing
- *  moves).  body(F, two) gets F(k) -> v2f {field k of the first neighbor, of the second} and whether the second
- *  exists (a missing second neighbor reads slot 0).  Field bases every 9 fields keep ds_read's 16-bit offsets. */
-template<int CH, int NF, class Body>
-__device__ __forceinline__ void packedLoop(const Clu& cu, const float* sf, Body&& body)
-{
-    const uint32_t  wLast = cu.wEnd - 1;
-    const uint32_t* nl    = cu.nl;
-    auto            ld    = [&](uint32_t w) { return nl[(size_t)min(w, wLast) * kWave]; };
-    uint32_t        q0 = ld(cu.wBeg + 1), q1 = ld(cu.wBeg + 2);
-    uint32_t        wd = nl[(size_t)cu.wBeg * kWave];
-    constexpr int   NB = (NF + 8) / 9;
-    for (uint32_t w = cu.wBeg;;)
-    {
-        const bool two = 2 * w + 1 < cu.cnt;
-        uint32_t   i0[NB], i1[NB];
-        i0[0] = wd & 0xffffu, i1[0] = wd >> 16;
-#pragma unroll
-        for (int b = 1; b < NB; ++b)
-        {
-            i0[b] = i0[0] + 9 * b * CH, i1[b] = i1[0] + 9 * b * CH;
-            asm volatile("" : "+v"(i0[b]));
-            asm volatile("" : "+v"(i1[b]));
-        }
-        auto F = [&](int k) { return v2f{sf[i0[k / 9] + (k % 9) * CH], sf[i1[k / 9] + (k % 9) * CH]}; };
-        wd = q0, q0 = q1, q1 = ld(w + 3);
-        body(F, two);
-        if (++w >= cu.wEnd) break;
-    }
-}
-
-#ifndef SX_AV_PK
-#define SX_AV_PK 0 // AV switches: packed FP32 over field-major LDS records
-#endif
-
 // ---- AV switches: AVswitchesJLoop (av_switches_kern.hpp:43-137) -------------------------------------------------
 template<int CH, int SPLIT, int UMIN = 0, int UMAX = 0>
 __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
 {
-    constexpr bool    SOA = SX_AV_PK;
-    constexpr int     CA  = SOA ? 1 : CH;
-    __shared__ float4 sP[CA]; // x, y, z, vol
-    __shared__ float4 sV[CA]; // vx, vy, vz, c
-    __shared__ float  sD[CA]; // divv
-    __shared__ float  sF[SOA ? 9 * CH : 1]; // SOA: the same 9 fields, field-major
+    __shared__ float4 sP[CH]; // x, y, z, vol
+    __shared__ float4 sV[CH]; // vx, vy, vz, c
+    __shared__ float  sD[CH]; // divv
     __shared__ float  s_red[kClusterWaves * SPLIT];
     if constexpr (UMIN > 0 || UMAX > 0)
     {
@@ -715,65 +647,12 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         const RecX r = a.rx[j];
         const RecV v = a.rv[j];
         const RecT t = a.rt[j];
-        if constexpr (SOA)
-        {
-            const float f[9] = {relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
-                                t.xm / t.kx, v.vx, v.vy, v.vz, v.c, a.rc[j].divv};
-#pragma unroll
-            for (int k = 0; k < 9; ++k)
-                sF[k * CH + slot] = f[k];
-            return;
-        }
         sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
                                t.xm / t.kx);
         sV[slot] = make_float4(v.vx, v.vy, v.vz, v.c);
         sD[slot] = a.rc[j].divv;
     };
-    auto loadRec = [&](uint32_t p) {
-        if constexpr (SOA)
-            return Rec9{make_float4(sF[p], sF[CH + p], sF[2 * CH + p], sF[3 * CH + p]),
-                        make_float4(sF[4 * CH + p], sF[5 * CH + p], sF[6 * CH + p], sF[7 * CH + p]), sF[8 * CH + p]};
-        else return Rec9{sP[p], sV[p], sD[p]};
-    };
-#if SX_AV_PK
-    if (cu.U <= (uint32_t)CH)
-    {
-        // stage the resident union (neighborLoop's fill), then both neighbors of a list word per packed instruction
-        constexpr int  NT = kB * SPLIT;
-        for (uint32_t u = threadIdx.x; u < cu.U; u += NT)
-            stage(cu.un[u], u);
-        __syncthreads();
-        if (cu.wBeg < cu.wEnd)
-        {
-            const v2f xi2 = {xi, xi}, yi2 = {yi, yi}, zi2 = {zi, zi}, vx2 = {vi.vx, vi.vx}, vy2 = {vi.vy, vi.vy},
-                      vz2 = {vi.vz, vi.vz}, hiInv2_2 = {hiInv2, hiInv2}, ci2 = {ci, ci}, dv2 = {divv_i, divv_i};
-            v2f       G[3] = {{0, 0}, {0, 0}, {0, 0}};
-            packedLoop<CH, 9>(cu, sF, [&](auto&& F, bool two) {
-                v2f rx = xi2 - F(0), ry = yi2 - F(1), rz = zi2 - F(2);
-                if (cu.pbc)
-                {
-                    float x0 = rx.x, y0 = ry.x, z0 = rz.x, x1 = rx.y, y1 = ry.y, z1 = rz.y;
-                    applyPBC(a.box, h2, x0, y0, z0);
-                    applyPBC(a.box, h2, x1, y1, z1);
-                    rx = v2f{x0, x1}, ry = v2f{y0, y1}, rz = v2f{z0, z1};
-                }
-                v2f r2 = rx * rx + ry * ry + rz * rz;
-                r2.y   = two ? r2.y : 1.0f; // slot 0 may be the target itself: keep the skipped term finite
-                const v2f rinv = {rsqrtf(r2.x), rsqrtf(r2.y)};
-                const v2f rv   = rx * (vx2 - F(4)) + ry * (vy2 - F(5)) + rz * (vz2 - F(6));
-                const v2f t    = ci2 + F(7) - v2f{3.0f, 3.0f} * rv * rinv;
-                const float s0 = rv.x < 0.0f ? t.x : 0.0f, s1 = (two && rv.y < 0.0f) ? t.y : 0.0f;
-                vijsignal_i    = fmaxf(vijsignal_i, fmaxf(s0, s1));
-                const v2f fw   = kernelWt2(r2 * hiInv2_2) * (F(3) * (dv2 - F(8))) * v2f{1.0f, two ? 1.0f : 0.0f};
-                G[0] += fw * rx;
-                G[1] += fw * ry;
-                G[2] += fw * rz;
-            });
-            gx = G[0].x + G[0].y, gy = G[1].x + G[1].y, gz = G[2].x + G[2].y;
-        }
-    }
-    else
-#endif
+    auto loadRec = [&](uint32_t p) { return Rec9{sP[p], sV[p], sD[p]}; };
     neighborLoop<CH, SPLIT>(
         cu, stage, loadRec,
         [&](const Rec9& r) {
@@ -797,7 +676,7 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
         res);
     {
         float v[4] = {gx, gy, gz, vijsignal_i};
-        combineShares<SPLIT>(cu, v, SOA ? sF : reinterpret_cast<float*>(sP), 8u, true);
+        combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 8u, true);
         gx = v[0], gy = v[1], gz = v[2], vijsignal_i = v[3];
     }
     if (!cu.valid || cu.part != 0) return;
@@ -850,10 +729,6 @@ __device__ __forceinline__ void atwoodWeights(float Atwood, float Atmin, float A
         b_mom             = exp2f(fmaf(-sigma, dl, 2.0f * lxj));
     }
 }
-
-#ifndef SX_ME_PK
-#define SX_ME_PK 0 // momentum: both neighbors of a list word per packed-FP32 instruction (resident unions, no avClean)
-#endif
 
 //! LDS record of the momentum kernel: 80 B, + 24 B of velocity gradient with avClean
 template<bool AVC>
@@ -924,16 +799,11 @@ __device__ __forceinline__ MeRaw<AVC> meLoadRaw(const PairArgs& a, uint32_t j)
 template<int CH, int SPLIT, bool AVC>
 __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, uint32_t numClusters)
 {
-    // SOA (packed build without avClean): the 20 record fields as separate float arrays, so the two neighbors of a
-    // list word land in the two halves of one register pair (ds_read_b32 each) with no packing moves
-    constexpr bool    SOA = SX_ME_PK && !AVC;
-    constexpr int     CA  = SOA ? 1 : CH;
-    __shared__ float4 sP[CA]; // x, y, z, 1/h
-    __shared__ float4 sV[CA]; // vx, vy, vz, c
-    __shared__ float4 sT[CA]; // m, xm, rho, m*prho
-    __shared__ float4 sA[CA]; // alpha, c11, c12, c13
-    __shared__ float4 sB[CA]; // c22, c23, c33, m/rho
-    __shared__ float  sF[SOA ? 20 : 1][SOA ? CH : 1]; // the same 20 fields, field-major
+    __shared__ float4 sP[CH]; // x, y, z, 1/h
+    __shared__ float4 sV[CH]; // vx, vy, vz, c
+    __shared__ float4 sT[CH]; // m, xm, rho, m*prho
+    __shared__ float4 sA[CH]; // alpha, c11, c12, c13
+    __shared__ float4 sB[CH]; // c22, c23, c33, m/rho
     __shared__ float4 sG[AVC ? CH : 1];  // dV11, dV12, dV13, dV22 (avClean)
     __shared__ float2 sG2[AVC ? CH : 1]; // dV23, dV33
     __shared__ float  s_ext[kClusterWaves * SPLIT];
@@ -1024,9 +894,6 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         const uint32_t nw = (cu.cnt + 1) >> 1;
         cu.wBeg           = nw * cu.part / SPLIT;
         cu.wEnd           = nw * (cu.part + 1) / SPLIT;
-#ifdef SX_PAIR_NOLOOP
-        cu.wEnd = cu.wBeg;
-#endif
         cu.U              = cur.U;
         cu.un             = a.uni + (size_t)cu.c * a.ucap;
         cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
@@ -1059,16 +926,6 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
             const RecT& tq  = q.t;
             const MeC&  c6  = q.c;
             const float rho = tq.kx * r.m / tq.xm;
-            if constexpr (SOA)
-            {
-                const float f[20] = {relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
-                                     1.0f / r.h, q.v.vx, q.v.vy, q.v.vz, q.v.c, r.m, tq.xm, rho, r.m * tq.prho,
-                                     tq.alpha, c6.a.x, c6.a.y, c6.a.z, c6.a.w, c6.b.x, c6.b.y, r.m / rho};
-#pragma unroll
-                for (int k = 0; k < 20; ++k)
-                    sF[k][slot] = f[k];
-                return;
-            }
             sP[slot]        = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1),
                                    relc(r.z, cu.oz, a.box, 2), 1.0f / r.h);
             sV[slot]        = make_float4(q.v.vx, q.v.vy, q.v.vz, q.v.c);
@@ -1120,15 +977,6 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         }
         auto loadRec = [&](uint32_t p) {
                 RecM<AVC> r;
-                if constexpr (SOA)
-                {
-                    r.p = make_float4(sF[0][p], sF[1][p], sF[2][p], sF[3][p]);
-                    r.v = make_float4(sF[4][p], sF[5][p], sF[6][p], sF[7][p]);
-                    r.t = make_float4(sF[8][p], sF[9][p], sF[10][p], sF[11][p]);
-                    r.a = make_float4(sF[12][p], sF[13][p], sF[14][p], sF[15][p]);
-                    r.b = make_float4(sF[16][p], sF[17][p], sF[18][p], sF[19][p]);
-                    return r;
-                }
                 r.p = sP[p], r.v = sV[p], r.t = sT[p], r.a = sA[p], r.b = sB[p];
                 if constexpr (AVC) r.g = sG[p], r.g2 = sG2[p];
                 return r;
@@ -1193,114 +1041,6 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
                 my += ki * u2i + kj * u2j;
                 mz += ki * u3i + kj * u3j;
             };
-#if SX_ME_PK
-        if (SOA && res && cu.wBeg < cu.wEnd)
-        {
-            // packed FP32: the two neighbors of a list word are evaluated together, each v2f lane one neighbor; the
-            // fields are paired once per word (v_pk_mov), the next word's records load during the evaluation
-            const v2f      xi2 = {xi, xi}, yi2 = {yi, yi}, zi2 = {zi, zi};
-            const v2f      vxi2 = {vi.vx, vi.vx}, vyi2 = {vi.vy, vi.vy}, vzi2 = {vi.vz, vi.vz};
-            const v2f      hiInv2_2 = {hiInv2, hiInv2}, hiInv3_2 = {hiInv3, hiInv3};
-            const v2f      c11 = {ci6.c11, ci6.c11}, c12 = {ci6.c12, ci6.c12}, c13 = {ci6.c13, ci6.c13},
-                      c22 = {ci6.c22, ci6.c22}, c23 = {ci6.c23, ci6.c23}, c33 = {ci6.c33, ci6.c33};
-            const v2f      ci2 = {ci, ci}, alpha2 = {alpha_i, alpha_i}, rhoi2 = {rhoi, rhoi};
-            const v2f      rhoiInv2 = {rhoiInv, rhoiInv}, prhoi2 = {prhoi, prhoi}, xmi2v = {xmi2, xmi2};
-            const float    AtminLo2 = AtminLo * AtminLo;
-            const uint32_t wLast = cu.wEnd - 1;
-            const uint32_t* nl   = cu.nl;
-            auto           ld    = [&](uint32_t w) { return nl[(size_t)min(w, wLast) * kWave]; };
-            uint32_t       q0 = ld(cu.wBeg + 1), q1 = ld(cu.wBeg + 2);
-            uint32_t       wd = nl[(size_t)cu.wBeg * kWave];
-            v2f            sMx = {0, 0}, sMy = {0, 0}, sMz = {0, 0}, sE = {0, 0}, sV = {0, 0};
-            for (uint32_t w = cu.wBeg;;)
-            {
-                const bool     two = 2 * w + 1 < cu.cnt; // the word's second neighbor exists
-                // three bases per neighbor (fields 0-8, 9-17, 18-19) within ds_read's 16-bit offset: the bases are
-                // laundered so the compiler does not fold them back into one add per field
-                uint32_t i0[3] = {wd & 0xffffu, 0u, 0u}, i1[3] = {wd >> 16, 0u, 0u};
-#pragma unroll
-                for (int b = 1; b < 3; ++b)
-                {
-                    i0[b] = i0[0] + 9 * b * CH, i1[b] = i1[0] + 9 * b * CH;
-                    asm volatile("" : "+v"(i0[b]));
-                    asm volatile("" : "+v"(i1[b]));
-                }
-                const float* sf = &sF[0][0];
-                auto F = [&](int k) { return v2f{sf[i0[k / 9] + (k % 9) * CH], sf[i1[k / 9] + (k % 9) * CH]}; };
-                const v2f      PX = F(0), PY = F(1), PZ = F(2), PW = F(3), VX = F(4), VY = F(5), VZ = F(6), VW = F(7);
-                const v2f      TX = F(8), TY = F(9), TZ = F(10), TW = F(11), AX = F(12), AY = F(13), AZ = F(14);
-                const v2f      AW = F(15), BX = F(16), BY = F(17), BZ = F(18), BW = F(19);
-                wd = q0, q0 = q1, q1 = ld(w + 3);
-
-                v2f rx = xi2 - PX, ry = yi2 - PY, rz = zi2 - PZ;
-                if (cu.pbc)
-                {
-                    float x0 = rx.x, y0 = ry.x, z0 = rz.x, x1 = rx.y, y1 = ry.y, z1 = rz.y;
-                    applyPBC(a.box, h2, x0, y0, z0);
-                    applyPBC(a.box, h2, x1, y1, z1);
-                    rx = v2f{x0, x1}, ry = v2f{y0, y1}, rz = v2f{z0, z1};
-                }
-                v2f r2 = rx * rx + ry * ry + rz * rz;
-                // a missing second neighbor reads slot 0, which may be this target itself (r = 0): its terms are
-                // zeroed through W below, r2 = 1 keeps them finite
-                r2.y             = two ? r2.y : 1.0f;
-                const v2f rinv   = {rsqrtf(r2.x), rsqrtf(r2.y)};
-                const v2f vxij = vxi2 - VX, vyij = vyi2 - VY, vzij = vzi2 - VZ;
-                const v2f hjInv2 = PW * PW;
-                const v2f hjInv3 = hjInv2 * PW;
-                const v2f valid  = {1.0f, two ? 1.0f : 0.0f};
-                const v2f Wi     = hiInv3_2 * kernelWt2(r2 * hiInv2_2) * valid;
-                const v2f Wj     = hjInv3 * kernelWt2(r2 * hjInv2) * valid;
-                const v2f u1i = c11 * rx + c12 * ry + c13 * rz;
-                const v2f u2i = c12 * rx + c22 * ry + c23 * rz;
-                const v2f u3i = c13 * rx + c23 * ry + c33 * rz;
-                const v2f u1j = AY * rx + AZ * ry + AW * rz;
-                const v2f u2j = AZ * rx + BX * ry + BY * rz;
-                const v2f u3j = AW * rx + BY * ry + BZ * rz;
-                const v2f rv  = rx * vxij + ry * vyij + rz * vzij;
-                const v2f wij = rv * rinv;
-                const v2f cij = ci2 + VW;
-                const v2f vs  = (alpha2 + AX) * v2f{0.25f, 0.25f} * cij - v2f{2.0f, 2.0f} * wij;
-                const v2f hv0 = v2f{-0.5f, -0.5f} * vs * wij;
-                const v2f halfVisc = {wij.x < 0.0f ? hv0.x : 0.0f, wij.y < 0.0f ? hv0.y : 0.0f};
-                const v2f vsig = v2f{0.5f, 0.5f} * cij - v2f{2.0f, 2.0f} * wij;
-                maxvsignali    = vsig.x > maxvsignali ? vsig.x : maxvsignali;
-                maxvsignali    = (two && vsig.y > maxvsignali) ? vsig.y : maxvsignali;
-                // the common Atwood branch when no lane's pair reaches Atmin: |drho| >= AtminLo srho compared squared
-                const v2f drho = rhoi2 - TZ, srho = rhoi2 + TZ;
-                const v2f dd = drho * drho, ss = srho * srho * v2f{AtminLo2, AtminLo2};
-                v2f       a_mom, b_mom;
-                if (__ballot(dd.x >= ss.x || (two && dd.y >= ss.y)) == 0)
-                {
-                    a_mom = xmi2v;
-                    b_mom = TY * TY;
-                }
-                else
-                {
-                    float am0, bm0, am1, bm1;
-                    atwoodWeights(fabsf(drho.x) * __frcp_rn(srho.x), Atmin, Atmax, ramp, xmassi, lxi, TY.x, am0, bm0);
-                    atwoodWeights(fabsf(drho.y) * __frcp_rn(srho.y), Atmin, Atmax, ramp, xmassi, lxi, TY.y, am1, bm1);
-                    a_mom = v2f{am0, am1}, b_mom = v2f{bm0, bm1};
-                }
-                const v2f a_visc = TX * rhoiInv2 * halfVisc;
-                const v2f b_visc = BW * halfVisc;
-                const v2f mom_i  = TX * prhoi2 * a_mom;
-                const v2f mom_j  = TW * b_mom;
-                const v2f di     = -Wi * (vxij * u1i + vyij * u2i + vzij * u3i);
-                const v2f dj     = -Wj * (vxij * u1j + vyij * u2j + vzij * u3j);
-                sE += TX * a_mom * di;
-                sV += a_visc * di + b_visc * dj;
-                const v2f ki = -(mom_i + a_visc) * Wi, kj = -(mom_j + b_visc) * Wj;
-                sMx += ki * u1i + kj * u1j;
-                sMy += ki * u2i + kj * u2j;
-                sMz += ki * u3i + kj * u3j;
-                if (++w >= cu.wEnd) break;
-            }
-            mx += sMx.x + sMx.y, my += sMy.x + sMy.y, mz += sMz.x + sMz.y;
-            energy += sE.x + sE.y, a_visc_energy += sV.x + sV.y;
-        }
-        else
-#endif
         neighborLoop<CH, SPLIT, false, SX_ME_LEAN>(
             cu, [&](uint32_t j, uint32_t slot) { stageRaw(meLoadRaw<AVC>(a, j), slot); }, loadRec, computeOne,
             res);
@@ -1308,7 +1048,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         loadRecords(nxt, rr);
         {
             float v[6] = {mx, my, mz, energy, a_visc_energy, maxvsignali};
-            combineShares<SPLIT>(cu, v, SOA ? &sF[0][0] : reinterpret_cast<float*>(sP), 32u, true);
+            combineShares<SPLIT>(cu, v, reinterpret_cast<float*>(sP), 32u, true);
             mx = v[0], my = v[1], mz = v[2], energy = v[3], a_visc_energy = v[4], maxvsignali = v[5];
         }
         float dt_lane = INFINITY;

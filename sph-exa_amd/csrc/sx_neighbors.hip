@@ -41,6 +41,7 @@
  * range b % 8 and steals from the other ranges when its own is done): consecutive clusters share neighbors in the
  * XCD's L2, and every workgroup owns a fixed slot of the hit-mask scratch.
  */
+#include "sx_skin.hpp"
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
@@ -86,30 +87,6 @@ __device__ __forceinline__ void storeList(uint32_t* p, uint32_t w)
     else *p = w;
 }
 
-#ifndef SX_NS_PROBE
-#define SX_NS_PROBE 0
-#endif
-#if SX_NS_PROBE
-//! phase cycle counters of the search (probe builds only): [0] regions, [1] tree walk, [2] scan + reach, [3] stream
-//! and test, [4] h-iteration vote, [5] union, [6] early-entry rewrite + final expansion, [7] tail; [8] waves;
-//! read from the host through the symbol (scripts/search_probe.py)
-__device__ unsigned long long g_nsProbe[16];
-#ifdef SX_NS_SMALL
-#define SX_PROBE_FN sx_debug_ns_probe_small
-#else
-#define SX_PROBE_FN sx_debug_ns_probe_large
-#endif
-//! probe builds only (not part of the C-ABI): copy the counters out (reset: and zero them)
-extern "C" __attribute__((visibility("default"))) int SX_PROBE_FN(unsigned long long* out, int reset);
-#define SX_PROBE(k)                                                                                                    \
-    {                                                                                                                  \
-        const unsigned long long t_ = __builtin_readcyclecounter();                                                    \
-        prAcc[k] += t_ - prT;                                                                                          \
-        prT = t_;                                                                                                      \
-    }
-#else
-#define SX_PROBE(k)
-#endif
 
 __device__ __forceinline__ uint32_t bitRank(const uint32_t* bits, const uint32_t* pre, uint32_t idx)
 {
@@ -294,10 +271,6 @@ findNeighborsKernel(NsArgs a)
     // this workgroup's work item: a cluster, or a position in the redo list (uniform: the cluster's origin, list and
     // scratch addresses are then scalar)
     uint32_t ci = __builtin_amdgcn_readfirstlane(s_next);
-#if SX_NS_PROBE
-    unsigned long long prAcc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prT = __builtin_readcyclecounter(), prWaves = 0;
-    unsigned long long prCnt[6] = {0, 0, 0, 0, 0, 0}; // blocks, streamed, staged, chunks, exact chunks, test cycles
-#endif
     while (ci < numClusters)
     {
     const uint32_t c = a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[1 + ci]) : ci;
@@ -313,7 +286,9 @@ findNeighborsKernel(NsArgs a)
     const uint32_t iSafe = valid ? i : c0; // positions only: the cluster's first particle is always in range
     const double   xi = a.x[iSafe], yi = a.y[iSafe], zi = a.z[iSafe];
     const double   ox = a.x[c0], oy = a.y[c0], oz = a.z[c0]; // cluster origin of the float prefilter
-    float          hi = a.h[iSafe];
+    // skin builds (sx_skin.hpp) search within 2 h (1 + s): every radius of this kernel scales with hi, and a skin
+    // build neither iterates h nor writes it
+    float          hi = a.skin1 > 0.0f ? a.h[iSafe] * a.skin1 : a.h[iSafe];
 
     const bool     local = a.localLists != 0;
     uint32_t*      gl    = a.nidx + (size_t)g * a.ngmax * kWave + lane;
@@ -450,7 +425,6 @@ findNeighborsKernel(NsArgs a)
     bool abandoned = false;
     while (true)
     {
-        SX_PROBE(7)
         // ---- 1./2. search regions, then the candidate leaves within reach of one, numbered into the candidate space
         if (threadIdx.x == 0) s_nreg = 0;
         __syncthreads();
@@ -527,7 +501,6 @@ findNeighborsKernel(NsArgs a)
             }
             return bits;
         };
-        SX_PROBE(0)
         bool      overflow = false;
         const int nCand    = clusterCollectLeaves(
             a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, s_bfsCnt, wave,
@@ -584,7 +557,6 @@ findNeighborsKernel(NsArgs a)
             abandoned = true; // nothing of this cluster is written: h, nc, lists and union stay for the redo
             break;
         }
-        SX_PROBE(1)
         // which waves may reach which candidate leaf: leaf box vs wave box grown by the wave's search radius
         // (conservative; replaces a per-lane test inside the stream, so the stream touches no tree data)
         for (int cc = threadIdx.x; cc < numCand; cc += kCluster)
@@ -600,7 +572,6 @@ findNeighborsKernel(NsArgs a)
         }
         __syncthreads(); // the regions (aliasing the stream LDS) are no longer read
 
-        SX_PROBE(2)
         // ---- 3. stream candidates, test against each lane's own particle ------------------------------
         const float  r2f    = 4.0f * hi * hi;
         const double radSq  = (double)r2f;
@@ -704,9 +675,6 @@ findNeighborsKernel(NsArgs a)
 
         // test the fill staged slots of table row nq: hit mask -> count, union bitmap, the batch (or global lists)
         auto testChunk = [&]() {
-#if SX_NS_PROBE
-            const unsigned long long tc0_ = __builtin_readcyclecounter();
-#endif
             const int m = fill;
             candTested += m;
             uint16_t* tq = wl.tab[nq];
@@ -757,10 +725,6 @@ findNeighborsKernel(NsArgs a)
                 }
             }
             if (exact) hm = exactChunk(m, tq);
-#if SX_NS_PROBE
-            prCnt[3]++;
-            prCnt[4] += exact ? 1 : 0;
-#endif
             const uint32_t sd = selfSeq - seq;
             if (sd < (uint32_t)m) hm &= ~(1ull << sd); // j != i
             const unsigned nh = __popcll(hm);
@@ -806,9 +770,6 @@ findNeighborsKernel(NsArgs a)
             seq += m;
             fill = 0;
             __builtin_amdgcn_wave_barrier(); // every lane's slot reads precede the next staging writes
-#if SX_NS_PROBE
-            prCnt[5] += __builtin_readcyclecounter() - tc0_;
-#endif
         };
 
         // blocks of up to 64 consecutive particles of the reachable candidate leaves, in candidate order; the next
@@ -891,11 +852,6 @@ findNeighborsKernel(NsArgs a)
             }
             const uint64_t bm = __ballot(pass);
             const int      n  = __popcll(bm);
-#if SX_NS_PROBE
-            prCnt[0]++;
-            prCnt[1] += __popcll(__ballot(in));
-            prCnt[2] += n;
-#endif
             if (fill + n > kWave) testChunk();
             if (pass)
             {
@@ -925,7 +881,6 @@ findNeighborsKernel(NsArgs a)
             cur = nxt, cx = nx, cy = ny, cz = nz;
         }
 
-        SX_PROBE(3)
         // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33) ----------------------------------------
         bool again = false;
         if (a.iterateH)
@@ -950,7 +905,6 @@ findNeighborsKernel(NsArgs a)
         int any = 0;
         for (int w = 0; w < kClusterWaves; ++w)
             any |= s_again[w];
-        SX_PROBE(4)
         if (!any) break;
         __syncthreads(); // s_again / candidate space / regions are rewritten by the next iteration
     }
@@ -998,7 +952,7 @@ findNeighborsKernel(NsArgs a)
             run += __popc(mine(w));
         }
         // union entries: candidate index -> global index, through the leaf it belongs to
-        uint32_t* uni = a.uni + (size_t)c * a.ucap;
+        uint32_t* uni = a.uni + (size_t)c * a.ucap + a.uoff; // a skin build's union: the slot's upper part
         run           = off + incl - sum;
         // first candidate leaf of this thread's run by binary search (s_cOff ascending), then walk forward
         int cc = 0;
@@ -1021,13 +975,13 @@ findNeighborsKernel(NsArgs a)
                 bits &= bits - 1u;
                 while (s_cOff[cc + 1] <= idx)
                     ++cc;
-                if (run < a.ucap) uni[run] = s_p0[cc] + (idx - s_cOff[cc]);
-                else atomicOr(&a.stats[0], 1u | 8u); // union larger than its capacity (bit 8)
+                if (run < a.ucap - a.uoff) uni[run] = s_p0[cc] + (idx - s_cOff[cc]);
+                else if (!(a.skin1 > 0.0f)) atomicOr(&a.stats[0], 1u | 8u); // union beyond its capacity (bit 8);
+                // a skin build records the true size (ucount) instead: the filter sends such a cluster to the exact search
                 ++run;
             }
         }
         __syncthreads(); // s_pre complete
-        SX_PROBE(5)
         // the last batch's chunk tables -> union positions
         for (int q = 0; q < nq; ++q)
         {
@@ -1067,7 +1021,6 @@ findNeighborsKernel(NsArgs a)
         __syncthreads(); // the candidate space and the union bitmap are dead: the masks take their bytes
         // the last batch: union positions straight into the lists (the early entries' last pending half included)
         expandFinal();
-        SX_PROBE(6)
         if (stored & 1u) ll[(size_t)(stored >> 1) * kWave] = pend;
     }
 
@@ -1103,34 +1056,9 @@ findNeighborsKernel(NsArgs a)
     }
     __syncthreads(); // LDS is reused by the next cluster (s_next was written before this barrier)
     ci = __builtin_amdgcn_readfirstlane(s_next);
-#if SX_NS_PROBE
-    ++prWaves;
-#endif
     }
-#if SX_NS_PROBE
-    SX_PROBE(7)
-    if (lane == 0)
-    {
-        for (int k = 0; k < 8; ++k)
-            atomicAdd(&g_nsProbe[k], prAcc[k]);
-        atomicAdd(&g_nsProbe[8], prWaves);
-        for (int k = 0; k < 6; ++k)
-            atomicAdd(&g_nsProbe[9 + k], prCnt[k]);
-    }
-#endif
 }
 
-#if SX_NS_PROBE
-extern "C" int SX_PROBE_FN(unsigned long long* out, int reset)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nsProbe), sizeof(g_nsProbe), 0, hipMemcpyDeviceToHost) != hipSuccess)
-        return 1;
-    const unsigned long long z[16] = {};
-    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_nsProbe), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
-        return 1;
-    return 0;
-}
-#endif
 
 //! lane-interleaved lists (either format) -> row-major global lists out[(i-first)*ngmax + k]
 __global__ void exportKernel(NsArgs a, uint32_t* out)
@@ -1204,42 +1132,9 @@ size_t     searchScratchWords();
 
 size_t searchScratchBytes() { return std::max(searchScratchWords(), small::searchScratchWords()) * sizeof(uint64_t); }
 
-//! per-cluster statistics -> stats[2] (max count), u64 stats[4] (stored), [6] (tested), [8] (union entries),
-//! stats[12] (largest union)
-__global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
-{
-    __shared__ uint32_t           s_max[2][16];
-    __shared__ unsigned long long s_sum[3][16];
-    uint32_t                      mx = 0, mu = 0;
-    unsigned long long            st = 0, te = 0, un = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-    {
-        const uint4 v = cl[i];
-        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w, mu = max(mu, v.w);
-    }
-    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
-        s_max[0][w] = mx, s_max[1][w] = mu, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
-    __syncthreads();
-    if (threadIdx.x == 0)
-    {
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), st += s_sum[0][k], te += s_sum[1][k],
-            un += s_sum[2][k];
-        stats[2]                                            = mx;
-        stats[12]                                           = mu;
-        *reinterpret_cast<unsigned long long*>(stats + 4) = st;
-        *reinterpret_cast<unsigned long long*>(stats + 6) = te;
-        *reinterpret_cast<unsigned long long*>(stats + 8) = un;
-    }
-}
-
 static hipError_t reduceClusterStats(const NsArgs& a, hipStream_t s)
 {
-    const uint32_t clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    reduceClusterStatsKernel<<<1, 1024, 0, s>>>(a.clStats, clusters, a.stats);
-    return hipGetLastError();
+    return reduceClusterStats(a.clStats, (a.numGroups + kClusterWaves - 1) / kClusterWaves, a.stats, s);
 }
 
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
@@ -1251,7 +1146,9 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
     const int mode = a.policy ? a.policy->mode : 1;
     if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge()))
     {
-        if ((e = findNeighborsOnce(a, s))) return e;
+        NsArgs l   = a;
+        l.redoList = a.subset; // only the listed clusters, or all
+        if ((e = findNeighborsOnce(l, s))) return e;
         return reduceClusterStats(a, s);
     }
     // compact build first: a cluster over its capacities is not written and goes to a redo list (in the hSave
@@ -1262,6 +1159,7 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
     NsArgs c        = a;
     c.forceOverflow = mode == 3;
     c.redo          = redo;
+    c.redoList      = a.subset;
     if ((e = small::findNeighborsOnce(c, s))) return e;
     NsArgs b   = a;
     b.redoList = redo;

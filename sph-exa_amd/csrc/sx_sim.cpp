@@ -39,6 +39,7 @@
 #include "sx_hydro.hpp"
 #include "sx_observables.hpp"
 #include "sx_sim.hpp"
+#include "sx_skin.hpp"
 #include "sx_traverse.hpp"
 #include "sx_tree.hpp"
 
@@ -1420,6 +1421,159 @@ void maxAccSq(sx_sim* s, hipStream_t st)
                                                                           &s->sc->maxAccSqBits);
 }
 
+//! skin lists serve this sim: one rank, no self-gravity (its tree is rebuilt every step), not ve-bdt, cluster lists
+bool skinUsable(const sx_sim* s)
+{
+    return s->skin.factor > 0.0f && !(s->comm && s->comm->size() > 1) && s->p.g == 0.0 && s->p.propagator != 2 &&
+           NbLists::localPossible(s->p.ngmax);
+}
+
+//! the displacement grid over the box: kSkinGridN cells per axis
+SkinGrid skinGrid(const DevBox& b)
+{
+    SkinGrid g{};
+    g.n = kSkinGridN;
+    for (int d = 0; d < 3; ++d)
+    {
+        g.lo[d]  = b.lim[2 * d];
+        g.inv[d] = (double)kSkinGridN / b.l[d];
+        g.pbc[d] = b.pbc[d];
+    }
+    return g;
+}
+
+//! skin-list capacity per target: the neighbor capacity scaled by the skin volume, with room for density variation
+uint32_t skinCapacity(uint32_t ngmax, float factor)
+{
+    const double f = std::pow(1.0 + factor, 3.0) * 1.15;
+    const uint32_t c = (uint32_t)std::ceil(ngmax * f);
+    return std::min<uint32_t>(256u, (c + 1u) & ~1u);
+}
+
+//! the skin arrays the position update feeds: per particle the path length and this step's displacement, the grid
+//! of per-step displacement maxima by cell (zeroed here: the update scatters into it)
+bool skinParticleBuffers(sx_sim* s, PosArgs& q, hipStream_t st)
+{
+    q.disp  = s->mem.get<float>("skin.disp", s->cap);
+    q.odo   = s->mem.get<float>("skin.odo", s->cap);
+    q.cells = s->mem.get<uint32_t>("skin.cells", (size_t)kSkinGridN * kSkinGridN * kSkinGridN);
+    q.grid  = skinGrid(s->dbox);
+    if (!q.disp || !q.odo || !q.cells) return false;
+    return hipMemsetAsync(q.cells, 0, sizeof(uint32_t) * kSkinGridN * kSkinGridN * kSkinGridN, st) == hipSuccess;
+}
+
+/*! The step's neighbor search through skin lists (sx_skin.hpp).  A full build (after a full sync) builds every
+ *  cluster's skin and filters it; a reuse step only filters.  Stale clusters are rebuilt at once on node boxes refreshed
+ *  from the current positions (reuse steps) and filtered; clusters stale again take the exact search.  na: the step's
+ *  search arguments (exact lists, h, nc, tree).  One host read of the stale count, two when some cluster is stale. */
+int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
+{
+    auto&          K   = s->skin;
+    const uint32_t ncl = (na.numGroups + kClusterWaves - 1) / kClusterWaves;
+    if (!ncl) return SX_OK;
+    K.ngmaxS      = skinCapacity(s->p.ngmax, K.factor);
+    const size_t G    = kSkinGridN;
+    float*       odo  = s->mem.get<float>("skin.odo", s->cap);
+    uint32_t*   sloc = s->mem.get<uint32_t>("skin.sloc", na.numGroups * (size_t)nlocWords(K.ngmaxS) * kWave);
+    uint32_t*   scnt = s->mem.get<uint32_t>("skin.scnt", s->cap);
+    float*      hb   = s->mem.get<float>("skin.hb", s->cap);
+    float*      ob   = s->mem.get<float>("skin.ob", s->cap);
+    float*      acc  = s->mem.get<float>("skin.acc", ncl);
+    uint32_t*   cells = s->mem.get<uint32_t>("skin.cells", G * G * G);
+    uint32_t*   ucS   = s->mem.get<uint32_t>("skin.ucount", ncl);
+    uint32_t*   l1    = s->mem.get<uint32_t>("skin.l1", ncl + 1);
+    uint32_t*   l2    = s->mem.get<uint32_t>("skin.l2", ncl + 1);
+    uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 2);
+    if (!odo || !sloc || !scnt || !hb || !ob || !acc || !cells || !ucS || !l1 || !l2 || !hl) return SX_ERR_NOMEM;
+
+    const SkinGrid g = skinGrid(s->dbox);
+    SkinArgs fa{};
+    fa.first = na.first, fa.last = na.last, fa.numGroups = na.numGroups, fa.ngmax = na.ngmax, fa.ng0 = na.ng0;
+    fa.ngmaxS = K.ngmaxS, fa.iterateH = na.iterateH, fa.skin1 = 1.0f + K.factor;
+    fa.x = na.x, fa.y = na.y, fa.z = na.z, fa.h = na.h, fa.m = na.m, fa.nc = na.nc, fa.rxOut = na.rxOut;
+    // the skin union lives in the upper half of each cluster's union slot, the exact union (the pair kernels') at its
+    // start
+    const uint32_t uoff = na.ucap / 2;
+    fa.nloc = na.nloc, fa.uni = na.uni, fa.ucount = na.ucount, fa.ucap = na.ucap, fa.uoff = uoff, fa.ucountS = ucS;
+    fa.sloc = sloc, fa.scnt = scnt, fa.hb = hb, fa.ob = ob, fa.odo = odo, fa.acc = acc, fa.cells = cells, fa.grid = g;
+    fa.box = na.box, fa.powTab = na.powTab, fa.stats = na.stats, fa.clStats = na.clStats;
+
+    // the skin build: the search with radii 2 h (1 + s), no h iteration, skin lists and counts as its outputs
+    NsArgs b   = na;
+    b.skin1    = 1.0f + K.factor;
+    b.iterateH = 0;
+    b.nloc     = sloc;
+    b.ngmax    = K.ngmaxS;
+    b.nc       = scnt;
+    b.rxOut    = nullptr;
+    b.uoff     = uoff;
+    b.ucount   = ucS;
+
+    SIM_HIP(hipMemsetAsync(l1, 0, 4, st));
+    SIM_HIP(hipMemsetAsync(l2, 0, 4, st));
+    if (!reuse)
+    {
+        SIM_HIP(hipMemsetAsync(odo, 0, 4 * s->cap, st));
+        SIM_HIP(findNeighbors(b, st));
+        fa.fresh = 1;
+    }
+    else fa.fresh = 0; // the grid of this step's displacements came from the last position update
+    fa.list  = nullptr;
+    fa.stale = l1;
+    SIM_HIP(skinFilter(fa, ncl, st));
+    SIM_HIP(hipMemcpyAsync(hl, l1, 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    const uint32_t n1 = hl[0];
+    uint32_t       n2 = 0;
+    if (n1)
+    {
+        NsArgs x = na; // the exact search, for clusters whose h iteration outgrows even a fresh skin
+        if (reuse)
+        {
+            // particles have left the cells of the last full sync's tree: the walk takes boxes of the current positions
+            double* c3 = s->mem.get<double>("skin.centers", 3 * (size_t)s->tree.numNodes);
+            double* s3 = s->mem.get<double>("skin.sizes", 3 * (size_t)s->tree.numNodes);
+            if (!c3 || !s3) return SX_ERR_NOMEM;
+            SIM_HIP(skinRefreshBoxes(s->tree, na.x, na.y, na.z, na.box, c3, s3, st));
+            b.centers = x.centers = c3;
+            b.sizes = x.sizes = s3;
+        }
+        b.subset = l1;
+        SIM_HIP(findNeighbors(b, st));
+        fa.fresh = 1;
+        fa.list  = l1;
+        fa.stale = l2;
+        SIM_HIP(skinFilter(fa, ncl, st));
+        SIM_HIP(hipMemcpyAsync(hl + 1, l2, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        n2 = hl[1];
+        if (n2)
+        {
+            x.subset = l2;
+            SIM_HIP(findNeighbors(x, st));
+            SIM_HIP(skinMarkStale(l2, ncl, acc, st)); // their skins are rebuilt next step
+        }
+    }
+    SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
+    K.lastStale = n1, K.lastExact = n2;
+    K.staleClusters += n1, K.exactClusters += n2;
+    if (reuse)
+    {
+        K.reuseSteps++;
+        K.sinceBuild++;
+    }
+    else
+    {
+        K.builds++;
+        K.valid      = true;
+        K.forceBuild = false;
+        K.sinceBuild = 0;
+    }
+    // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once
+    if ((double)n1 > K.staleLimit * ncl) K.forceBuild = true;
+    return SX_OK;
+}
+
 int localSync(sx_sim* s, hipStream_t st)
 {
     const size_t n = s->n;
@@ -1498,6 +1652,7 @@ extern "C"
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
         s->keysFresh  = false;
+        s->skin.valid = false;
         s->comm       = sx_comm_transport_internal(c);
         s->commHandle = c;
         return SX_OK;
@@ -1516,6 +1671,44 @@ extern "C"
         return SX_OK;
     }
 
+    int sx_sim_set_skin(sx_sim* s, float factor, int maxReuse)
+    {
+        if (!s || !(factor >= 0.0f) || factor > 1.0f || maxReuse < 1) return SX_ERR_ARG;
+        s->skin.factor   = factor;
+        s->skin.maxReuse = maxReuse;
+        s->skin.valid    = false;
+        return SX_OK;
+    }
+
+    int sx_sim_rebuild_lists(sx_sim* s)
+    {
+        if (!s) return SX_ERR_ARG;
+        s->skin.forceBuild = true;
+        return SX_OK;
+    }
+
+    int sx_sim_skin_stats(sx_sim* s, uint64_t out[8])
+    {
+        if (!s) return SX_ERR_ARG;
+        const auto& K = s->skin;
+        out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
+        out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = (uint64_t)K.sinceBuild;
+        return SX_OK;
+    }
+
+    int sx_sim_export_neighbors(sx_sim* s, uint32_t* out)
+    {
+        if (!s || !out) return SX_ERR_ARG;
+        if (s->nb.first != s->first || s->nb.last != s->last || s->nb.ngmax != s->p.ngmax) return SX_ERR_ARG;
+        NsArgs a{};
+        a.first = (uint32_t)s->first, a.last = (uint32_t)s->last, a.ngmax = s->p.ngmax, a.nc = s->nc;
+        a.setLists(s->nb);
+        hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
+        SIM_HIP(exportNeighbors(a, out, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        return SX_OK;
+    }
+
     size_t sx_sim_size(sx_sim* s) { return s->last - s->first; }
 
     int sx_sim_layout(sx_sim* s, uint64_t out[4])
@@ -1529,7 +1722,8 @@ extern "C"
 
     int sx_sim_init_sedov_rank(sx_sim* s, uint32_t side, int rank, int size)
     {
-        s->keysFresh = false;
+        s->keysFresh  = false;
+        s->skin.valid = false;
         size_t N  = (size_t)side * side * side;
         size_t f  = N * rank / size, l = N * (rank + 1) / size;
         size_t n  = l - f;
@@ -1562,7 +1756,8 @@ extern "C"
                          const float* x_m1, const float* y_m1, const float* z_m1, const float* du_m1,
                          const float* alpha, const uint64_t* id, double minDt, double minDt_m1)
     {
-        s->keysFresh = false;
+        s->keysFresh  = false;
+        s->skin.valid = false;
         if (n > s->cap) return SX_ERR_ARG;
         if (s->p.propagator == 2)
         {   // ve-bdt carries the rung in the id's top byte through the particle exchange (PRec): ids must fit 56 bits
@@ -1716,6 +1911,11 @@ extern "C"
         int                ev  = 0;
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
 
+        // skin lists (sx_skin.hpp): a reuse step keeps the order and tree of the last full build and filters the
+        // skin lists instead of syncing and searching
+        const bool skinOn = !dist && skinUsable(s);
+        const bool reuse  = skinOn && s->skin.valid && !s->skin.forceBuild && s->skin.sinceBuild < s->skin.maxReuse;
+        if (!skinOn) s->skin.valid = false;
         // h before the h iteration, to redo the search if the halo margin proves too small
         float* h0     = dist ? s->work.get<float>("h0", s->cap) : nullptr;
         double margin = kHaloMargin;
@@ -1736,7 +1936,7 @@ extern "C"
                 }
                 SIM_HIP(hipMemcpyAsync(h0, s->h + s->first, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
             }
-            else if (attempt == 0)
+            else if (attempt == 0 && !reuse)
             {
                 if (int e = localSync(s, st)) return e;
             }
@@ -1799,7 +1999,11 @@ extern "C"
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));
-            SIM_HIP(findNeighbors(na, st));
+            if (skinOn)
+            {
+                if (int e = skinSearch(s, na, reuse, st)) return e;
+            }
+            else SIM_HIP(findNeighbors(na, st));
             SIM_HIP(hipEventRecord(s->kev[1], st));
             SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
             if (s->evStats) SIM_HIP(hipEventRecord(s->evStats, st));
@@ -2071,6 +2275,7 @@ extern "C"
         qa.constCv = idealGasCv(s->p.muiConst, s->p.gamma);
         // one rank: the next localSync's keys come from this pass (the coordinates are in registers here)
         qa.keys    = (!dist && s->p.propagator != 2) ? s->keys : nullptr;
+        if (skinOn && !skinParticleBuffers(s, qa, st)) return SX_ERR_NOMEM;
         H.positions(qa, st);
         s->keysFresh = qa.keys != nullptr;
         H.updateH((uint32_t)s->first, (uint32_t)s->last, s->p.ng0, s->nc, s->h, na.powTab, st);

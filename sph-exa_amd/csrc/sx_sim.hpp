@@ -62,6 +62,22 @@ struct BdtState
     uint64_t    substeps{0};
 };
 
+//! skin-list reuse of the neighbor search (sx_skin.hpp), one rank without self-gravity: between full builds the
+//! particle order and tree are kept and each step's search is the filter of the last build's skin lists
+struct SkinState
+{
+    float    factor{0.08f};     // s: skin radius 2 h (1 + s); 0 = every step syncs and searches (the reference's flow)
+    int      maxReuse{24};      // steps after a full build before the next one at the latest
+    float    staleLimit{0.125f}; // share of stale clusters in a step after which the next step does a full build
+    bool     valid{false};      // every cluster's skin lists are current (a full build since the last state change)
+    bool     forceBuild{false};
+    int      sinceBuild{0};
+    uint32_t ngmaxS{0};         // skin-list capacity per target
+    // statistics: full builds, steps served by the filter, clusters rebuilt (stale), clusters sent to the exact search
+    uint64_t builds{0}, reuseSteps{0}, staleClusters{0}, exactClusters{0};
+    uint32_t lastStale{0}, lastExact{0};
+};
+
 } // namespace sx::sim
 
 struct sx_sim
@@ -154,6 +170,7 @@ struct sx_sim
     uint64_t                 gravRemoteCells{0};
 
     sx::sim::BdtState bdt; // propagator 2 only
+    sx::sim::SkinState skin;
 
     Fields fields() const { return Fields{x, y, z, temp, h, m, vx, vy, vz, xm1, ym1, zm1, dum1, alpha, id, rung}; }
 };

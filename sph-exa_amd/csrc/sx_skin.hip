@@ -1,0 +1,556 @@
+/*! @file sx_skin.hip
+ * @brief Skin-list reuse of the neighbor search on gfx950 (see sx_skin.hpp): displacement grid, node-box refresh,
+ *        and the filter that turns the last build's skin lists into the step's exact lists.
+ *
+ * The filter replaces the step's search (cstone::findNeighbors + sph::findNeighborsSph, findneighbors.hpp:95-188,
+ * find_neighbors.hpp:10-44) for every cluster whose skin is still valid.  One 256-thread workgroup per cluster:
+ *   1. validity: each target's drift bound against its skin (sx_skin.hpp); the region's per-step displacement maximum
+ *      comes from the grid cells around the wave boxes;
+ *   2. the cluster's skin union U_s is staged in LDS as float positions relative to the cluster origin (minimum image,
+ *      folded in double) with |p|^2, and the global indices;
+ *   3. every lane walks its skin list (two u16 positions per word, prefetched) and tests each entry with the packed
+ *      form of the search, t = |p|^2 + (|r|^2 - 4h^2) - 2 p.r in float, an error bound deciding when the reference's
+ *      double criterion d2 < (double)(4h^2) must be evaluated (x, y, z from global memory) -- so the neighbor set is
+ *      bit-identical to findNeighbors; j != i by global index;
+ *   4. lanes with nc outside [ng0/4, ngmax+1] update h and walk again (at most 10 updates, the CPU loop's bound); an
+ *      updated h must stay within the skin, else the cluster is stale;
+ *   5. h, nc, the targets' RecX and the exact lists (ascending positions into U_s, first ngmax in stream order) are
+ *      written only by a cluster that completes.
+ * This file is compiled with -ffp-contract=off (the double criterion must round like the reference).
+ */
+#include "sx_skin.hpp"
+#include "sx_traverse.hpp"
+
+namespace sx
+{
+
+namespace
+{
+
+constexpr int kSkinCap = 1920; //!< U_s entries staged (16 B each; a larger skin union takes the exact search)
+constexpr int kWalkPF  = 8;    //!< skin-list words per walk block (16 entries: one u16 of hit bits per lane)
+//! walk blocks per lane at the largest skin-list capacity (256 entries)
+constexpr int kWalkBlocks = (nlocWords(256) + kWalkPF - 1) / kWalkPF;
+constexpr int kB       = kCluster;
+
+__device__ __forceinline__ int cellIndex(double v, const SkinGrid& g, int d) { return gridCell(v, g, d); }
+
+//! leaf boxes from their particles (relative to the geometric center, minimum image), one wave per leaf node
+__global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* internalToLeaf, const uint32_t* layout,
+                              int numNodes, const double* gc, const double* gs, const double* x, const double* y,
+                              const double* z, DevBox box, double* centers, double* sizes)
+{
+    const int node = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (node >= numNodes || childOffsets[node] != 0) return;
+    const int      leaf = internalToLeaf[node];
+    const uint32_t p0 = layout[leaf], p1 = layout[leaf + 1];
+    const double   c[3] = {gc[3 * node], gc[3 * node + 1], gc[3 * node + 2]};
+    double         lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t j = p0 + lane; j < p1; j += kWave)
+    {
+        const double q[3] = {x[j], y[j], z[j]};
+        for (int d = 0; d < 3; ++d)
+        {
+            const double r = foldPbc(q[d] - c[d], box, d);
+            lo[d]          = fmin(lo[d], r);
+            hi[d]          = fmax(hi[d], r);
+        }
+    }
+    for (int d = 0; d < 3; ++d)
+    {
+        lo[d] = -waveMax(-lo[d]);
+        hi[d] = waveMax(hi[d]);
+    }
+    if (lane == 0)
+    {
+        for (int d = 0; d < 3; ++d)
+        {
+            // an empty leaf keeps its cell (it contributes no candidates either way)
+            const bool   empty = p1 <= p0;
+            const double m     = empty ? 0.0 : 0.5 * (lo[d] + hi[d]);
+            const double s     = empty ? gs[3 * node + d] : 0.5 * (hi[d] - lo[d]);
+            centers[3 * node + d] = c[d] + m;
+            sizes[3 * node + d]   = s;
+        }
+    }
+}
+
+//! inner boxes of one level from their eight children (folded relative to the node's geometric center)
+__global__ void innerBoxKernel(const int32_t* childOffsets, int b, int e, const double* gc, DevBox box, double* centers,
+                               double* sizes)
+{
+    const int node = b + blockIdx.x * blockDim.x + threadIdx.x;
+    if (node >= e) return;
+    const int c0 = childOffsets[node];
+    if (c0 == 0) return;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = c0; k < c0 + 8; ++k)
+        for (int d = 0; d < 3; ++d)
+        {
+            const double r = foldPbc(centers[3 * k + d] - gc[3 * node + d], box, d);
+            lo[d]          = fmin(lo[d], r - sizes[3 * k + d]);
+            hi[d]          = fmax(hi[d], r + sizes[3 * k + d]);
+        }
+    for (int d = 0; d < 3; ++d)
+    {
+        centers[3 * node + d] = gc[3 * node + d] + 0.5 * (lo[d] + hi[d]);
+        sizes[3 * node + d]   = 0.5 * (hi[d] - lo[d]);
+    }
+}
+
+__global__ void markStaleKernel(const uint32_t* list, uint32_t numClusters, float* acc)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < list[0] && k < numClusters) acc[list[1 + k]] = INFINITY;
+}
+
+__global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
+{
+    __shared__ uint32_t           s_max[2][16];
+    __shared__ unsigned long long s_sum[3][16];
+    uint32_t                      mx = 0, mu = 0;
+    unsigned long long            st = 0, te = 0, un = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    {
+        const uint4 v = cl[i];
+        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w, mu = max(mu, v.w);
+    }
+    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_max[0][w] = mx, s_max[1][w] = mu, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), st += s_sum[0][k], te += s_sum[1][k],
+            un += s_sum[2][k];
+        stats[2]                                          = mx;
+        stats[12]                                         = mu;
+        *reinterpret_cast<unsigned long long*>(stats + 4) = st;
+        *reinterpret_cast<unsigned long long*>(stats + 6) = te;
+        *reinterpret_cast<unsigned long long*>(stats + 8) = un;
+    }
+}
+
+__global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numClusters)
+{
+    // LDS: 39.9 KB, four workgroups per CU
+    __shared__ float4   s_rec[kSkinCap]; // U_s positions relative to the cluster origin, |p|^2; then the exact-union
+                                         // ranks (u16) of the U_s entries, once pass A is done with the positions
+    __shared__ uint8_t  s_hit[kSkinCap]; // U_s entry hit by some target (exact union)
+    __shared__ uint16_t s_bm[kWalkBlocks][kB]; // pass A's stored hits per walk block and lane (bit e: entry e)
+    uint16_t* const     s_rank = reinterpret_cast<uint16_t*>(s_rec);
+    __shared__ float    s_red[kClusterWaves];
+    __shared__ int      s_vote[kClusterWaves];
+    __shared__ uint32_t s_wsum[kClusterWaves];
+    __shared__ uint4    s_cst[kClusterWaves];
+
+    const uint32_t nWork = a.list ? __builtin_amdgcn_readfirstlane(a.list[0]) : numClusters;
+    if (blockIdx.x >= nWork) return;
+    const uint32_t blk  = a.list ? blockIdx.x : xcdBlock(blockIdx.x, gridDim.x);
+    const uint32_t c    = __builtin_amdgcn_readfirstlane(a.list ? a.list[1 + blk] : blk);
+    const int      wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t gw   = c * kClusterWaves + wave;
+    const uint32_t c0   = a.first + c * kCluster;
+    const uint32_t i    = c0 + threadIdx.x;
+    const bool     valid = gw < a.numGroups && i < a.last;
+    const uint32_t iS    = valid ? i : c0;
+    const double   xi = a.x[iS], yi = a.y[iS], zi = a.z[iS];
+    const double   ox = a.x[c0], oy = a.y[c0], oz = a.z[c0];
+    float          hi   = a.h[iS];
+    const float    h0   = hi;
+    const float    hbi  = a.fresh ? hi : a.hb[iS];
+    const float    odoi = a.odo[iS];
+    const float    di   = a.fresh ? 0.0f : fmaxf(0.0f, odoi - a.ob[iS]);
+    const float    Ri   = 2.0f * (hbi * a.skin1);
+    const uint32_t scount = valid ? a.scnt[i] - 1u : 0u;
+    const uint32_t U      = __builtin_amdgcn_readfirstlane(a.ucountS[c]);
+    const float    kEps   = 0x1p-16f;
+    auto           blockAny = [&](bool v) -> bool {
+        const bool w = __ballot(v) != 0;
+        if (lane == 0) s_vote[wave] = w;
+        __syncthreads();
+        bool any = false;
+        for (int k = 0; k < kClusterWaves; ++k)
+            any |= s_vote[k] != 0;
+        __syncthreads();
+        return any;
+    };
+
+    // ---- 1. the region's displacement since the build: A = acc + this step's maximum over the grid cells around
+    //         the wave boxes grown by the largest skin radius
+    float A = 0.0f;
+    if (!a.fresh)
+    {
+        const double rx = foldPbc(xi - ox, a.box, 0), ry = foldPbc(yi - oy, a.box, 1), rz = foldPbc(zi - oz, a.box, 2);
+        double       lo[3]  = {valid ? rx : INFINITY, valid ? ry : INFINITY, valid ? rz : INFINITY};
+        double       hb3[3] = {valid ? rx : -INFINITY, valid ? ry : -INFINITY, valid ? rz : -INFINITY};
+        float        rmax   = valid ? Ri : 0.0f;
+        for (int d = 0; d < 3; ++d)
+        {
+            lo[d]  = -waveMax(-lo[d]);
+            hb3[d] = waveMax(hb3[d]);
+        }
+        rmax      = waveMax(rmax);
+        float gmx = 0.0f;
+        if (rmax > 0.0f)
+        {
+            const double o[3] = {ox, oy, oz};
+            int          k0[3], nk[3];
+            long long    total = 1;
+            for (int d = 0; d < 3; ++d)
+            {
+                k0[d]  = cellIndex(o[d] + lo[d] - (double)rmax, a.grid, d);
+                int k1 = cellIndex(o[d] + hb3[d] + (double)rmax, a.grid, d);
+                nk[d]  = k1 - k0[d] + 1;
+                if (a.grid.pbc[d] && nk[d] >= a.grid.n) k0[d] = 0, nk[d] = a.grid.n;
+                total *= nk[d];
+            }
+            // a region of many cells (a wave spanning an SFC seam across the box) scans them all: rare
+            for (long long q = lane; q < total; q += kWave)
+            {
+                int       k[3];
+                long long r = q;
+                for (int d = 0; d < 3; ++d)
+                {
+                    k[d] = k0[d] + (int)(r % nk[d]);
+                    r /= nk[d];
+                    if (a.grid.pbc[d]) k[d] = wrapCell(k[d], a.grid.n);
+                }
+                gmx = fmaxf(gmx, __uint_as_float(a.cells[((size_t)k[2] * a.grid.n + k[1]) * a.grid.n + k[0]]));
+            }
+        }
+        gmx = waveMax(gmx);
+        if (lane == 0) s_red[wave] = gmx;
+        __syncthreads();
+        float g = s_red[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+            g = fmaxf(g, s_red[w]);
+        A = a.acc[c] + g;
+        __syncthreads();
+    }
+    // a target's skin holds every current neighbor while 2h + d + A <= R (1 - eps); a build that overflowed a capacity
+    // (skin list beyond ngmaxS, union beyond the slot) never serves, nor a union beyond the LDS capacity
+    auto withinSkin = [&](float h) { return 2.0f * h + di + A <= Ri * (1.0f - kEps); };
+    {
+        const bool bad = valid && (scount > a.ngmaxS || !withinSkin(hi));
+        if (blockAny(bad) || U > (uint32_t)kSkinCap || U > a.ucap - a.uoff)
+        {
+            if (threadIdx.x == 0) a.stale[1 + atomicAdd(&a.stale[0], 1u)] = c;
+            return;
+        }
+    }
+
+    // ---- 2. stage U_s: every thread's entries, all loads in flight together
+    const uint32_t* un = a.uni + (size_t)c * a.ucap + a.uoff;
+    float           pmax;
+    {
+        constexpr int S = kSkinCap / kB;
+        uint32_t      js[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+        {
+            // unconditional (clamped): a load under a condition is waited for at the branch merge
+            js[q] = un[min(threadIdx.x + q * kB, U - 1u)];
+        }
+        double px[S], py[S], pz[S];
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+            px[q] = a.x[js[q]], py[q] = a.y[js[q]], pz[q] = a.z[js[q]];
+        float pm = 0.0f;
+#pragma unroll
+        for (int q = 0; q < S; ++q)
+        {
+            const uint32_t u = threadIdx.x + q * kB;
+            if (u < U)
+            {
+                const float fx = (float)foldPbc(px[q] - ox, a.box, 0);
+                const float fy = (float)foldPbc(py[q] - oy, a.box, 1);
+                const float fz = (float)foldPbc(pz[q] - oz, a.box, 2);
+                s_rec[u]       = make_float4(fx, fy, fz, fmaf(fx, fx, fmaf(fy, fy, fz * fz)));
+                pm             = fmaxf(pm, fabsf(fx) + fabsf(fy) + fabsf(fz));
+            }
+        }
+        pm = waveMax(pm);
+        if (lane == 0) s_red[wave] = pm;
+        __syncthreads();
+        pmax = s_red[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+            pmax = fmaxf(pmax, s_red[w]);
+    }
+
+    // ---- 3. walk the skin lists: count, mark the exact union, store the hits' U_s positions (rewritten in step 5)
+    const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
+                zr = (float)foldPbc(zi - oz, a.box, 2);
+    const uint32_t  WS = nlocWords(a.ngmaxS);
+    const uint32_t* sl = a.sloc + (size_t)gw * WS * kWave + lane;
+    uint32_t*       ll = a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane;
+    const unsigned  ngmin     = a.ng0 / 4;
+    int             iteration = 0;
+    bool            active    = valid;
+    unsigned        count     = 0, stored = 0;
+    //! one pass over this lane's skin list in blocks of kWalkPF words (16 entries): begin(b) starts block b,
+    //! test(p, e) decides entry e of the block (U_s position p), onHit(p, e) takes the accepted ones in list order,
+    //! end(b) closes the block.  List words are loaded a block ahead, every load unconditional (clamped to the lane's
+    //! last word, word 0 for an empty list): a load under a condition is waited for at the branch merge
+    auto walk = [&](auto&& begin, auto&& test, auto&& onHit, auto&& end) {
+        if (!valid) return;
+        const uint32_t nw   = (scount + 1) >> 1;
+        const uint32_t last = nw ? nw - 1 : 0u;
+        constexpr int  PF   = kWalkPF;
+        uint32_t       nx[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u)
+            nx[u] = sl[(size_t)min((uint32_t)u, last) * kWave];
+        for (uint32_t w0 = 0, b = 0; w0 < nw; w0 += PF, ++b)
+        {
+            uint32_t cw[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u)
+            {
+                cw[u] = nx[u];
+                nx[u] = sl[(size_t)min(w0 + PF + u, last) * kWave];
+            }
+            begin(b);
+#pragma unroll
+            for (int u = 0; u < PF; ++u)
+            {
+                const uint32_t w = w0 + u;
+                if (w < nw)
+                {
+                    const uint32_t p0 = cw[u] & 0xffffu;
+                    if (test(p0, 2 * u)) onHit(p0, 2 * u);
+                    if (2 * w + 1 < scount)
+                    {
+                        const uint32_t p1 = cw[u] >> 16;
+                        if (test(p1, 2 * u + 1)) onHit(p1, 2 * u + 1);
+                    }
+                }
+            }
+            end(b);
+        }
+    };
+    float          cr = 0, tol = 0;
+    double         radSq = 0;
+    bool           safe = true, usePbc = false;
+    //! the float test (sx_neighbors.hip's form) with the reference's double criterion where |t| may be rounding
+    auto test = [&](uint32_t p, int) -> bool {
+        const float4 q = s_rec[p];
+        float        t = q.w + cr;
+        t              = fmaf(-2.0f * xr, q.x, t);
+        t              = fmaf(-2.0f * yr, q.y, t);
+        t              = fmaf(-2.0f * zr, q.z, t);
+        bool hit       = t < 0.0f;
+        if (!safe || fabsf(t) <= tol)
+        {
+            const uint32_t j  = un[p];
+            double         dx = a.x[j] - xi, dy = a.y[j] - yi, dz = a.z[j] - zi;
+            if (usePbc)
+            {
+                dx = foldPbc(dx, a.box, 0);
+                dy = foldPbc(dy, a.box, 1);
+                dz = foldPbc(dz, a.box, 2);
+            }
+            hit = dx * dx + dy * dy + dz * dz < radSq;
+        }
+        return hit; // j != i: the build's skin list never holds the target itself
+    };
+    while (true)
+    {
+        for (uint32_t u = threadIdx.x; u < U; u += kB)
+            s_hit[u] = 0;
+        __syncthreads();
+        const float  r2f = 4.0f * hi * hi;
+        radSq            = (double)r2f;
+        const double tw  = 2.0 * (double)hi;
+        const bool inside = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) && (zi - tw >= a.box.lim[4]) &&
+                            (xi + tw <= a.box.lim[1]) && (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
+        usePbc = a.box.anyPbc && !inside;
+        // the float test is exact only where the minimum image relative to the cluster origin is the pair's minimum
+        // image (|r| + 2h < L/2 on periodic axes); other lanes test every entry in double
+        safe = true;
+        for (int d = 0; d < 3; ++d)
+        {
+            const float rd = d == 0 ? xr : (d == 1 ? yr : zr);
+            if (a.box.pbc[d] && (fabsf(rd) + 2.05f * hi) >= 0.49f * (float)a.box.l[d]) safe = false;
+        }
+        cr = fmaf(xr, xr, fmaf(yr, yr, fmaf(zr, zr, -r2f)));
+        // |t| below tol may be rounding: those entries take the double criterion (sx_neighbors.hip's bound, with
+        // E >= |p| + |r| over the staged entries)
+        const float E = pmax + fabsf(xr) + fabsf(yr) + fabsf(zr);
+        tol           = 0x1p-19f * fmaf(E, E, r2f);
+        // every valid lane walks (a converged lane marks the same union entries again); no global store in the walk:
+        // vmcnt counts stores too, in order, so a store between the prefetch and its use would be waited for as well
+        unsigned cnt = 0, st = 0;
+        uint32_t bits = 0;
+        walk([&](uint32_t) { bits = 0; }, test,
+             [&](uint32_t p, int e) {
+                 if (cnt < a.ngmax)
+                 {
+                     s_hit[p] = 1;
+                     bits |= 1u << e;
+                     ++st;
+                 }
+                 ++cnt;
+             },
+             [&](uint32_t b) { s_bm[b][threadIdx.x] = (uint16_t)bits; });
+        count  = cnt;
+        stored = st;
+        // ---- 4. h-nc iteration (sph/find_neighbors.hpp:28-33); a grown h must stay within the skin
+        bool again = false, outgrown = false;
+        if (a.iterateH && active)
+        {
+            const unsigned ncSph = count + 1;
+            if (ngmin > ncSph || (ncSph - 1) > a.ngmax)
+            {
+                if (iteration < 10)
+                {
+                    iteration++;
+                    hi       = updateH(a.ng0, ncSph, hi, a.powTab);
+                    again    = true;
+                    outgrown = !withinSkin(hi);
+                }
+                else iteration = 11;
+            }
+        }
+        active = again;
+        if (blockAny(outgrown))
+        {
+            if (threadIdx.x == 0) a.stale[1 + atomicAdd(&a.stale[0], 1u)] = c;
+            return; // h, nc untouched; lists and union are rewritten by the rebuild
+        }
+        if (!blockAny(again)) break;
+    }
+
+    // ---- 5. exact union: ranks of the hit U_s entries (U_s order), the union at the slot's start, lists rewritten
+    uint32_t ue = 0;
+    {
+        // every thread a run of consecutive entries
+        const uint32_t B  = (U + kB - 1) / kB;
+        const uint32_t b0 = min(U, threadIdx.x * B), b1 = min(U, b0 + B);
+        uint32_t       sum = 0;
+        for (uint32_t u = b0; u < b1; ++u)
+            sum += s_hit[u];
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1)
+        {
+            const uint32_t t = __shfl_up(incl, o, kWave);
+            if (lane >= o) incl += t;
+        }
+        if (lane == kWave - 1) s_wsum[wave] = incl;
+        __syncthreads();
+        uint32_t run = incl - sum;
+        for (int w = 0; w < wave; ++w)
+            run += s_wsum[w];
+        for (int w = 0; w < kClusterWaves; ++w)
+            ue += s_wsum[w];
+        uint32_t* ux = a.uni + (size_t)c * a.ucap;
+        for (uint32_t u0 = b0; u0 < b1; u0 += 8)
+        {
+            uint32_t jj[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                jj[q] = un[min(u0 + q, U - 1u)];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (u0 + q < b1)
+                {
+                    s_rank[u0 + q] = (uint16_t)run;
+                    if (s_hit[u0 + q]) ux[run++] = jj[q];
+                }
+        }
+        __syncthreads();
+    }
+    // pass B: the same walk, the first ngmax hits written as exact-union ranks (two per word)
+    {
+        unsigned st = 0;
+        uint32_t pend = 0, bits = 0;
+        walk([&](uint32_t b) { bits = s_bm[b][threadIdx.x]; }, [&](uint32_t, int e) { return ((bits >> e) & 1u) != 0; },
+             [&](uint32_t p, int) {
+                 const uint32_t r = s_rank[p];
+                 if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend | (r << 16);
+                 else pend = r;
+                 ++st;
+             },
+             [](uint32_t) {});
+        if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend;
+    }
+
+    // ---- 6. outputs
+    if (valid)
+    {
+        a.nc[i] = count + 1;
+        if (a.iterateH) a.h[i] = hi;
+        if (a.rxOut) a.rxOut[i] = RecX{xi, yi, zi, hi, a.m[i]};
+        if (a.fresh)
+        {
+            a.hb[i] = h0;
+            a.ob[i] = odoi;
+        }
+    }
+    if (threadIdx.x == 0)
+    {
+        a.acc[c]    = a.fresh ? 0.0f : A;
+        a.ucount[c] = ue;
+    }
+    const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
+    const unsigned           nfail  = waveSum(failed);
+    const unsigned           maxCnt = waveMax(valid ? count : 0u);
+    const unsigned long long nst    = waveSum((unsigned long long)(valid ? stored : 0u));
+    const unsigned long long walked = waveSum((unsigned long long)scount);
+    if (lane == 0)
+    {
+        if (nfail) atomicAdd(&a.stats[1], nfail);
+        s_cst[wave] = make_uint4(maxCnt, (uint32_t)nst, (uint32_t)walked, 0u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint4 t = s_cst[0];
+        for (int w = 1; w < kClusterWaves; ++w)
+            t.x = max(t.x, s_cst[w].x), t.y += s_cst[w].y, t.z += s_cst[w].z;
+        t.w          = ue;
+        a.clStats[c] = t;
+    }
+}
+
+inline unsigned grid1(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+} // namespace
+
+hipError_t skinFilter(const SkinArgs& a, uint32_t numClusters, hipStream_t s)
+{
+    if (numClusters) skinFilterKernel<<<numClusters, kB, 0, s>>>(a, numClusters);
+    return hipGetLastError();
+}
+
+hipError_t skinRefreshBoxes(const DevTree& t, const double* x, const double* y, const double* z, const DevBox& box,
+                            double* centers, double* sizes, hipStream_t s)
+{
+    if (t.numNodes <= 0) return hipSuccess;
+    // leaves first (any level), then the inner nodes level by level from the deepest
+    leafBoxKernel<<<grid1(t.numNodes, 4), 256, 0, s>>>(t.childOffsets, t.internalToLeaf, t.layout, t.numNodes,
+                                                         t.centers, t.sizes, x, y, z, box, centers, sizes);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = t.levelRangeHost[level], e = t.levelRangeHost[level + 1];
+        if (e > b) innerBoxKernel<<<grid1(e - b), 256, 0, s>>>(t.childOffsets, b, e, t.centers, box, centers, sizes);
+    }
+    return hipGetLastError();
+}
+
+hipError_t skinMarkStale(const uint32_t* list, uint32_t numClusters, float* acc, hipStream_t s)
+{
+    if (numClusters) markStaleKernel<<<grid1(numClusters), 256, 0, s>>>(list, numClusters, acc);
+    return hipGetLastError();
+}
+
+hipError_t reduceClusterStats(const uint4* clStats, uint32_t numClusters, uint32_t* stats, hipStream_t s)
+{
+    reduceClusterStatsKernel<<<1, 1024, 0, s>>>(clStats, numClusters, stats);
+    return hipGetLastError();
+}
+
+} // namespace sx

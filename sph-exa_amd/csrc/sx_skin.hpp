@@ -1,0 +1,87 @@
+/*! @file sx_skin.hpp
+ * @brief Neighbor lists kept behind a skin across steps (sx_skin.hip): the search of a step becomes a filter of the
+ *        last build's inflated lists whenever no particle can have entered a target's 2h sphere since that build.
+ *
+ * A BUILD (the search of sx_neighbors.hip with every radius scaled by skin1 = 1 + s, no h iteration) leaves, per
+ * 256-particle cluster, the union U_s of its targets' neighbors within R_i = 2 h_i (1 + s) and per target its SKIN
+ * LIST: u16 positions into U_s, ascending (U_s in the upper part of the cluster's union slot, uni[c*ucap + uoff]).
+ * The FILTER (skinFilterKernel) then produces the step's exact lists -- the reference criterion d2 < (double)(4 h^2),
+ * j != i (cstone/findneighbors.hpp:133-158), h-nc iteration (sph/find_neighbors.hpp:28-33) included -- and the exact
+ * union (the U_s entries some target hit, in U_s order) at the slot's start, exactly what the search leaves for the
+ * pair kernels.
+ *
+ * Validity (checked by the filter for every target, every step): a particle j outside i's skin list at the build
+ * (|x_i^b - x_j^b| >= R_i) can now be closer than 2 h_i only if the two moved towards each other by R_i - 2 h_i.
+ * Before it entered the ball of radius R_i around i it was outside it; from then on it sits, at the end of every step,
+ * inside the cluster's region (the targets' box grown by max R), so each of its steps is bounded by that step's
+ * largest displacement in the region (the displacement grid, a max over cells of the end-of-step positions), and the
+ * running sum of those maxima since the build, A_C, bounds its approach; i's own approach is its path length d_i.
+ * So   2 h_i + d_i + A_C <= R_i (1 - eps)   guarantees the skin list holds every current neighbor of i.  A cluster
+ * failing it for some target (or whose build overflowed a capacity) is STALE: it is rebuilt on the spot (a build over
+ * the stale clusters only, on node boxes refreshed from the current positions, then the filter); a cluster stale
+ * again (its h iteration outgrew the fresh skin) takes the exact search, which writes its lists directly.
+ *
+ * Between builds the particle order and the tree are kept (no SFC re-sort: that would renumber the union entries);
+ * sx_sim does a full sync + build of every cluster when the stale share or the steps since the last full build pass
+ * their limits (SkinState).
+ */
+#pragma once
+
+#include "sx_tree.hpp"
+
+namespace sx
+{
+
+using SkinGrid = DispGrid; //!< per-step displacement maxima by cell (sx_device.hpp)
+
+constexpr int kSkinGridN = 64;
+
+//! filter arguments (one 256-thread workgroup per cluster)
+struct SkinArgs
+{
+    uint32_t first, last, numGroups, ngmax, ng0;
+    uint32_t ngmaxS; // skin-list capacity per target
+    int      iterateH;
+    int      fresh; // 1: the listed clusters were just built: record hb, ob, acc = 0 instead of checking the drift
+    float    skin1; // 1 + s
+    const double *x, *y, *z;
+    float*       h;
+    const float* m;
+    uint32_t*    nc;
+    RecX*        rxOut; // nullable
+    // exact lists and unions (output, the pair kernels' nloc / uni[c*ucap ...] / ucount) and the skin unions (input,
+    // uni[c*ucap + uoff ...], ucountS[c] entries)
+    uint32_t*       nloc;
+    uint32_t*       uni;
+    uint32_t*       ucount;
+    uint32_t        ucap;
+    uint32_t        uoff;
+    const uint32_t* ucountS;
+    // skin state
+    const uint32_t* sloc; // skin lists (nlocWords(ngmaxS) words per target, lane-interleaved like nloc)
+    const uint32_t* scnt; // skin count + 1 per target (the build's nc)
+    float*          hb;   // h at the build
+    float*          ob;   // path length at the build
+    const float*    odo;  // path length since the last full build
+    float*          acc;  // per cluster: sum of the per-step displacement maxima of its region since its build
+    const uint32_t* cells; // displacement grid (float bits, per-step maxima)
+    SkinGrid        grid;
+    const uint32_t* list;  // nullable: the clusters list[1 .. list[0]], else all
+    uint32_t*       stale; // [0] count, [1..] stale clusters (output)
+    DevBox          box;
+    const float*    powTab;
+    uint32_t*       stats;   // kStatsWords (failures)
+    uint4*          clStats; // per cluster {max count, stored, skin entries walked, union}
+};
+
+hipError_t skinFilter(const SkinArgs& a, uint32_t numClusters, hipStream_t s);
+//! node boxes (center, half size) of the tree refreshed from the current positions: leaf boxes bound their particles,
+//! inner boxes their children (for a build between full syncs, when particles have left their cells)
+hipError_t skinRefreshBoxes(const DevTree& t, const double* x, const double* y, const double* z, const DevBox& box,
+                            double* centers, double* sizes, hipStream_t s);
+//! acc[c] = +inf for the listed clusters (their lists came from the exact search: the next step rebuilds their skin)
+hipError_t skinMarkStale(const uint32_t* list, uint32_t numClusters, float* acc, hipStream_t s);
+//! per-cluster statistics -> stats (the search's reduction)
+hipError_t reduceClusterStats(const uint4* clStats, uint32_t numClusters, uint32_t* stats, hipStream_t s);
+
+} // namespace sx

@@ -238,6 +238,13 @@ struct NsArgs
     // for every target it completes, so no separate packing pass is needed for [first, last)
     RecX*           rxOut;
     const float*    m;
+    // skin build (sx_skin.hpp): > 0 scales every search radius by skin1 = 1 + s (the caller passes iterateH = 0, the
+    // skin lists as nloc with their capacity as ngmax, the skin counts as nc, no rxOut); a union beyond ucap is then
+    // recorded in ucount instead of failing the search
+    float           skin1;
+    uint32_t        uoff; // the union is written at uni[c*ucap + uoff ...] (capacity ucap - uoff); 0 but for skin builds
+    // nullable: search only the clusters subset[1 .. subset[0]] (findNeighbors; device-resident list)
+    const uint32_t* subset;
 
     void setLists(const NbLists& L)
     {

@@ -201,6 +201,10 @@ def lib():
         "sx_sim_timestep": (C.c_int, [vp, C.POINTER(SxTimestep)]),
         "sx_sim_set_timestep": (C.c_int, [vp, C.POINTER(SxTimestep), vp]),
         "sx_sim_set_time": (C.c_int, [vp, C.c_double]),
+        "sx_sim_set_skin": (C.c_int, [vp, C.c_float, C.c_int]),
+        "sx_sim_rebuild_lists": (C.c_int, [vp]),
+        "sx_sim_skin_stats": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "sx_sim_export_neighbors": (C.c_int, [vp, vp]),
         "sx_comm_unique_id": (C.c_int, [vp]),
         "sx_comm_create_rccl": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, vp]),
         "sx_comm_create_host": (C.c_int, [C.POINTER(vp), C.c_int, C.c_int, ALLTOALLV_CB, ALLREDUCE_CB, vp]),
@@ -328,6 +332,12 @@ class Context:
         d = self.alloc(arr.size, arr.dtype)
         self.check(self.L.sx_memcpy(self.h, d.ptr, arr.ctypes.data, arr.nbytes, 1), "upload")
         return d
+
+    def free(self, arr):
+        """release one DeviceArray of alloc/upload"""
+        if arr.ptr in self.allocs:
+            self.allocs.remove(arr.ptr)
+            self.L.sx_device_free(self.h, arr.ptr)
 
     def free_all(self):
         for p in self.allocs:
@@ -538,6 +548,9 @@ class Sim:
                 raise ValueError(f"ve-bdt checkpoint inside a time-step hierarchy (substep {ts['substep']} of "
                                  f"{1 << (ts['numRungs'] - 1)}): save after the hierarchy's last substep")
         st = self.get(self.CONSERVED + (["rung"] if bdt else []))
+        # a run restarted from this file begins with a full sync + neighbor build; so does this one's next step, so
+        # the two take identical steps (skin lists, sx_sim_rebuild_lists)
+        self.rebuild_lists()
         if num_particles_global is None:
             num_particles_global = self.size()
             comm = getattr(self, "comm", None)
@@ -618,6 +631,34 @@ class Sim:
         t = float(d["time"] if "time" in d else d["ttot"])
         self.ctx.check(self.L.sx_sim_set_time(self.h, t), "set_time")
         return t
+
+    def set_skin(self, factor=0.08, max_reuse=24):
+        """neighbor lists behind a skin of relative width `factor` (sx_sim_set_skin; 0: sync + search every step)"""
+        self.ctx.check(self.L.sx_sim_set_skin(self.h, float(factor), int(max_reuse)), "set_skin")
+
+    def rebuild_lists(self):
+        """the next step does a full sync + build of every skin (sx_sim_rebuild_lists)"""
+        self.ctx.check(self.L.sx_sim_rebuild_lists(self.h), "rebuild_lists")
+
+    def skin_stats(self):
+        out = (C.c_uint64 * 8)()
+        self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
+        return dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
+                         "capacity", "since_build"], list(out)))
+
+    def neighbor_sets(self):
+        """the last step's neighbor lists as {particle id: sorted array of neighbor ids} (sx_sim_export_neighbors)"""
+        n = self.size()
+        ngmax = int(self.params.ngmax)
+        buf = self.ctx.alloc(max(1, n * ngmax), np.uint32)
+        try:
+            self.ctx.check(self.L.sx_sim_export_neighbors(self.h, buf.ptr), "export_neighbors")
+            rows = buf.get()[: n * ngmax].reshape(n, ngmax)
+        finally:
+            self.ctx.free(buf)
+        g = self.get(["id", "nc"])
+        ids, nc = g["id"], g["nc"].astype(np.int64)
+        return {int(ids[i]): np.sort(ids[rows[i, : min(nc[i] - 1, ngmax)]]) for i in range(n)}
 
     def step(self):
         rc = self.L.sx_sim_step(self.h)

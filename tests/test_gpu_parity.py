@@ -316,6 +316,7 @@ def test_local_sort_order(ctx, ora, pairs):
             for c, off in zip(("x", "y", "z"), (1.5e-4, 2.5e-4, 3.5e-4)):
                 st.arrays[c][d] = st.arrays[c][s] + off
     sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_skin(0.0, 1)  # every step syncs (skin lists keep the order between their builds)
     sim.set_state(st.arrays, st.minDt, st.minDt_m1)
     conserved = list(gutil.StepChecker.CONSERVED)
     cur = {k: st.arrays[k].copy() for k in conserved}

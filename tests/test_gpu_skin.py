@@ -1,0 +1,104 @@
+"""Skin-list reuse of the neighbor search (sph-exa_amd/csrc/sx_skin.hpp) against a fresh search and the oracle.
+
+Between full builds a one-rank step filters the last build's lists within 2h(1 + s) instead of syncing and
+searching.  What must not change is the step's neighbor search result (cstone::findNeighbors + findNeighborsSph,
+findneighbors.hpp:95-188, find_neighbors.hpp:10-44):
+  * the neighbor SETS, nc and h of a filtered step equal those of a fresh sync + search of the same state (a second
+    Sim with the skin off, handed the state before every step), particle by particle by id, over runs that rebuild
+    stale clusters (Sedov's blast, Noh's infall, an Evrard-like collapse IC) and run the exact-search fallback;
+  * every filtered step checked per particle against the CPU oracle (gpu_util.shadow_steps: nc and h exact, rates
+    within the fast-variant tolerance);
+  * the skin does its job: most steps are served by the filter on a quiescent state.
+"""
+import numpy as np
+import pytest
+
+import gpu_util as gutil
+import pyoracle as po
+import sphexa_amd as sx
+
+pytestmark = pytest.mark.gpu
+
+STATE = ["x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "id"]
+
+
+def _ic(kind, side):
+    if kind == "sedov":
+        return po.sedov_state(side)
+    if kind == "noh":
+        return po.noh_state(side)
+    return po.evrard_state(side)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sx.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("kind,side,steps,factor", [("sedov", 24, 14, 0.08), ("noh", 24, 12, 0.08),
+                                                    ("evrard", 22, 10, 0.08), ("sedov", 20, 10, 0.02)])
+def test_skin_sets_equal_fresh_search(ctx, kind, side, steps, factor):
+    """each filtered step's neighbor sets, nc and h equal a fresh search's from the same state"""
+    st, obox = _ic(kind, side)
+    box = gutil.box_to_sx(obox)
+    a = sx.Sim(ctx, st.n, box)
+    a.set_skin(factor, 24)
+    b = sx.Sim(ctx, st.n, box)
+    b.set_skin(0.0, 1)
+    a.set_state(st.arrays, st.minDt, st.minDt_m1)
+    try:
+        for s in range(steps):
+            g = a.get(STATE)
+            sc = a.scalars()
+            b.set_state(g, sc["minDt"], sc["minDt_m1"])
+            a.step()
+            b.step()
+            ga, gb = a.get(["id", "nc", "h"]), b.get(["id", "nc", "h"])
+            oa, ob = np.argsort(ga["id"]), np.argsort(gb["id"])
+            assert np.array_equal(ga["nc"][oa], gb["nc"][ob]), (kind, s)
+            assert np.array_equal(ga["h"][oa], gb["h"][ob]), (kind, s)
+            na, nb = a.neighbor_sets(), b.neighbor_sets()
+            bad = [k for k in na if not np.array_equal(na[k], nb[k])]
+            assert not bad, (kind, s, len(bad), bad[:3])
+        ks = a.skin_stats()
+        print(kind, side, factor, ks)
+        assert ks["reuse_steps"] > 0, ks
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("kind,side,steps", [("sedov", 16, 6), ("noh", 24, 6)])
+def test_skin_steps_vs_oracle(ctx, kind, side, steps):
+    """filtered steps, each checked per particle against an oracle step from the same state"""
+    ora = po.load_oracle()
+    st, obox = _ic(kind, side)
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    try:
+        gutil.shadow_steps(ctx, ora, sim, obox, steps, ora.params(), ["x", "y", "z", "vx", "vy", "vz", "temp", "du",
+                                                                     "ax", "ay", "az", "alpha", "xm", "kx"])
+        ks = sim.skin_stats()
+        assert ks["reuse_steps"] >= steps - 2, ks
+    finally:
+        sim.close()
+
+
+def test_skin_quiescent_lattice_reuses(ctx):
+    """a lattice at rest (Sedov outside the blast): after the first full build every step is served by the filter,
+    without stale clusters, until maxReuse forces the next full build"""
+    st, obox = po.sedov_state(20)
+    st.temp[:] = st.temp.min()  # no blast: nothing moves
+    sim = sx.Sim(ctx, st.n, gutil.box_to_sx(obox))
+    sim.set_skin(0.08, 5)
+    sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+    try:
+        for _ in range(11):
+            sim.step()
+            assert sim.stats()["numFailed"] == 0
+        ks = sim.skin_stats()
+        assert ks["builds"] == 2 and ks["reuse_steps"] == 9 and ks["stale_clusters"] == 0, ks
+    finally:
+        sim.close()
