@@ -1570,7 +1570,17 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
         K.sinceBuild = 0;
     }
     // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once
-    if ((double)n1 > K.staleLimit * ncl) K.forceBuild = true;
+    if ((double)n1 > K.staleLimit * ncl)
+    {
+        K.forceBuild = true;
+        if (reuse && K.sinceBuild < 2)
+        {
+            // the skin did not outlast its build: search without it for a while
+            K.backoff    = K.backoffLen;
+            K.backoffLen = std::min(2 * K.backoffLen, 32);
+        }
+    }
+    else if (reuse && K.sinceBuild >= 2) K.backoffLen = 1;
     return SX_OK;
 }
 
@@ -1692,7 +1702,7 @@ extern "C"
         if (!s) return SX_ERR_ARG;
         const auto& K = s->skin;
         out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
-        out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = (uint64_t)K.sinceBuild;
+        out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = K.plainSteps;
         return SX_OK;
     }
 
@@ -1913,7 +1923,13 @@ extern "C"
 
         // skin lists (sx_skin.hpp): a reuse step keeps the order and tree of the last full build and filters the
         // skin lists instead of syncing and searching
-        const bool skinOn = !dist && skinUsable(s);
+        bool skinOn = !dist && skinUsable(s);
+        if (skinOn && s->skin.backoff > 0)
+        {
+            s->skin.backoff--;
+            s->skin.plainSteps++;
+            skinOn = false;
+        }
         const bool reuse  = skinOn && s->skin.valid && !s->skin.forceBuild && s->skin.sinceBuild < s->skin.maxReuse;
         if (!skinOn) s->skin.valid = false;
         // h before the h iteration, to redo the search if the halo margin proves too small

@@ -73,6 +73,10 @@ struct SkinState
     bool     forceBuild{false};
     int      sinceBuild{0};
     uint32_t ngmaxS{0};         // skin-list capacity per target
+    // a skin that does not outlast its build by two steps (fast flows: every cluster stale at once) costs more than it
+    // saves: the next backoff steps search without it, backoffLen doubling with every such failure (up to 32)
+    int      backoff{0}, backoffLen{1};
+    uint64_t plainSteps{0};     // steps searched without the skin while backing off
     // statistics: full builds, steps served by the filter, clusters rebuilt (stale), clusters sent to the exact search
     uint64_t builds{0}, reuseSteps{0}, staleClusters{0}, exactClusters{0};
     uint32_t lastStale{0}, lastExact{0};

@@ -644,7 +644,7 @@ class Sim:
         out = (C.c_uint64 * 8)()
         self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
         return dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
-                         "capacity", "since_build"], list(out)))
+                         "capacity", "plain_steps"], list(out)))
 
     def neighbor_sets(self):
         """the last step's neighbor lists as {particle id: sorted array of neighbor ids} (sx_sim_export_neighbors)"""
