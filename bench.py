@@ -447,7 +447,7 @@ def main():
                        "gravity_far_cells": sim.gravity_stats()["far_cells"]} if world > 1 and args.init == "evrard"
                       else {}),
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)",
-                   "neighbor_skin": {"factor": args.skin, "max_reuse": args.skin_reuse,
+                   "neighbor_skin": {"initial_factor": args.skin, "max_reuse": args.skin_reuse,
                                      "note": "one rank without gravity: steps between full builds filter the last "
                                              "build's lists within 2h(1+s) (sx_skin.hpp); same neighbor sets, nc, h",
                                      **skin}},

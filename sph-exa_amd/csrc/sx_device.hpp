@@ -230,13 +230,28 @@ __host__ __device__ inline int wrapCell(int k, int n)
     return k < 0 ? k + n : k;
 }
 
-/*! cells[cell of (x, y, z)] = max(., d) for every lane with d > 0, called by every lane of the wave.  SFC-ordered
- *  particles: a wave's moving particles share one or two cells, so the first moving lane's cell takes one atomic with
- *  the wave's maximum over it and lanes in other cells add their own */
-__device__ inline void gridMaxAtomic(uint32_t* cells, const DispGrid& g, double x, double y, double z, float d)
+//! order-preserving image of a float as an unsigned integer (atomic min / max of signed floats)
+__host__ __device__ inline uint32_t orderedBits(float f)
+{
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float orderedFloat(uint32_t o)
+{
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+//! per cell the ranges of the three displacement components as ordered bits, six planes of n^3 words: min x, min y,
+//! min z (initialised to 0xffffffff), max x, max y, max z (initialised to 0); an empty cell keeps min > max
+constexpr int kGridWords = 6;
+
+/*! the cell of (x, y, z) takes the displacement (dx, dy, dz) into its component ranges, for every lane with `on`;
+ *  called by every lane of the wave.  SFC-ordered particles: a wave's particles share one or a few cells, so the wave
+ *  takes its cells one at a time -- the ranges of the cell's lanes reduced across the wave, six atomics by one lane */
+__device__ inline void gridRangeAtomic(uint32_t* cells, const DispGrid& g, double x, double y, double z, float dx,
+                                       float dy, float dz, bool on)
 {
     uint32_t cell = 0;
-    if (d > 0.0f)
+    if (on)
     {
         const double p[3] = {x, y, z};
         int          k[3];
@@ -244,17 +259,33 @@ __device__ inline void gridMaxAtomic(uint32_t* cells, const DispGrid& g, double 
             k[e] = g.pbc[e] ? wrapCell(gridCell(p[e], g, e), g.n) : gridCell(p[e], g, e);
         cell = ((uint32_t)k[2] * g.n + (uint32_t)k[1]) * g.n + (uint32_t)k[0];
     }
-    const uint64_t mv = __ballot(d > 0.0f);
-    if (!mv) return;
-    const int      l0   = __builtin_ctzll(mv);
-    const uint32_t c0   = __builtin_amdgcn_readlane(cell, l0);
-    const bool     same = d > 0.0f && cell == c0;
-    float          m    = same ? d : 0.0f;
+    const float  d[3] = {dx, dy, dz};
+    const size_t nc   = (size_t)g.n * g.n * g.n;
+    const int    lane = (int)(threadIdx.x & 63);
+    uint64_t     left = __ballot(on);
+    while (left)
+    {
+        const int      l0   = __builtin_ctzll(left);
+        const uint32_t c0   = __builtin_amdgcn_readlane(cell, l0);
+        const bool     same = on && cell == c0;
+        left &= ~__ballot(same);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        m = fmaxf(m, __shfl_xor(m, o, kWave));
-    if ((int)(threadIdx.x & 63) == l0) atomicMax(&cells[c0], __float_as_uint(m));
-    if (d > 0.0f && !same) atomicMax(&cells[cell], __float_as_uint(d));
+        for (int e = 0; e < 3; ++e)
+        {
+            float lo = same ? d[e] : INFINITY, hi = same ? d[e] : -INFINITY;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+            {
+                lo = fminf(lo, __shfl_xor(lo, o, kWave));
+                hi = fmaxf(hi, __shfl_xor(hi, o, kWave));
+            }
+            if (lane == l0)
+            {
+                atomicMin(&cells[e * nc + c0], orderedBits(lo));
+                atomicMax(&cells[(3 + e) * nc + c0], orderedBits(hi));
+            }
+        }
+    }
 }
 
 //! float atomic min for non-negative values via the ordered int representation

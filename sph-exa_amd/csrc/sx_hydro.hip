@@ -599,8 +599,9 @@ __global__ __launch_bounds__(kBlock) void momentumStdKernel(PairArgs a)
 __global__ void positionsKernel(PosArgs a)
 {
     uint32_t i = a.first + blockIdx.x * blockDim.x + threadIdx.x;
-    float    dcell = 0.0f; // this step's displacement for the grid (every lane reaches the grid update below)
+    float    dv[3] = {0.0f, 0.0f, 0.0f}; // this step's displacement for the grid (every lane reaches it below)
     double   pc[3] = {0.0, 0.0, 0.0};
+    bool     moved = false;
     if (i < a.last)
     {
         const DevBox& b    = a.box;
@@ -647,19 +648,20 @@ __global__ void positionsKernel(PosArgs a)
             a.vy[i]   = (float)Vn1[1];
             a.vz[i]   = (float)Vn1[2];
             if (a.keys) a.keys[i] = sfcKey(Xn[0], Xn[1], Xn[2], b);
-            if (a.disp)
+            if (a.dispX)
             {
-                // an upper bound of the move (the periodic wrap above does not count): float rounding pushed upwards
-                const float d = (float)(sqrt(dXn1[0] * dXn1[0] + dXn1[1] * dXn1[1] + dXn1[2] * dXn1[2]) * (1.0 + 0x1p-20));
-                a.disp[i]     = d;
-                a.odo[i] += d;
-                dcell = d, pc[0] = Xn[0], pc[1] = Xn[1], pc[2] = Xn[2];
+                // the move without the periodic wrap above (float; the filter's bounds allow for its rounding)
+                dv[0] = (float)dXn1[0], dv[1] = (float)dXn1[1], dv[2] = (float)dXn1[2];
+                a.dispX[i] = dv[0], a.dispY[i] = dv[1], a.dispZ[i] = dv[2];
+                pc[0] = Xn[0], pc[1] = Xn[1], pc[2] = Xn[2];
+                moved = true;
             }
         }
         else
         {
             if (a.keys) a.keys[i] = sfcKey(a.x[i], a.y[i], a.z[i], b);
-            if (a.disp) a.disp[i] = 0.0f;
+            if (a.dispX) a.dispX[i] = 0.0f, a.dispY[i] = 0.0f, a.dispZ[i] = 0.0f;
+            if (a.dispX) pc[0] = a.x[i], pc[1] = a.y[i], pc[2] = a.z[i], moved = true;
         }
         double u_old = (double)a.constCv * a.temp[i];
         double du = a.du[i], du_m1 = (double)a.du_m1[i];
@@ -668,7 +670,7 @@ __global__ void positionsKernel(PosArgs a)
         a.temp[i]  = u_new / (double)a.constCv;
         a.du_m1[i] = (float)du;
     }
-    if (a.cells) gridMaxAtomic(a.cells, a.grid, pc[0], pc[1], pc[2], dcell);
+    if (a.cells) gridRangeAtomic(a.cells, a.grid, pc[0], pc[1], pc[2], dv[0], dv[1], dv[2], moved);
 }
 
 //! updateSmoothingLengthGpuKernel (update_h_gpu.cu:39-46)

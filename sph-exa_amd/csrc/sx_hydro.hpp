@@ -155,12 +155,10 @@ struct PosArgs
     float         constCv;
     // nullable: the next sync's SFC keys of the updated coordinates (sfcKey, box `box`), written in the same pass
     uint64_t*     keys;
-    // nullable (skin lists, sx_skin.hpp): this step's displacement |dX| (rounded up) and the path length since the
-    // last full build (odo += disp)
-    float*        disp;
-    float*        odo;
-    // nullable (skin lists): the per-step displacement maxima by cell of the updated position (gridMaxAtomic; zeroed
-    // by the caller), so the next step's filter needs no pass over the particles
+    // nullable (skin lists, sx_skin.hpp): this step's displacement vector (unwrapped), per particle, and its
+    // component ranges by cell of the updated position (gridRangeAtomic; initialised by the caller), so the next
+    // step's filter needs no pass over the particles
+    float *       dispX, *dispY, *dispZ;
     uint32_t*     cells;
     DispGrid      grid;
 };

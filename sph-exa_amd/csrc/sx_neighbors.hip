@@ -538,14 +538,17 @@ findNeighborsKernel(NsArgs a)
 #ifdef SX_NS_SMALL
                 if (a.forceOverflow) f |= 4u; // test hook (sx_set_search_mode 3): exercise the device-side fallback
 #endif
-                // with a redo list (compact build first) an over-capacity cluster is handed to the large build,
-                // otherwise it is an error of the search
-                s_abandon = f && a.redo ? 1 : 0;
+                // with a redo list (compact build first) an over-capacity cluster is handed to the large build; a
+                // skin build's cluster over the large build's capacities is left unbuilt with an over-capacity union
+                // count (the filter sends it to the exact search); otherwise it is an error of the search
+                const bool skinB = a.skin1 > 0.0f;
+                s_abandon        = f && (a.redo || skinB) ? 1 : 0;
                 if (f && a.redo)
                 {
                     a.redo[1 + atomicAdd(&a.redo[0], 1u)] = c;
                     atomicAdd(&a.stats[10], 1u);
                 }
+                else if (f && skinB) a.ucount[c] = 0xffffffffu;
                 else if (f) atomicOr(&a.stats[0], 1u | f);
                 s_numCand = f ? 0 : nCand;
             }

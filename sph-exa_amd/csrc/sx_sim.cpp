@@ -1428,6 +1428,23 @@ bool skinUsable(const sx_sim* s)
            NbLists::localPossible(s->p.ngmax);
 }
 
+//! widest skin the adaptation goes to: skin lists (1.16)^3 = 1.56x the neighbors; wider unions outgrow the filter's LDS
+//! staging (kSkinCap) in dense regions (Noh at s = 0.25: 37% of the clusters)
+constexpr float kMaxSkin = 0.16f;
+
+//! a skin that did not outlast two steps: the next build takes a twice wider one; at the widest, the next steps
+//! search without skin (backoff, doubling up to 32 steps)
+void skinTooThin(SkinState& K)
+{
+    K.forceBuild = true;
+    if (K.cur < kMaxSkin) K.cur = std::min(2.0f * K.cur, kMaxSkin);
+    else
+    {
+        K.backoff    = K.backoffLen;
+        K.backoffLen = std::min(2 * K.backoffLen, 32);
+    }
+}
+
 //! the displacement grid over the box: kSkinGridN cells per axis
 SkinGrid skinGrid(const DevBox& b)
 {
@@ -1450,57 +1467,71 @@ uint32_t skinCapacity(uint32_t ngmax, float factor)
     return std::min<uint32_t>(256u, (c + 1u) & ~1u);
 }
 
-//! the skin arrays the position update feeds: per particle the path length and this step's displacement, the grid
-//! of per-step displacement maxima by cell (zeroed here: the update scatters into it)
+//! the skin arrays the position update feeds: per particle this step's displacement vector, and per cell of the grid
+//! the component ranges (initialised here: the update scatters into them)
 bool skinParticleBuffers(sx_sim* s, PosArgs& q, hipStream_t st)
 {
-    q.disp  = s->mem.get<float>("skin.disp", s->cap);
-    q.odo   = s->mem.get<float>("skin.odo", s->cap);
-    q.cells = s->mem.get<uint32_t>("skin.cells", (size_t)kSkinGridN * kSkinGridN * kSkinGridN);
+    const size_t nc = (size_t)kSkinGridN * kSkinGridN * kSkinGridN;
+    q.dispX = s->mem.get<float>("skin.dx", s->cap);
+    q.dispY = s->mem.get<float>("skin.dy", s->cap);
+    q.dispZ = s->mem.get<float>("skin.dz", s->cap);
+    q.cells = s->mem.get<uint32_t>("skin.cells", kGridWords * nc);
     q.grid  = skinGrid(s->dbox);
-    if (!q.disp || !q.odo || !q.cells) return false;
-    return hipMemsetAsync(q.cells, 0, sizeof(uint32_t) * kSkinGridN * kSkinGridN * kSkinGridN, st) == hipSuccess;
+    if (!q.dispX || !q.dispY || !q.dispZ || !q.cells) return false;
+    return hipMemsetAsync(q.cells, 0xff, 3 * nc * sizeof(uint32_t), st) == hipSuccess &&
+           hipMemsetAsync(q.cells + 3 * nc, 0, 3 * nc * sizeof(uint32_t), st) == hipSuccess;
 }
+
+constexpr int kSkinResync = 1000; //!< skinSearch: redo this step's search from a full sync (not an error code)
 
 /*! The step's neighbor search through skin lists (sx_skin.hpp).  A full build (after a full sync) builds every
  *  cluster's skin and filters it; a reuse step only filters.  Stale clusters are rebuilt at once on node boxes refreshed
- *  from the current positions (reuse steps) and filtered; clusters stale again take the exact search.  na: the step's
- *  search arguments (exact lists, h, nc, tree).  One host read of the stale count, two when some cluster is stale. */
-int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
+ *  from the current positions (reuse steps) and filtered; clusters stale again take the exact search (on a reuse step
+ *  over the refreshed boxes: should it outgrow a capacity there, kSkinResync makes the caller restore h and redo the
+ *  step's search from a full sync).  na: the step's search arguments (exact lists, h, nc, tree).  One host read of the
+ *  stale count, two or three when some cluster is stale. */
+int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* xmOut, RecT* rtXm)
 {
     auto&          K   = s->skin;
     const uint32_t ncl = (na.numGroups + kClusterWaves - 1) / kClusterWaves;
     if (!ncl) return SX_OK;
-    K.ngmaxS      = skinCapacity(s->p.ngmax, K.factor);
+    if (!reuse) K.built = K.cur, K.ngmaxS = skinCapacity(s->p.ngmax, K.built);
     const size_t G    = kSkinGridN;
-    float*       odo  = s->mem.get<float>("skin.odo", s->cap);
+    float*       rel  = s->mem.get<float>("skin.rel", s->cap);
+    float*       dx   = s->mem.get<float>("skin.dx", s->cap);
+    float*       dy   = s->mem.get<float>("skin.dy", s->cap);
+    float*       dz   = s->mem.get<float>("skin.dz", s->cap);
     uint32_t*   sloc = s->mem.get<uint32_t>("skin.sloc", na.numGroups * (size_t)nlocWords(K.ngmaxS) * kWave);
     uint32_t*   scnt = s->mem.get<uint32_t>("skin.scnt", s->cap);
     float*      hb   = s->mem.get<float>("skin.hb", s->cap);
-    float*      ob   = s->mem.get<float>("skin.ob", s->cap);
     float*      acc  = s->mem.get<float>("skin.acc", ncl);
-    uint32_t*   cells = s->mem.get<uint32_t>("skin.cells", G * G * G);
+    uint32_t*   cells = s->mem.get<uint32_t>("skin.cells", kGridWords * G * G * G);
     uint32_t*   ucS   = s->mem.get<uint32_t>("skin.ucount", ncl);
     uint32_t*   l1    = s->mem.get<uint32_t>("skin.l1", ncl + 1);
     uint32_t*   l2    = s->mem.get<uint32_t>("skin.l2", ncl + 1);
     uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 2);
-    if (!odo || !sloc || !scnt || !hb || !ob || !acc || !cells || !ucS || !l1 || !l2 || !hl) return SX_ERR_NOMEM;
+    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl)
+        return SX_ERR_NOMEM;
 
     const SkinGrid g = skinGrid(s->dbox);
     SkinArgs fa{};
     fa.first = na.first, fa.last = na.last, fa.numGroups = na.numGroups, fa.ngmax = na.ngmax, fa.ng0 = na.ng0;
-    fa.ngmaxS = K.ngmaxS, fa.iterateH = na.iterateH, fa.skin1 = 1.0f + K.factor;
+    fa.ngmaxS = K.ngmaxS, fa.iterateH = na.iterateH, fa.skin1 = 1.0f + K.built;
     fa.x = na.x, fa.y = na.y, fa.z = na.z, fa.h = na.h, fa.m = na.m, fa.nc = na.nc, fa.rxOut = na.rxOut;
     // the skin union lives in the upper half of each cluster's union slot, the exact union (the pair kernels') at its
     // start
     const uint32_t uoff = na.ucap / 2;
     fa.nloc = na.nloc, fa.uni = na.uni, fa.ucount = na.ucount, fa.ucap = na.ucap, fa.uoff = uoff, fa.ucountS = ucS;
-    fa.sloc = sloc, fa.scnt = scnt, fa.hb = hb, fa.ob = ob, fa.odo = odo, fa.acc = acc, fa.cells = cells, fa.grid = g;
+    fa.sloc = sloc, fa.scnt = scnt, fa.hb = hb, fa.rel = rel, fa.acc = acc, fa.cells = cells, fa.grid = g;
+    fa.dispX = dx, fa.dispY = dy, fa.dispZ = dz;
+    fa.xmOut = xmOut, fa.rtXm = rtXm, fa.K = s->p.K;
+    K.xmFused   = xmOut != nullptr;
+    K.exactList = l2;
     fa.box = na.box, fa.powTab = na.powTab, fa.stats = na.stats, fa.clStats = na.clStats;
 
     // the skin build: the search with radii 2 h (1 + s), no h iteration, skin lists and counts as its outputs
     NsArgs b   = na;
-    b.skin1    = 1.0f + K.factor;
+    b.skin1    = 1.0f + K.built;
     b.iterateH = 0;
     b.nloc     = sloc;
     b.ngmax    = K.ngmaxS;
@@ -1513,7 +1544,6 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
     SIM_HIP(hipMemsetAsync(l2, 0, 4, st));
     if (!reuse)
     {
-        SIM_HIP(hipMemsetAsync(odo, 0, 4 * s->cap, st));
         SIM_HIP(findNeighbors(b, st));
         fa.fresh = 1;
     }
@@ -1551,10 +1581,30 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
         {
             x.subset = l2;
             SIM_HIP(findNeighbors(x, st));
+            if (reuse)
+            {
+                // on a reuse step the walk takes the drifted tree's refreshed boxes, which overlap: should the exact
+                // search outgrow its capacities there, the step's search is redone from a full sync
+                SIM_HIP(hipMemcpyAsync(hl, na.stats, 4, hipMemcpyDeviceToHost, st));
+                SIM_HIP(hipStreamSynchronize(st));
+                if (hl[0] & 1u)
+                {
+                    SIM_HIP(hipMemsetAsync(na.stats, 0, 4, st));
+                    return kSkinResync;
+                }
+            }
             SIM_HIP(skinMarkStale(l2, ncl, acc, st)); // their skins are rebuilt next step
         }
     }
     SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
+    if (getenv("SX_SKIN_DEBUG"))
+    {
+        uint32_t f = 0;
+        SIM_HIP(hipMemcpyAsync(&f, na.stats, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        fprintf(stderr, "skin: reuse %d s %.3f clusters %u stale %u exact %u flags 0x%x mode %d\n", (int)reuse,
+                K.built, ncl, n1, n2, f, s->nsPolicy.mode);
+    }
     K.lastStale = n1, K.lastExact = n2;
     K.staleClusters += n1, K.exactClusters += n2;
     if (reuse)
@@ -1569,19 +1619,29 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st)
         K.forceBuild = false;
         K.sinceBuild = 0;
     }
-    // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once
-    if ((double)n1 > K.staleLimit * ncl)
+    // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once.  A
+    // stale-heavy step costs about a build; a skin with fewer than two clean reuse steps since its build saved
+    // nothing, so the next steps search without it (backoff, doubling up to 32 steps with every such skin)
+    const bool clean = (double)n1 <= K.staleLimit * ncl;
+    if (!reuse) K.cleanSinceBuild = 0;
+    else if (clean) K.cleanSinceBuild++;
+    if (!clean)
     {
         K.forceBuild = true;
-        if (reuse && K.sinceBuild < 2)
-        {
-            // the skin did not outlast its build: search without it for a while
-            K.backoff    = K.backoffLen;
-            K.backoffLen = std::min(2 * K.backoffLen, 32);
-        }
+        if (!reuse || K.cleanSinceBuild < 2) skinTooThin(K);
     }
-    else if (reuse && K.sinceBuild >= 2) K.backoffLen = 1;
+    if (clean && K.cleanSinceBuild >= 2) K.backoffLen = 4;
     return SX_OK;
+}
+
+//! XMass of the step: all clusters, or after a filter that computed it only the exact-search clusters
+void xmassRest(sx_sim* s, const HydroLaunch& H, PairArgs a, hipStream_t st)
+{
+    if (!s->skin.xmFused) return H.xmass(a, st);
+    if (!s->skin.lastExact) return;
+    a.clusterList = s->skin.exactList + 1;
+    a.listCount   = s->skin.lastExact;
+    H.xmass(a, st);
 }
 
 int localSync(sx_sim* s, hipStream_t st)
@@ -1685,6 +1745,8 @@ extern "C"
     {
         if (!s || !(factor >= 0.0f) || factor > 1.0f || maxReuse < 1) return SX_ERR_ARG;
         s->skin.factor   = factor;
+        s->skin.cur      = factor;
+        s->skin.built    = factor;
         s->skin.maxReuse = maxReuse;
         s->skin.valid    = false;
         return SX_OK;
@@ -1697,12 +1759,14 @@ extern "C"
         return SX_OK;
     }
 
-    int sx_sim_skin_stats(sx_sim* s, uint64_t out[8])
+    int sx_sim_skin_stats(sx_sim* s, uint64_t out[11])
     {
         if (!s) return SX_ERR_ARG;
         const auto& K = s->skin;
         out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
         out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = K.plainSteps;
+        out[8] = (uint64_t)std::lround(1e6 * K.built), out[9] = (uint64_t)std::lround(1e6 * K.cur);
+        out[10] = K.resyncs;
         return SX_OK;
     }
 
@@ -1930,8 +1994,13 @@ extern "C"
             s->skin.plainSteps++;
             skinOn = false;
         }
-        const bool reuse  = skinOn && s->skin.valid && !s->skin.forceBuild && s->skin.sinceBuild < s->skin.maxReuse;
+        bool reuse = skinOn && s->skin.valid && !s->skin.forceBuild && s->skin.sinceBuild < s->skin.maxReuse;
         if (!skinOn) s->skin.valid = false;
+        // h before a reuse step's filter (its h iteration), for a search redone from a full sync (kSkinResync)
+        float* hReuse = reuse ? s->mem.get<float>("skin.h0", s->cap) : nullptr;
+        if (reuse && !hReuse) return SX_ERR_NOMEM;
+        if (reuse) SIM_HIP(hipMemcpyAsync(hReuse, s->h + s->first, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
+        bool synced = false;
         // h before the h iteration, to redo the search if the halo margin proves too small
         float* h0     = dist ? s->work.get<float>("h0", s->cap) : nullptr;
         double margin = kHaloMargin;
@@ -1952,9 +2021,10 @@ extern "C"
                 }
                 SIM_HIP(hipMemcpyAsync(h0, s->h + s->first, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
             }
-            else if (attempt == 0 && !reuse)
+            else if (!reuse && !synced)
             {
                 if (int e = localSync(s, st)) return e;
+                synced = true;
             }
             if (attempt == 0) SIM_HIP(hipEventRecord(s->ev[ev++], st));
 
@@ -2017,9 +2087,28 @@ extern "C"
             SIM_HIP(hipEventRecord(s->kev[0], st));
             if (skinOn)
             {
-                if (int e = skinSearch(s, na, reuse, st)) return e;
+                // the fast variant's XMass (or the std density's xmass pass) rides on the filter's final pass
+                const bool fastXm = !sx_ctx_exact_internal(s->ctx);
+                float*     xmOut  = fastXm ? (s->p.propagator == 1 ? s->rho : s->xm) : nullptr;
+                RecT*      rtXm   = (fastXm && s->p.propagator != 1 && H.clusterLists) ? s->rt : nullptr;
+                const int e = skinSearch(s, na, reuse, st, xmOut, rtXm);
+                if (e == kSkinResync)
+                {
+                    // h as before the filter, then this step's search again after a full sync + build
+                    SIM_HIP(hipMemcpyAsync(s->h + s->first, hReuse, (s->last - s->first) * 4, hipMemcpyDeviceToDevice,
+                                           st));
+                    s->skin.resyncs++;
+                    if (s->skin.cleanSinceBuild < 2) skinTooThin(s->skin);
+                    reuse = false;
+                    continue;
+                }
+                if (e) return e;
             }
-            else SIM_HIP(findNeighbors(na, st));
+            else
+            {
+                s->skin.xmFused = false;
+                SIM_HIP(findNeighbors(na, st));
+            }
             SIM_HIP(hipEventRecord(s->kev[1], st));
             SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
             if (s->evStats) SIM_HIP(hipEventRecord(s->evStats, st));
@@ -2068,7 +2157,7 @@ extern "C"
             SIM_HIP(hipEventRecord(s->kev[2], st));
             PairArgs da = pa;
             da.xm       = s->rho; // computeDensity: xmass written to rho (xmass_gpu.cu:151-153)
-            H.xmass(da, st);
+            xmassRest(s, H, da, st);
             H.xmassToRho((uint32_t)s->first, (uint32_t)s->last, s->m, s->rho, st);
             SIM_HIP(hipEventRecord(s->kev[3], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
@@ -2125,7 +2214,7 @@ extern "C"
             {
                 PairArgs xa = pa;
                 xa.rtOut    = fused ? s->rt : nullptr;
-                H.xmass(xa, st);
+                xmassRest(s, H, xa, st);
             }
             SIM_HIP(hipEventRecord(s->kev[3], st));
             // ---- [xm] halos, VeDefGradh (overlapped: interior clusters while the halos are in flight)
@@ -2310,6 +2399,13 @@ extern "C"
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->lastStats.maxUnion      = s->statsHost[12];
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
+        if (reuse && s->skin.cleanSinceBuild <= 1 && !s->skin.forceBuild)
+        {
+            // the first clean step after a build, but most clusters would not survive another such drift: the skin
+            // cannot outlast two steps; stop using it now rather than after a stale-heavy step
+            const uint32_t ncl = (uint32_t)((s->last - s->first + kCluster - 1) / kCluster);
+            if ((double)s->statsHost[13] > s->skin.staleLimit * ncl) skinTooThin(s->skin);
+        }
         s->lastStats.build         = s->nsPolicy.lastBuild;
         if (s->statsHost[0] & 1u)
         {

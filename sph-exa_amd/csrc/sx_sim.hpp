@@ -67,6 +67,8 @@ struct BdtState
 struct SkinState
 {
     float    factor{0.08f};     // s: skin radius 2 h (1 + s); 0 = every step syncs and searches (the reference's flow)
+    float    cur{0.08f};        // s of the next build: doubled (up to kMaxSkin) while skins cannot outlast two steps
+    float    built{0.08f};      // s of the current skin lists
     int      maxReuse{24};      // steps after a full build before the next one at the latest
     float    staleLimit{0.125f}; // share of stale clusters in a step after which the next step does a full build
     bool     valid{false};      // every cluster's skin lists are current (a full build since the last state change)
@@ -75,11 +77,18 @@ struct SkinState
     uint32_t ngmaxS{0};         // skin-list capacity per target
     // a skin that does not outlast its build by two steps (fast flows: every cluster stale at once) costs more than it
     // saves: the next backoff steps search without it, backoffLen doubling with every such failure (up to 32)
-    int      backoff{0}, backoffLen{1};
+    int      backoff{0}, backoffLen{4};
+    int      cleanSinceBuild{0}; // reuse steps since the last full build with a stale share within the limit
     uint64_t plainSteps{0};     // steps searched without the skin while backing off
     // statistics: full builds, steps served by the filter, clusters rebuilt (stale), clusters sent to the exact search
     uint64_t builds{0}, reuseSteps{0}, staleClusters{0}, exactClusters{0};
+    // reuse steps whose search was redone from a full sync (clusters stale again after their rebuild on a reuse step:
+    // the exact search on the drifted tree's boxes could outgrow its capacities)
+    uint64_t resyncs{0};
     uint32_t lastStale{0}, lastExact{0};
+    // this step: the filter computed XMass of every cluster but the exact-search ones (exactList[1 ..], lastExact)
+    bool      xmFused{false};
+    uint32_t* exactList{nullptr};
 };
 
 } // namespace sx::sim

@@ -18,6 +18,7 @@
  *      written only by a cluster that completes.
  * This file is compiled with -ffp-contract=off (the double criterion must round like the reference).
  */
+#include "sx_kernel_poly.hpp"
 #include "sx_skin.hpp"
 #include "sx_traverse.hpp"
 
@@ -34,6 +35,13 @@ constexpr int kWalkBlocks = (nlocWords(256) + kWalkPF - 1) / kWalkPF;
 constexpr int kB       = kCluster;
 
 __device__ __forceinline__ int cellIndex(double v, const SkinGrid& g, int d) { return gridCell(v, g, d); }
+
+//! |(x, y, z)| of float differences, rounded upwards (an upper bound of the exact length of the exact differences:
+//! each float difference is within 2^-24 relative, the sum of squares and the root within a few ulp more)
+__device__ __forceinline__ float norm3up(float x, float y, float z)
+{
+    return sqrtf(fmaf(x, x, fmaf(y, y, z * z))) * (1.0f + 0x1p-18f) + 1e-30f;
+}
 
 //! leaf boxes from their particles (relative to the geometric center, minimum image), one wave per leaf node
 __global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* internalToLeaf, const uint32_t* layout,
@@ -161,9 +169,12 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     float          hi   = a.h[iS];
     const float    h0   = hi;
     const float    hbi  = a.fresh ? hi : a.hb[iS];
-    const float    odoi = a.odo[iS];
-    const float    di   = a.fresh ? 0.0f : fmaxf(0.0f, odoi - a.ob[iS]);
-    const float    Ri   = 2.0f * (hbi * a.skin1);
+    // the last step's displacement relative to the cluster's reference particle (its first): this target's relative
+    // path since the build, d_i (rounding of the float displacements pushed upwards)
+    const float    ux = a.dispX[c0], uy = a.dispY[c0], uz = a.dispZ[c0];
+    const float    di = a.fresh ? 0.0f
+                                : a.rel[iS] + norm3up(a.dispX[iS] - ux, a.dispY[iS] - uy, a.dispZ[iS] - uz);
+    const float    Ri = 2.0f * (hbi * a.skin1);
     const uint32_t scount = valid ? a.scnt[i] - 1u : 0u;
     const uint32_t U      = __builtin_amdgcn_readfirstlane(a.ucountS[c]);
     const float    kEps   = 0x1p-16f;
@@ -218,7 +229,17 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
                     r /= nk[d];
                     if (a.grid.pbc[d]) k[d] = wrapCell(k[d], a.grid.n);
                 }
-                gmx = fmaxf(gmx, __uint_as_float(a.cells[((size_t)k[2] * a.grid.n + k[1]) * a.grid.n + k[0]]));
+                const size_t nc   = (size_t)a.grid.n * a.grid.n * a.grid.n;
+                const size_t cell = ((size_t)k[2] * a.grid.n + k[1]) * a.grid.n + k[0];
+                const uint32_t lx = a.cells[cell], ly = a.cells[nc + cell], lz = a.cells[2 * nc + cell];
+                if (lx != 0xffffffffu) // a cell without particles has no range
+                {
+                    // the largest |d - u| over the cell's component ranges
+                    const float ex = fmaxf(fabsf(orderedFloat(lx) - ux), fabsf(orderedFloat(a.cells[3 * nc + cell]) - ux));
+                    const float ey = fmaxf(fabsf(orderedFloat(ly) - uy), fabsf(orderedFloat(a.cells[4 * nc + cell]) - uy));
+                    const float ez = fmaxf(fabsf(orderedFloat(lz) - uz), fabsf(orderedFloat(a.cells[5 * nc + cell]) - uz));
+                    gmx = fmaxf(gmx, norm3up(ex, ey, ez));
+                }
             }
         }
         gmx = waveMax(gmx);
@@ -240,24 +261,29 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
             if (threadIdx.x == 0) a.stale[1 + atomicAdd(&a.stale[0], 1u)] = c;
             return;
         }
+        // one more drift like the one since the build would make the cluster stale (stats[13]: the host stops using
+        // skins that cannot outlast two steps, sx_sim.cpp)
+        if (!a.fresh && blockAny(valid && 2.0f * hi + 2.0f * (di + A) > Ri * (1.0f - kEps)) && threadIdx.x == 0)
+            atomicAdd(&a.stats[13], 1u);
     }
 
     // ---- 2. stage U_s: every thread's entries, all loads in flight together
     const uint32_t* un = a.uni + (size_t)c * a.ucap + a.uoff;
     float           pmax;
     {
-        constexpr int S = kSkinCap / kB;
+        constexpr int S = (kSkinCap + kB - 1) / kB; // every entry of a union up to kSkinCap
         uint32_t      js[S];
 #pragma unroll
         for (int q = 0; q < S; ++q)
         {
             // unconditional (clamped): a load under a condition is waited for at the branch merge
-            js[q] = un[min(threadIdx.x + q * kB, U - 1u)];
+            js[q] = un[min(threadIdx.x + q * kB, U ? U - 1u : 0u)];
         }
         double px[S], py[S], pz[S];
+        float  mq[S];
 #pragma unroll
         for (int q = 0; q < S; ++q)
-            px[q] = a.x[js[q]], py[q] = a.y[js[q]], pz[q] = a.z[js[q]];
+            px[q] = a.x[js[q]], py[q] = a.y[js[q]], pz[q] = a.z[js[q]], mq[q] = a.m[js[q]];
         float pm = 0.0f;
 #pragma unroll
         for (int q = 0; q < S; ++q)
@@ -268,7 +294,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
                 const float fx = (float)foldPbc(px[q] - ox, a.box, 0);
                 const float fy = (float)foldPbc(py[q] - oy, a.box, 1);
                 const float fz = (float)foldPbc(pz[q] - oz, a.box, 2);
-                s_rec[u]       = make_float4(fx, fy, fz, fmaf(fx, fx, fmaf(fy, fy, fz * fz)));
+                s_rec[u]       = make_float4(fx, fy, fz, mq[q]);
                 pm             = fmaxf(pm, fabsf(fx) + fabsf(fy) + fabsf(fz));
             }
         }
@@ -331,38 +357,47 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
             end(b);
         }
     };
-    float          cr = 0, tol = 0;
+    float          r2f = 0, tol = 0;
     double         radSq = 0;
     bool           safe = true, usePbc = false;
-    //! the float test (sx_neighbors.hip's form) with the reference's double criterion where |t| may be rounding
+    float          lastR2 = 0, lastM = 0; // r^2 and m_j of the entry test() accepted last (the fused XMass)
+    //! t = |p - r|^2 - 4h^2 in float (p, r relative to the cluster origin), with the reference's double criterion
+    //! where |t| may be rounding (the bound of sx_neighbors.hip's |p|^2 + |r|^2 - 2p.r form, which covers this one)
     auto test = [&](uint32_t p, int) -> bool {
-        const float4 q = s_rec[p];
-        float        t = q.w + cr;
-        t              = fmaf(-2.0f * xr, q.x, t);
-        t              = fmaf(-2.0f * yr, q.y, t);
-        t              = fmaf(-2.0f * zr, q.z, t);
-        bool hit       = t < 0.0f;
+        const float4 q  = s_rec[p];
+        const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+        float        r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+        const float  t  = r2 - r2f;
+        bool         hit = t < 0.0f;
         if (!safe || fabsf(t) <= tol)
         {
             const uint32_t j  = un[p];
-            double         dx = a.x[j] - xi, dy = a.y[j] - yi, dz = a.z[j] - zi;
+            double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
             if (usePbc)
             {
-                dx = foldPbc(dx, a.box, 0);
-                dy = foldPbc(dy, a.box, 1);
-                dz = foldPbc(dz, a.box, 2);
+                ex = foldPbc(ex, a.box, 0);
+                ey = foldPbc(ey, a.box, 1);
+                ez = foldPbc(ez, a.box, 2);
             }
-            hit = dx * dx + dy * dy + dz * dz < radSq;
+            const double d2 = ex * ex + ey * ey + ez * ez;
+            hit             = d2 < radSq;
+            r2              = (float)d2;
         }
+        lastR2 = r2, lastM = q.w;
         return hit; // j != i: the build's skin list never holds the target itself
     };
+    const float mi   = a.m[iS];
+    float       rho0 = mi, hInv2 = 0; // fused XMass (xmassJLoop, hydro_ve/xmass_kern.hpp:50-79) of the final pass
     while (true)
     {
         for (uint32_t u = threadIdx.x; u < U; u += kB)
             s_hit[u] = 0;
         __syncthreads();
-        const float  r2f = 4.0f * hi * hi;
+        r2f              = 4.0f * hi * hi;
         radSq            = (double)r2f;
+        const float hInv = 1.0f / hi;
+        hInv2            = hInv * hInv;
+        rho0             = mi;
         const double tw  = 2.0 * (double)hi;
         const bool inside = (xi - tw >= a.box.lim[0]) && (yi - tw >= a.box.lim[2]) && (zi - tw >= a.box.lim[4]) &&
                             (xi + tw <= a.box.lim[1]) && (yi + tw <= a.box.lim[3]) && (zi + tw <= a.box.lim[5]);
@@ -375,7 +410,6 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
             const float rd = d == 0 ? xr : (d == 1 ? yr : zr);
             if (a.box.pbc[d] && (fabsf(rd) + 2.05f * hi) >= 0.49f * (float)a.box.l[d]) safe = false;
         }
-        cr = fmaf(xr, xr, fmaf(yr, yr, fmaf(zr, zr, -r2f)));
         // |t| below tol may be rounding: those entries take the double criterion (sx_neighbors.hip's bound, with
         // E >= |p| + |r| over the staged entries)
         const float E = pmax + fabsf(xr) + fabsf(yr) + fabsf(zr);
@@ -391,6 +425,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
                      s_hit[p] = 1;
                      bits |= 1u << e;
                      ++st;
+                     if (a.xmOut) rho0 += kernelWt(lastR2 * hInv2) * lastM;
                  }
                  ++cnt;
              },
@@ -484,10 +519,15 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         a.nc[i] = count + 1;
         if (a.iterateH) a.h[i] = hi;
         if (a.rxOut) a.rxOut[i] = RecX{xi, yi, zi, hi, a.m[i]};
-        if (a.fresh)
+        if (a.fresh) a.hb[i] = h0;
+        a.rel[i] = di; // 0 for a fresh cluster
+        if (a.xmOut)
         {
-            a.hb[i] = h0;
-            a.ob[i] = odoi;
+            const float hInv  = 1.0f / hi;
+            const float h3Inv = hInv * hInv * hInv;
+            const float xm    = (float)((double)mi / ((double)rho0 * a.K * (double)h3Inv));
+            a.xmOut[i]        = xm;
+            if (a.rtXm) a.rtXm[i] = RecT{xm, 0.0f, 0.0f, 0.0f};
         }
     }
     if (threadIdx.x == 0)

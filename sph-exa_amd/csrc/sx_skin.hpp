@@ -10,13 +10,16 @@
  * union (the U_s entries some target hit, in U_s order) at the slot's start, exactly what the search leaves for the
  * pair kernels.
  *
- * Validity (checked by the filter for every target, every step): a particle j outside i's skin list at the build
- * (|x_i^b - x_j^b| >= R_i) can now be closer than 2 h_i only if the two moved towards each other by R_i - 2 h_i.
- * Before it entered the ball of radius R_i around i it was outside it; from then on it sits, at the end of every step,
- * inside the cluster's region (the targets' box grown by max R), so each of its steps is bounded by that step's
- * largest displacement in the region (the displacement grid, a max over cells of the end-of-step positions), and the
- * running sum of those maxima since the build, A_C, bounds its approach; i's own approach is its path length d_i.
- * So   2 h_i + d_i + A_C <= R_i (1 - eps)   guarantees the skin list holds every current neighbor of i.  A cluster
+ * Validity (checked by the filter for every target, every step), Galilean invariant: with u(t) any displacement per
+ * step (here the step's displacement of the cluster's first particle), x_i - x_j changes by sum_t (d_i(t) - u(t)) -
+ * (d_j(t) - u(t)).  A particle j outside i's skin list at the build (|x_i^b - x_j^b| >= R_i) can now be closer than
+ * 2 h_i only if the relative paths add up to R_i - 2 h_i.  From its last step outside the ball of radius R_i around i
+ * on, j sits at the end of every step inside the cluster's region (the targets' box grown by max R), so each of its
+ * steps is bounded by that step's largest |d - u| in the region (the displacement grid: per cell the component ranges
+ * of the end-of-step positions' displacements), and the running sum of those maxima since the build, A_C, bounds its
+ * part; i's part is its own relative path d_i = sum_t |d_i(t) - u(t)|.
+ * So   2 h_i + d_i + A_C <= R_i (1 - eps)   guarantees the skin list holds every current neighbor of i.  A flow that
+ * moves a region as a whole (Noh's infall) does not use up the skin; only relative motion does.  A cluster
  * failing it for some target (or whose build overflowed a capacity) is STALE: it is rebuilt on the spot (a build over
  * the stale clusters only, on node boxes refreshed from the current positions, then the filter); a cluster stale
  * again (its h iteration outgrew the fresh skin) takes the exact search, which writes its lists directly.
@@ -60,16 +63,22 @@ struct SkinArgs
     // skin state
     const uint32_t* sloc; // skin lists (nlocWords(ngmaxS) words per target, lane-interleaved like nloc)
     const uint32_t* scnt; // skin count + 1 per target (the build's nc)
-    float*          hb;   // h at the build
-    float*          ob;   // path length at the build
-    const float*    odo;  // path length since the last full build
-    float*          acc;  // per cluster: sum of the per-step displacement maxima of its region since its build
-    const uint32_t* cells; // displacement grid (float bits, per-step maxima)
+    float*          hb;    // h at the build
+    float*          rel;   // per target: its path relative to its cluster's reference particle since the build
+    const float *   dispX, *dispY, *dispZ; // the last step's displacement of every particle
+    float*          acc;   // per cluster: sum over the steps since its build of the largest displacement in its region
+                           // relative to the reference particle (the first of the cluster)
+    const uint32_t* cells; // displacement grid: per cell the component ranges of the last step (kGridWords planes)
     SkinGrid        grid;
     const uint32_t* list;  // nullable: the clusters list[1 .. list[0]], else all
     uint32_t*       stale; // [0] count, [1..] stale clusters (output)
     DevBox          box;
     const float*    powTab;
+    // nullable: the fused XMass (xmassJLoop on the final lists, as sx_hydro_cluster.hip's xmassKernel): xm of every
+    // completed target (the std propagator's density seam passes rho), and its RecT {xm, 0, 0, 0}
+    float*          xmOut;
+    RecT*           rtXm;
+    double          K;
     uint32_t*       stats;   // kStatsWords (failures)
     uint4*          clStats; // per cluster {max count, stored, skin entries walked, union}
 };

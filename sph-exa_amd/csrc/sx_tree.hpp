@@ -150,7 +150,8 @@ struct NbLists
 constexpr int kStatsWords = 28; //!< [0] error flags, [1] failures, [2] max count, [3] scratch, u64 at [4] stored
                                 //!< neighbors, [6] candidates tested, [8] union entries, [10] clusters the
                                 //!< compact build handed to the large one, [11] the compact build ran first,
-                                //!< [12] the largest cluster union (local lists), [13..27] spare
+                                //!< [12] the largest cluster union (local lists), [13] clusters whose skin
+                                //!< the next step's drift would exhaust (sx_skin.hip), [14..27] spare
 
 //! which search build runs: the compact one (four workgroups per CU) with a device-side fallback to the large one,
 //! or the large one directly.  Host state of one caller (context or sim), fed with the stats of each finished

@@ -641,10 +641,13 @@ class Sim:
         self.ctx.check(self.L.sx_sim_rebuild_lists(self.h), "rebuild_lists")
 
     def skin_stats(self):
-        out = (C.c_uint64 * 8)()
+        out = (C.c_uint64 * 11)()
         self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
-        return dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
-                         "capacity", "plain_steps"], list(out)))
+        d = dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
+                      "capacity", "plain_steps"], list(out)[:8]))
+        d["factor"], d["next_factor"] = out[8] * 1e-6, out[9] * 1e-6
+        d["resyncs"] = out[10]
+        return d
 
     def neighbor_sets(self):
         """the last step's neighbor lists as {particle id: sorted array of neighbor ids} (sx_sim_export_neighbors)"""
