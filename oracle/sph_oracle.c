@@ -1178,6 +1178,40 @@ static float avRvCorrection(float rx, float ry, float rz, float eta_ab, float et
     return -phi_ab * (dmy1 + dmy2);
 }
 
+/* error scale of the avClean correction (tests only, with the scales on): per unit of the checker's rtol, the change
+ * of avRvCorrection when the velocity gradients gi, gj carry a relative error of that size.  The correction is
+ * ill-conditioned where its quadratic forms dmy1, dmy2 cancel (A_ab = dmy1 / dmy2): the sensitivity of q is
+ * propagated, capped at q's full range [0, 1] (5e4 = 1 / 2e-5, the step checker's rtol) */
+static double avRvCorrectionScale(float rx, float ry, float rz, float eta_ab, float eta_crit, const float* gi,
+                                  const float* gj)
+{
+    const double x = fabs((double)rx), y = fabs((double)ry), z = fabs((double)rz);
+    const double d1 = dot3(rx, ry, rz, gi[0] * rx + gi[1] * ry + gi[2] * rz, gi[3] * ry + gi[4] * rz, gi[5] * rz);
+    const double d2 = dot3(rx, ry, rz, gj[0] * rx + gj[1] * ry + gj[2] * rz, gj[3] * ry + gj[4] * rz, gj[5] * rz);
+    const double S1 = x * (fabs(gi[0]) * x + fabs(gi[1]) * y + fabs(gi[2]) * z) + y * (fabs(gi[3]) * y + fabs(gi[4]) * z) +
+                      z * fabs(gi[5]) * z;
+    const double S2 = x * (fabs(gj[0]) * x + fabs(gj[1]) * y + fabs(gj[2]) * z) + y * (fabs(gj[3]) * y + fabs(gj[4]) * z) +
+                      z * fabs(gj[5]) * z;
+    double dmy3 = 1.0;
+    if (eta_ab < eta_crit)
+    {
+        const double e = 5.0 * ((double)eta_ab - eta_crit);
+        dmy3           = exp(-e * e);
+    }
+    const double kCap = 5e4;
+    double       uq   = kCap, q = 1.0;
+    if (d2 != 0.0 && d1 != 0.0)
+    {
+        const double A  = d1 / d2;
+        const double uA = fabs(A) * (S1 / fabs(d1) + S2 / fabs(d2));
+        q               = 4.0 * A / ((1.0 + A) * (1.0 + A));
+        q               = q < 0.0 ? 0.0 : (q > 1.0 ? 1.0 : q);
+        const double dq = fabs(4.0 * (1.0 - A) / ((1.0 + A) * (1.0 + A) * (1.0 + A)));
+        uq              = fmin(kCap, dq * uA);
+    }
+    return 0.5 * dmy3 * (uq * fabs(d1 + d2) + q * (S1 + S2));
+}
+
 static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t* nb, unsigned cnt, ox_state* s,
                           float Atmin, float Atmax, float ramp, int avClean, float* maxvsignal)
 {
@@ -1237,10 +1271,14 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
         float xmassj = s->xm[j];
         float rhoj   = kxj * mj / xmassj;
         float rv     = rx * vx_ij + ry * vy_ij + rz * vz_ij;
+        double urv   = 0.0; /* avClean: error scale of rv (avRvCorrectionScale), with the scales on */
         if (avClean)
         {
             float gradV_j[6] = {s->dV11[j], s->dV12[j], s->dV13[j], s->dV22[j], s->dV23[j], s->dV33[j]};
             rv += avRvCorrection(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gradV_j); /* stl::min */
+            if (g_sc_du)
+                urv = avRvCorrectionScale(rx, ry, rz, v2 < v1 ? v2 : v1, eta_crit, gradV_i, gradV_j) +
+                      0.01 * (fabs((double)rx * vx_ij) + fabs((double)ry * vy_ij) + fabs((double)rz * vz_ij));
         }
         float wij    = rv / dist;
         /* artificial_viscosity<float> (kernels.hpp:70-84): (alpha_i + alpha_j) / 4.0 is a double */
@@ -1291,6 +1329,18 @@ static void momentumJLoop(uint32_t i, double K, const ox_box* b, const uint32_t*
             sA += fabs((double)momentum_i) * (fabs((double)tA1i) + fabs((double)tA2i) + fabs((double)tA3i)) +
                   fabs((double)momentum_j) * (fabs((double)tA1j) + fabs((double)tA2j) + fabs((double)tA3j)) +
                   fabs((double)a_visc_x) + fabs((double)a_visc_y) + fabs((double)a_visc_z);
+            if (urv > 0.0 && wij < 0.0)
+            {
+                /* the viscosity's change with rv: d(-s w)/dw, s = (alpha_i + alpha_j)/4 (c_i + c_j) - 2 w */
+                const double dvis = fabs((double)(alpha_i + s->alpha[j]) / 4.0 * (ci + cj) - 4.0 * wij) * urv / dist;
+                const double wi = (double)mj / rhoi, wj = (double)mj / rhoj;
+                sV += dvis * 0.5 *
+                      (wi * (fabs((double)tA1i * vx_ij) + fabs((double)tA2i * vy_ij) + fabs((double)tA3i * vz_ij)) +
+                       wj * (fabs((double)tA1j * vx_ij) + fabs((double)tA2j * vy_ij) + fabs((double)tA3j * vz_ij)));
+                sA += dvis * 0.5 *
+                      (wi * (fabs((double)tA1i) + fabs((double)tA2i) + fabs((double)tA3i)) +
+                       wj * (fabs((double)tA1j) + fabs((double)tA2j) + fabs((double)tA3j)));
+            }
         }
     }
     if (g_sc_du)

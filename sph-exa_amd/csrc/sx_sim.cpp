@@ -191,6 +191,7 @@ __global__ void histKernel(const uint64_t* keys, size_t n, uint32_t* bins)
     if (i < n) atomicAdd(&bins[keys[i] >> (63 - kHistBits)], 1u);
 }
 
+//! out[q] = first local key >= split[q] (out[0] = 0, out[P] = n: the whole range is assigned)
 __global__ void lowerBoundsKernel(const uint64_t* keys, size_t n, const uint64_t* split, int P, uint64_t* out)
 {
     int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -203,7 +204,15 @@ __global__ void lowerBoundsKernel(const uint64_t* keys, size_t n, const uint64_t
         if (keys[mid] < v) lo = mid + 1;
         else hi = mid;
     }
-    out[q] = lo;
+    out[q] = q == 0 ? 0 : (q == P ? n : lo);
+}
+
+//! per peer count = difference of consecutive segment boundaries (u64 or u32), into the count-exchange buffer
+__global__ void diffCountsKernel(const uint64_t* b64, const uint32_t* b32, int P, uint64_t* out)
+{
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    out[q] = b64 ? b64[q + 1] - b64[q] : (uint64_t)(b32[q + 1] - b32[q]);
 }
 
 __global__ void packPRecKernel(Fields f, size_t n, PRec* out)
@@ -377,7 +386,7 @@ __global__ void scatterIdxKernel(const uint32_t* flag, const uint32_t* scan, siz
 //! start of every peer's send list in the scan (P entries) and the total (entry P)
 __global__ void segStartsKernel(const uint32_t* scan, size_t n, int P, uint32_t* out)
 {
-    const int q = threadIdx.x;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q <= P) out[q] = scan[q < P ? (size_t)q * (n + 1) : (size_t)P * (n + 1) - 1];
 }
 
@@ -407,6 +416,11 @@ __global__ void cellFlagKernel(const uint64_t* keys, size_t n, uint32_t* flag)
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i > n) return;
     flag[i] = (i < n && (i == 0 || (keys[i] >> kCellShift) != (keys[i - 1] >> kCellShift))) ? 1u : 0u;
+}
+
+__global__ void cellCountCheckKernel(const uint32_t* total, uint32_t expected, unsigned* err)
+{
+    if (*total != expected) *err = 1u;
 }
 
 __global__ void cellScatterKernel(const uint64_t* keys, const uint32_t* flag, const uint32_t* scan, size_t n,
@@ -440,7 +454,7 @@ __global__ void reqScatterKernel(const GCell* cells, const uint32_t* reqFlag, co
 //! v[q] = scan[off[q]] for the P+1 segment boundaries
 __global__ void segmentAtKernel(const uint32_t* scan, const uint64_t* off, int P, uint32_t* out)
 {
-    int q = threadIdx.x;
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q <= P) out[q] = scan[off[q]];
 }
 
@@ -894,6 +908,38 @@ int countsOrAbort(sx_sim* s, std::vector<uint64_t>& send, std::vector<uint64_t>&
     return abort ? SX_ERR_NOMEM : SX_OK;
 }
 
+//! the same exchange for counts the device computed (cntBuf[0, P), e.g. diffCountsKernel): sent as they are (or the
+//! abort marker), and the sent and received counts read back in one synchronisation; sendOff = prefix sums of send
+int deviceCountsOrAbort(sx_sim* s, bool fail, hipStream_t st, std::vector<uint64_t>& send,
+                        std::vector<uint64_t>& sendOff, std::vector<uint64_t>& recv)
+{
+    const int P = s->comm->size();
+    uint64_t* h = s->work.pinned<uint64_t>("dom.cnth", 2 * (size_t)P);
+    if (!h || !s->cntBuf) return SX_ERR_NOMEM;
+    if (fail)
+    {
+        for (int q = 0; q < P; ++q)
+            h[q] = kAbortCount;
+        SIM_HIP(hipMemcpyAsync(s->cntBuf, h, 8 * (size_t)P, hipMemcpyHostToDevice, st));
+    }
+    std::vector<uint64_t> bytes(P, 8), off(P);
+    for (int q = 0; q < P; ++q)
+        off[q] = 8 * (uint64_t)q;
+    SIM_COMM(s->comm->alltoallv(s->cntBuf, bytes.data(), off.data(), s->cntBuf + P, bytes.data(), off.data(), st));
+    SIM_HIP(hipMemcpyAsync(h, s->cntBuf, 16 * (size_t)P, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipStreamSynchronize(st));
+    send.assign(h, h + P);
+    recv.assign(h + P, h + 2 * P);
+    sendOff.assign(P + 1, 0);
+    bool abort = fail;
+    for (int q = 0; q < P; ++q)
+    {
+        abort |= recv[q] == kAbortCount;
+        sendOff[q + 1] = sendOff[q] + (fail ? 0 : send[q]);
+    }
+    return abort ? SX_ERR_NOMEM : SX_OK;
+}
+
 int distributedSync(sx_sim* s, hipStream_t st, double margin)
 {
     sx::Transport* T  = s->comm;
@@ -928,25 +974,25 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     // every rank's particle count after the exchange: the histogram bins of its range (splitters are bin
     // boundaries), so the request-box counts of step 4 need no exchange
     std::vector<uint64_t> nlOf(P, 0);
+    s->cellsOf.assign(P, 0);
     for (int q = 0; q < P; ++q)
         for (uint64_t b = split[q] >> (63 - kHistBits); b < (split[q + 1] >> (63 - kHistBits)) && b < nb; ++b)
+        {
             nlOf[q] += hb[b];
+            s->cellsOf[q] += hb[b] != 0;
+        }
 
     // --- 3. particle exchange
     uint64_t* dsplit = s->work.get<uint64_t>("dom.split", P + 1);
     uint64_t* dseg   = s->work.get<uint64_t>("dom.seg", P + 1);
-    SIM_HIP(hipMemcpyAsync(dsplit, split.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
-    lowerBoundsKernel<<<1, 64, 0, st>>>(s->keys, nl, dsplit, P, dseg);
-    std::vector<uint64_t> seg(P + 1);
-    SIM_HIP(hipMemcpyAsync(seg.data(), dseg, 8 * (P + 1), hipMemcpyDeviceToHost, st));
-    SIM_HIP(hipStreamSynchronize(st));
-    seg[0] = 0;
-    seg[P] = nl;
-    std::vector<uint64_t> sendCnt(P), recvCnt;
-    for (int q = 0; q < P; ++q)
-        sendCnt[q] = seg[q + 1] - seg[q];
     s->cntBuf = s->work.get<uint64_t>("dom.cnt", 2 * P);
-    if (!s->cntBuf) return SX_ERR_NOMEM; // 16 B per rank, kept from the first sync on
+    if (!dsplit || !dseg || !s->cntBuf) return SX_ERR_NOMEM; // 16 B per rank, kept from the first sync on
+    // the send counts stay on the device: segments of the sorted keys -> counts -> the count exchange, read back
+    // together with the receive counts (one synchronisation)
+    SIM_HIP(hipMemcpyAsync(dsplit, split.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
+    lowerBoundsKernel<<<grid(P + 1, 64), 64, 0, st>>>(s->keys, nl, dsplit, P, dseg);
+    diffCountsKernel<<<grid(P, 64), 64, 0, st>>>(dseg, nullptr, P, s->cntBuf);
+    std::vector<uint64_t> sendCnt, seg, recvCnt;
     // the new local count is this rank's histogram bins (nlOf[r], the sum of the receive counts); the exchange
     // buffers are sized by it before the count exchange, so a failure is decided there on every rank
     PRec* sbuf = nullptr;
@@ -958,7 +1004,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         rbuf   = s->work.get<PRec>("dom.precv", nlOf[r]);
         noRoom = !sbuf || !rbuf;
     }
-    if (int e = countsOrAbort(s, sendCnt, recvCnt, noRoom, st)) return e;
+    if (int e = deviceCountsOrAbort(s, noRoom, st, sendCnt, seg, recvCnt)) return e;
     bool moved = false;
     for (int q = 0; q < P; ++q)
         moved |= (q != r) && (sendCnt[q] || recvCnt[q]);
@@ -1054,7 +1100,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         maskFlagsKernel<<<grid(nfb), 256, 0, st>>>(mark, nl, q0, nb, r, flag);
         SIM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nfb, st));
         if (scatter) scatterIdxKernel<<<grid(nfb), 256, 0, st>>>(flag, scan, nl, nb, base, s->sendIdx);
-        segStartsKernel<<<1, 128, 0, st>>>(scan, nl, nb, segs);
+        segStartsKernel<<<grid(nb + 1, 64), 64, 0, st>>>(scan, nl, nb, segs);
         SIM_HIP(hipMemcpyAsync(hseg, segs, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
         for (int j = 0; j < nb; ++j)
@@ -1066,35 +1112,60 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     };
     // the send list is sized by what the peers request (a local may go to several peers): with one batch the scan
     // is read before the scatter; with several, a counting pass first (the arena's growth does not keep contents)
-    uint64_t total = 0;
-    for (int q0 = 0; q0 < P && !fail; q0 += Pb)
+    uint64_t total   = 0;
+    bool     idxFail = false; // the send list could not be sized (one batch: decided after the count exchange)
+    if (!fail && Pb >= P)
     {
-        const int nb = std::min(Pb, P - q0);
-        if (int e = batch(q0, nb, false, total)) return e;
-        total += hseg[nb];
+        // one batch (the common case): the send counts stay on the device -- segment starts of the scan -> counts ->
+        // the count exchange, read back with the halo receive counts in one synchronisation; the send list is sized
+        // and scattered after it (flags and scan are kept)
+        const size_t nfb = (size_t)P * (nl + 1);
+        maskFlagsKernel<<<grid(nfb), 256, 0, st>>>(mark, nl, 0, P, r, flag);
+        SIM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmpB, flag, scan, (int)nfb, st));
+        segStartsKernel<<<grid(P + 1, 64), 64, 0, st>>>(scan, nl, P, segs);
+        diffCountsKernel<<<grid(P, 64), 64, 0, st>>>(nullptr, segs, P, s->cntBuf);
+        std::vector<uint64_t> off;
+        if (int e = deviceCountsOrAbort(s, false, st, s->haloSend, off, s->haloRecv)) return e;
+        for (int q = 0; q < P; ++q)
+            s->haloSendOff[q] = off[q];
+        total      = off[P];
+        s->sendIdx = s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
+        idxFail    = !s->sendIdx;
+        if (!idxFail) scatterIdxKernel<<<grid(nfb), 256, 0, st>>>(flag, scan, nl, P, 0, s->sendIdx);
     }
-    s->sendIdx = fail ? nullptr : s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
-    fail |= !s->sendIdx;
-    if (!fail && Pb >= P) scatterIdxKernel<<<grid(nf), 256, 0, st>>>(flag, scan, nl, P, 0, s->sendIdx);
-    else if (!fail)
+    else
     {
-        uint64_t base = 0;
-        for (int q0 = 0; q0 < P; q0 += Pb)
+        // several batches (the flags of all peers beyond kFlagCap): a counting pass, then the scatter pass, the
+        // counts exchanged on the host's copy
+        for (int q0 = 0; q0 < P && !fail; q0 += Pb)
         {
             const int nb = std::min(Pb, P - q0);
-            if (int e = batch(q0, nb, true, base)) return e;
-            base += hseg[nb];
+            if (int e = batch(q0, nb, false, total)) return e;
+            total += hseg[nb];
         }
+        s->sendIdx = fail ? nullptr : s->work.get<uint32_t>("dom.sendIdx", std::max<uint64_t>(1, total));
+        fail |= !s->sendIdx;
+        if (!fail)
+        {
+            uint64_t base = 0;
+            for (int q0 = 0; q0 < P; q0 += Pb)
+            {
+                const int nb = std::min(Pb, P - q0);
+                if (int e = batch(q0, nb, true, base)) return e;
+                base += hseg[nb];
+            }
+        }
+        if (int e = countsOrAbort(s, s->haloSend, s->haloRecv, fail, st)) return e;
     }
-    s->numSend = total;
-    if (int e = countsOrAbort(s, s->haloSend, s->haloRecv, fail, st)) return e;
+    s->numSend     = total;
     s->haloRecv[r] = 0;
     uint64_t nLow = 0, nHigh = 0;
     for (int q = 0; q < P; ++q)
         (q < r ? nLow : nHigh) += s->haloRecv[q];
     {
+        // the halo capacity (known once the receive counts are) and the send list, decided on every rank together
         bool full = false;
-        if (int e = anyRank(s, nLow + nl + nHigh > s->cap, st, full)) return e;
+        if (int e = anyRank(s, nLow + nl + nHigh > s->cap || idxFail, st, full)) return e;
         if (full) return SX_ERR_NOMEM;
     }
     s->haloRecvOff.assign(P, 0);
@@ -1132,10 +1203,25 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     if (ovl) SIM_HIP(hipEventRecord(s->evComm, cs));
     SIM_HIP(buildTree(s->work, s->keys, s->n, s->bucket, s->dbox, s->tree, st));
     if (ovl) SIM_HIP(hipStreamWaitEvent(st, s->evComm, 0));
-    unsigned errH = 0;
-    SIM_HIP(hipMemcpy(&errH, err, 4, hipMemcpyDeviceToHost));
-    if (errH) return SX_ERR_TRAVERSAL;
+    s->syncErr = err; // read after the search, with its statistics (syncErrEnqueue / syncErrFailed)
     return SX_OK;
+}
+
+//! the last sync's halo-marking flag -> host, ordered on st before the caller's next synchronisation
+int syncErrEnqueue(sx_sim* s, hipStream_t st)
+{
+    uint32_t* h = s->work.pinned<uint32_t>("dom.errh", 1);
+    if (!h) return SX_ERR_NOMEM;
+    *h = 0;
+    if (s->syncErr) SIM_HIP(hipMemcpyAsync(h, s->syncErr, 4, hipMemcpyDeviceToHost, st));
+    return SX_OK;
+}
+
+//! after that synchronisation: the halo marking of the last sync overflowed its traversal stack
+bool syncErrFailed(sx_sim* s)
+{
+    const uint32_t* h = s->work.pinned<uint32_t>("dom.errh", 1);
+    return h && *h != 0;
 }
 
 /*! Self-gravity with several ranks (replaces syncGrav + MultipoleHolder::upsweep/traverse of the reference,
@@ -1189,10 +1275,10 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     size_t tmpB = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, flag, scan, (int)nl + 1, st);
     SIM_HIP(hipcub::DeviceScan::ExclusiveSum(W.get<char>("g.scantmp", tmpB), tmpB, flag, scan, (int)nl + 1, st));
-    uint32_t* hw = W.pinned<uint32_t>("g.host", 2 * (P + 2));
-    SIM_HIP(hipMemcpyAsync(hw, scan + nl, 4, hipMemcpyDeviceToHost, st));
-    SIM_HIP(hipStreamSynchronize(st));
-    const int nCells  = (int)hw[0];
+    // the cell count is known from the sync's histogram (cellsOf); the device checks the scan agrees
+    if (s->cellsOf.size() != (size_t)P) return SX_ERR_ARG;
+    const int nCells = (int)s->cellsOf[r];
+    cellCountCheckKernel<<<1, 1, 0, st>>>(scan + nl, (uint32_t)nCells, &s->sc->gravErr);
     uint32_t* cellBeg = W.get<uint32_t>("g.cellBeg", nCells + 1);
     uint32_t* cellIds = W.get<uint32_t>("g.cellIds", nCells);
     cellScatterKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, flag, scan, nl, cellBeg, cellIds);
@@ -1201,9 +1287,9 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
                         farL2N, s->farTree.centers, s->farTree.sizes, invTheta, mine, st));
 
     // --- 2. all-gather the cells (rank order = key order)
-    std::vector<uint64_t> cnt(P, (uint64_t)nCells), rcnt;
-    cnt[r] = 0;
-    SIM_COMM(T->exchangeCounts(cnt, rcnt, st, s->cntBuf));
+    std::vector<uint64_t> cnt(P, (uint64_t)nCells), rcnt(s->cellsOf);
+    cnt[r]  = 0;
+    rcnt[r] = 0;
     std::vector<uint64_t> aOff(P + 1, 0);
     for (int q = 0; q < P; ++q)
         aOff[q + 1] = aOff[q] + rcnt[q];
@@ -1237,16 +1323,13 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     uint64_t* dOff = W.get<uint64_t>("g.aOff", P + 1);
     uint32_t* dAt  = W.get<uint32_t>("g.at", P + 1);
     SIM_HIP(hipMemcpyAsync(dOff, aOff.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
-    segmentAtKernel<<<1, 64 * ((P + 64) / 64), 0, st>>>(reqS, dOff, P, dAt);
-    SIM_HIP(hipMemcpyAsync(hw, dAt, 4 * (P + 1), hipMemcpyDeviceToHost, st));
-    SIM_HIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> reqCnt(P), reqOff(P), reqRecv;
-    for (int q = 0; q < P; ++q)
-        reqCnt[q] = hw[q + 1] - hw[q], reqOff[q] = hw[q];
-    const uint64_t hwReq = hw[P]; // near (requested) remote cells
-
-    // --- 4. requests to the owners, owners send the cells' particles
-    SIM_COMM(T->exchangeCounts(reqCnt, reqRecv, st, s->cntBuf));
+    segmentAtKernel<<<grid(P + 1, 64), 64, 0, st>>>(reqS, dOff, P, dAt);
+    // --- 4. requests to the owners (counts from the device, exchanged and read back in one synchronisation), owners
+    //        send the cells' particles
+    diffCountsKernel<<<grid(P, 64), 64, 0, st>>>(nullptr, dAt, P, s->cntBuf);
+    std::vector<uint64_t> reqCnt, reqOff, reqRecv;
+    if (int e = deviceCountsOrAbort(s, false, st, reqCnt, reqOff, reqRecv)) return e;
+    const uint64_t hwReq = reqOff[P]; // near (requested) remote cells
     std::vector<uint64_t> rrOff(P + 1, 0);
     for (int q = 0; q < P; ++q)
         rrOff[q + 1] = rrOff[q] + reqRecv[q];
@@ -1266,19 +1349,16 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, rsize, roff, (int)nReq + 1, st);
     SIM_HIP(hipcub::DeviceScan::ExclusiveSum(W.get<char>("g.scantmp3", tmpB), tmpB, rsize, roff, (int)nReq + 1, st));
     SIM_HIP(hipMemcpyAsync(dOff, rrOff.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
-    segmentAtKernel<<<1, 64 * ((P + 64) / 64), 0, st>>>(roff, dOff, P, dAt);
-    SIM_HIP(hipMemcpyAsync(hw, dAt, 4 * (P + 1), hipMemcpyDeviceToHost, st));
-    SIM_HIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> pCnt(P), pOff(P), pRecv;
-    for (int q = 0; q < P; ++q)
-        pCnt[q] = hw[q + 1] - hw[q], pOff[q] = hw[q];
-    const size_t nSend = hw[P];
+    segmentAtKernel<<<grid(P + 1, 64), 64, 0, st>>>(roff, dOff, P, dAt);
+    diffCountsKernel<<<grid(P, 64), 64, 0, st>>>(nullptr, dAt, P, s->cntBuf);
+    std::vector<uint64_t> pCnt, pOff, pRecv;
+    if (int e = deviceCountsOrAbort(s, false, st, pCnt, pOff, pRecv)) return e;
+    const size_t nSend = pOff[P];
     GPart*       psend = W.get<GPart>("g.psend", nSend);
     if (nReq)
         gatherCellsKernel<<<grid(nReq * 64), 256, 0, st>>>(rbeg, rsize, roff, nReq, s->x + s->first, s->y + s->first,
                                                            s->z + s->first, s->m + s->first, s->h + s->first,
                                                            s->keys + s->first, psend);
-    SIM_COMM(T->exchangeCounts(pCnt, pRecv, st, s->cntBuf));
     uint64_t nLow = 0, nHigh = 0;
     for (int q = 0; q < P; ++q)
         (q < r ? nLow : nHigh) += (q == r ? 0 : pRecv[q]);
@@ -1408,7 +1488,9 @@ int halosOutgrown(sx_sim* s, hipStream_t st, unsigned& hf)
     SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
     unsigned* hflg = s->work.pinned<unsigned>("dom.hflagh", 1);
     SIM_HIP(hipMemcpyAsync(hflg, flg, 4, hipMemcpyDeviceToHost, st));
+    if (int e = syncErrEnqueue(s, st)) return e;
     SIM_HIP(hipStreamSynchronize(st));
+    if (syncErrFailed(s)) return SX_ERR_TRAVERSAL;
     hf = *hflg;
     return SX_OK;
 }
@@ -2136,7 +2218,9 @@ extern "C"
                                                                          s->clsList, s->clsCount);
                 SIM_HIP(hipMemcpyAsync(s->clsHost, s->clsCount, 8, hipMemcpyDeviceToHost, st));
             }
+            if (int e = syncErrEnqueue(s, st)) return e;
             SIM_HIP(hipStreamSynchronize(st));
+            if (syncErrFailed(s)) return SX_ERR_TRAVERSAL;
             if (overlapping(s, H)) s->nInterior = s->clsHost[0], s->nBoundary = s->clsHost[1];
             hf = s->statsHost[3];
             if (!hf) break;

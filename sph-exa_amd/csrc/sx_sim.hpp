@@ -158,6 +158,11 @@ struct sx_sim
     uint64_t              numSend{0};
     uint64_t              numHalos{0};
     uint64_t*             cntBuf{nullptr};
+    // per rank: its particles' occupied level-6 cells after the last sync (the nonzero global-histogram bins of its
+    // SFC range; the splitters are bin boundaries), so the gravity cell all-gather needs no count exchange
+    std::vector<uint64_t> cellsOf;
+    uint32_t*             syncErr{nullptr}; // the last sync's halo-marking failure flag (device), read with the step's
+                                            // statistics instead of a round trip of its own
 
     // overlap of the halo exchanges with the pair kernels of the interior clusters (no halo in their union):
     // exchanges run on commStream, joined by events; cluster index lists built after each search

@@ -44,10 +44,30 @@ def main():
     comm.allreduce(dg.ptr, f.size, "sum_f64", stream)
     ctx.sync()
     assert np.array_equal(du.get(), u) and np.array_equal(df.get(), f) and np.array_equal(dg.get(), f)
+
+    # a zero-byte exchange (every peer empty: the sync's "nothing moves" case) must leave the RCCL group closed, and
+    # an allreduce on a stream other than the context's must not leave one open either: the operations after each
+    # run normally
+    comm.alltoallv(src.ptr, [0], [0], dst.ptr, [0], [0], stream)
+    comm.allreduce(du.ptr, u.size, "sum_u32", stream)
+    hip = C.CDLL("libamdhip64.so")
+    other = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(other)) == 0
+    dh = ctx.upload(u)
+    comm.allreduce(dh.ptr, u.size, "sum_u32", other.value)
+    assert hip.hipStreamSynchronize(other) == 0
+    ctx.L.sx_memset(ctx.h, dst.ptr, 0, 1200)
+    comm.alltoallv(src.ptr, [1000], [0], dst.ptr, [1000], [0], stream)
+    comm.allreduce(df.ptr, f.size, "min_f64", stream)
+    ctx.sync()
+    assert hip.hipStreamDestroy(other) == 0
+    assert np.array_equal(dh.get(), u) and np.array_equal(du.get(), u) and np.array_equal(df.get(), f)
+    assert np.array_equal(dst.get()[:1000], payload)
     comm.close()
     ctx.close()
     dist.destroy_process_group()
-    print("RCCL one-rank OK: alltoallv (self segment) and allreduce sum_u32/min_f64/sum_f64 through RcclTransport")
+    print("RCCL one-rank OK: alltoallv (self segment, zero bytes) and allreduce sum_u32/min_f64/sum_f64 through "
+          "RcclTransport, on the context stream and another stream")
 
 
 if __name__ == "__main__":

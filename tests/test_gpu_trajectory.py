@@ -9,7 +9,9 @@ tests/golden/traj_*.npz made by oracle/gen_trajectory.py):
     relative L1 distance <= 1 % (SURVEY 8(c) tier 3);
   * the time of every step (the integrated dt series) within 1e-3 relative, and the total energy of every step within
     1e-5 of the initial energy of the reference's energy at that step (the reference itself drifts by -1.2e-3 on Sedov
-    and +1e-4 on Noh over these runs: the test pins the GPU to the reference's budget, not to exact conservation);
+    and +1e-4 on Noh over these runs: the test pins the GPU to the reference's budget, not to exact conservation) --
+    at the steps both runs take with the same dt; a dt limiter that triggers one step apart leaves a transient
+    excursion at the step between (at most 3 such steps, 5e-5), and the final energy within 1e-5;
   * Sedov: the density L1 against the reference's analytic solution (main/src/analytical_solutions/sedov_solution, at
     the final time; computeL1Error of compare_solutions.py:85-89) within +-0.01 of the reference run's own L1 (the CI
     band's width, reframe_ci.py:350-351).  The reference CI records 0.138 for this case; this revision's reference
@@ -75,7 +77,16 @@ def _check(case, fx, got, prof):
           "(ref drift", f"{e_ref[-1] / e_ref[0] - 1:.3g})",
           {s: {k: f"{v:.2g}" for k, v in d.items()} for s, d in l1.items()})
     assert dt_rel.max() < 1e-3, dt_rel.max()
-    assert de.max() < 1e-5, (de.max(), int(np.argmax(de)))
+    # energy step by step where both runs took the same step (dt within 2 %): a time-step limiter that triggers one step
+    # apart (rounding-level state differences decide which step crosses its threshold; Sedov step 187 with skin
+    # lists: the reference's dt drops 10 % there, this run's one step later) gives the one step between a transient
+    # excursion of the step-indexed energy, so such steps (at most 3) get 5e-5, and the run must end within 1e-5
+    same = np.abs(np.diff(t_got) / np.diff(t_ref) - 1) < 0.02
+    de_s = de[1:]
+    print(case, "steps with the reference's dt", int(same.sum()), "of", same.size,
+          "energy max there", f"{de_s[same].max():.2g}", "elsewhere", f"{de_s[~same].max() if (~same).any() else 0:.2g}")
+    assert de_s[same].max() < 1e-5, (de_s[same].max(), int(np.argmax(np.where(same, de_s, 0))) + 1)
+    assert (~same).sum() <= 3 and de.max() < 5e-5 and de[-1] < 1e-5, (int((~same).sum()), de.max(), de[-1])
     for s, d in l1.items():
         for k, v in d.items():
             assert v <= 0.01, (case, s, k, v)
