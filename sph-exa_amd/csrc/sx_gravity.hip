@@ -268,6 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
               args.last,
               args.G, args.active, args.interactions};
     __shared__ int  s_stack[4][kGStack];
+    __shared__ double s_tbox[4][4][6]; // per wave and quarter: target box center, half size
     __shared__ int  s_m2p[4][kGList];
     __shared__ int  s_p2p[4][kGList];
     __shared__ GSrc   s_src[FAST ? 1 : 4][kWave];
@@ -307,16 +308,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
             lo[d]  = fmin(lo[d], __shfl_xor(lo[d], o, 16));
             hiB[d] = fmax(hiB[d], __shfl_xor(hiB[d], o, 16));
         }
-    double tc[4][3], ts[4][3];
+    // the quarters' target boxes (center, half size): wave-uniform, read by every node test; in LDS (broadcast reads)
+    // -- as registers they did not stay scalar and were spilled to scratch inside the traversal loop
+    double* const tb = &s_tbox[wave][0][0];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq)
         for (int d = 0; d < 3; ++d)
         {
             const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
-            // wave-uniform: kept in scalar registers (48 VGPRs otherwise)
-            tc[qq][d]      = readfirstlaneD((h + l) * 0.5);
-            ts[qq][d]      = readfirstlaneD((h - l) * 0.5);
+            if (lane == 0) tb[6 * qq + d] = (h + l) * 0.5, tb[6 * qq + 3 + d] = (h - l) * 0.5;
         }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
     const uint64_t bv     = __ballot(valid); // quarters with at least one valid target (lanes fill in order)
     const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
                             (((bv >> 32) & 0xffffull) ? 4u : 0u) | (((bv >> 48) & 0xffffull) ? 8u : 0u);
@@ -342,8 +345,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         for (int qq = 0; qq < 4; ++qq)
         {
             if (!((mask >> qq) & 1u)) continue;
-            double d0 = fabs(tc[qq][0] - c0) - ts[qq][0], d1 = fabs(tc[qq][1] - c1) - ts[qq][1],
-                   d2 = fabs(tc[qq][2] - c2) - ts[qq][2];
+            const double* bq = tb + 6 * qq;
+            double d0 = fabs(bq[0] - c0) - bq[3], d1 = fabs(bq[1] - c1) - bq[4], d2 = fabs(bq[2] - c2) - bq[5];
             d0 += fabs(d0);
             d1 += fabs(d1);
             d2 += fabs(d2);
