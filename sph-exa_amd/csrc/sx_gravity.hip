@@ -25,8 +25,8 @@ namespace sx
 namespace
 {
 
-constexpr int kGStack = 512; //!< per-wave traversal stack (entries: node << 4 | quarter mask)
-constexpr int kGList  = 256; //!< per-wave M2P / P2P interaction lists
+constexpr int kGStack = 320; //!< per-wave traversal stack (entries: node << 4 | quarter mask)
+constexpr int kGList  = 176; //!< per-wave M2P / P2P interaction lists (LDS: 31 KB per workgroup, five per CU)
 
 //! leaf index -> node index (the reference's leafToInternal + numInternalNodes)
 __global__ void leafToNodeKernel(const int32_t* childOffsets, const int32_t* internalToLeaf, int numNodes,
@@ -241,7 +241,7 @@ struct __attribute__((aligned(16))) GSrc
 };
 
 #ifndef SX_GRAV_WPE
-#define SX_GRAV_WPE 4 // 128 VGPRs: four waves per SIMD without spills
+#define SX_GRAV_WPE 5 // 96 VGPRs: five waves per SIMD (a few spills, outside the evaluation loops)
 #endif
 //! COUNT: the per-target interaction counts (GravArgs::interactions, BhStats) -- a separate instantiation because the
 //! counters' registers cost the traversal 9 SGPR and 4 VGPR spills and 3.6 ms at Evrard n=300 (A/B)
