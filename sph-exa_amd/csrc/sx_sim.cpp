@@ -1591,8 +1591,9 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint32_t*   ucS   = s->mem.get<uint32_t>("skin.ucount", ncl);
     uint32_t*   l1    = s->mem.get<uint32_t>("skin.l1", ncl + 1);
     uint32_t*   l2    = s->mem.get<uint32_t>("skin.l2", ncl + 1);
-    uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 2);
-    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl)
+    uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 3);
+    uint8_t*    strk  = s->mem.get<uint8_t>("skin.streak", ncl);
+    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk)
         return SX_ERR_NOMEM;
 
     const SkinGrid g = skinGrid(s->dbox);
@@ -1626,39 +1627,48 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     SIM_HIP(hipMemsetAsync(l2, 0, 4, st));
     if (!reuse)
     {
+        SIM_HIP(hipMemsetAsync(strk, 0, ncl, st));
         SIM_HIP(findNeighbors(b, st));
         fa.fresh = 1;
     }
     else fa.fresh = 0; // the grid of this step's displacements came from the last position update
     fa.list  = nullptr;
     fa.stale = l1;
+    // reuse steps: a cluster stale again on the step after its rebuild goes straight to the exact search (l2)
+    fa.streak = reuse ? strk : nullptr;
+    fa.direct = reuse ? l2 : nullptr;
     SIM_HIP(skinFilter(fa, ncl, st));
     SIM_HIP(hipMemcpyAsync(hl, l1, 4, hipMemcpyDeviceToHost, st));
+    SIM_HIP(hipMemcpyAsync(hl + 1, l2, 4, hipMemcpyDeviceToHost, st));
     SIM_HIP(hipStreamSynchronize(st));
-    const uint32_t n1 = hl[0];
-    uint32_t       n2 = 0;
+    const uint32_t n1 = hl[0], nd = hl[1];
+    uint32_t       n2 = nd;
+    NsArgs         x  = na; // the exact search, for clusters whose h iteration outgrows even a fresh skin
+    if ((n1 || nd) && reuse)
+    {
+        // particles have left the cells of the last full sync's tree: the walk takes boxes of the current positions
+        double* c3 = s->mem.get<double>("skin.centers", 3 * (size_t)s->tree.numNodes);
+        double* s3 = s->mem.get<double>("skin.sizes", 3 * (size_t)s->tree.numNodes);
+        if (!c3 || !s3) return SX_ERR_NOMEM;
+        SIM_HIP(skinRefreshBoxes(s->tree, na.x, na.y, na.z, na.box, c3, s3, st));
+        b.centers = x.centers = c3;
+        b.sizes = x.sizes = s3;
+    }
     if (n1)
     {
-        NsArgs x = na; // the exact search, for clusters whose h iteration outgrows even a fresh skin
-        if (reuse)
-        {
-            // particles have left the cells of the last full sync's tree: the walk takes boxes of the current positions
-            double* c3 = s->mem.get<double>("skin.centers", 3 * (size_t)s->tree.numNodes);
-            double* s3 = s->mem.get<double>("skin.sizes", 3 * (size_t)s->tree.numNodes);
-            if (!c3 || !s3) return SX_ERR_NOMEM;
-            SIM_HIP(skinRefreshBoxes(s->tree, na.x, na.y, na.z, na.box, c3, s3, st));
-            b.centers = x.centers = c3;
-            b.sizes = x.sizes = s3;
-        }
-        b.subset = l1;
+        b.subset  = l1;
         SIM_HIP(findNeighbors(b, st));
-        fa.fresh = 1;
-        fa.list  = l1;
-        fa.stale = l2;
+        fa.fresh  = 1;
+        fa.list   = l1;
+        fa.stale  = l2; // appended after the direct ones
+        fa.streak = nullptr;
+        fa.direct = nullptr;
         SIM_HIP(skinFilter(fa, ncl, st));
-        SIM_HIP(hipMemcpyAsync(hl + 1, l2, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipMemcpyAsync(hl + 2, l2, 4, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
-        n2 = hl[1];
+        n2 = hl[2];
+    }
+    {
         if (n2)
         {
             x.subset = l2;
@@ -1685,10 +1695,10 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         SIM_HIP(hipMemcpyAsync(&f, na.stats, 4, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
         fprintf(stderr, "skin: reuse %d s %.3f clusters %u stale %u exact %u flags 0x%x mode %d\n", (int)reuse,
-                K.built, ncl, n1, n2, f, s->nsPolicy.mode);
+                K.built, ncl, n1 + nd, n2, f, s->nsPolicy.mode);
     }
-    K.lastStale = n1, K.lastExact = n2;
-    K.staleClusters += n1, K.exactClusters += n2;
+    K.lastStale = n1 + nd, K.lastExact = n2;
+    K.staleClusters += n1 + nd, K.exactClusters += n2;
     if (reuse)
     {
         K.reuseSteps++;
@@ -1704,7 +1714,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once.  A
     // stale-heavy step costs about a build; a skin with fewer than two clean reuse steps since its build saved
     // nothing, so the next steps search without it (backoff, doubling up to 32 steps with every such skin)
-    const bool clean = (double)n1 <= K.staleLimit * ncl;
+    const bool clean = (double)(n1 + nd) <= K.staleLimit * ncl;
     if (!reuse) K.cleanSinceBuild = 0;
     else if (clean) K.cleanSinceBuild++;
     if (!clean)

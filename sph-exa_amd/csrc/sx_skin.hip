@@ -141,6 +141,15 @@ __global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl
     }
 }
 
+//! a stale cluster goes to the rebuild list, or -- stale again on the step after its rebuild (a region whose relative
+//! motion outruns any skin: a shock, a convergent flow) -- straight to the exact-search list (a.direct)
+__device__ __forceinline__ void pushStale(const SkinArgs& a, uint32_t c)
+{
+    uint32_t* L = (a.direct && a.streak && a.streak[c]) ? a.direct : a.stale;
+    L[1 + atomicAdd(&L[0], 1u)] = c;
+    if (a.streak) a.streak[c] = 1;
+}
+
 __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numClusters)
 {
     // LDS: 39.9 KB, four workgroups per CU
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         const bool bad = valid && (scount > a.ngmaxS || !withinSkin(hi));
         if (blockAny(bad) || U > (uint32_t)kSkinCap || U > a.ucap - a.uoff)
         {
-            if (threadIdx.x == 0) a.stale[1 + atomicAdd(&a.stale[0], 1u)] = c;
+            if (threadIdx.x == 0) pushStale(a, c);
             return;
         }
         // one more drift like the one since the build would make the cluster stale (stats[13]: the host stops using
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         active = again;
         if (blockAny(outgrown))
         {
-            if (threadIdx.x == 0) a.stale[1 + atomicAdd(&a.stale[0], 1u)] = c;
+            if (threadIdx.x == 0) pushStale(a, c);
             return; // h, nc untouched; lists and union are rewritten by the rebuild
         }
         if (!blockAny(again)) break;
@@ -534,6 +543,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     {
         a.acc[c]    = a.fresh ? 0.0f : A;
         a.ucount[c] = ue;
+        if (a.streak && !a.fresh) a.streak[c] = 0; // served by its skin: a later stale step rebuilds it again
     }
     const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;
     const unsigned           nfail  = waveSum(failed);

@@ -72,6 +72,10 @@ struct SkinArgs
     SkinGrid        grid;
     const uint32_t* list;  // nullable: the clusters list[1 .. list[0]], else all
     uint32_t*       stale; // [0] count, [1..] stale clusters (output)
+    // nullable (reuse steps): per cluster 1 while its last stale step sent it to a rebuild and it has not been served
+    // by a skin since; such a cluster, stale again, is listed in `direct` (the exact search) instead of `stale`
+    uint8_t*        streak;
+    uint32_t*       direct;
     DevBox          box;
     const float*    powTab;
     // nullable: the fused XMass (xmassJLoop on the final lists, as sx_hydro_cluster.hip's xmassKernel): xm of every
