@@ -429,7 +429,7 @@ extern "C"
         a.stats          = c->stats;
         a.powTab         = ensurePowTab(c, p->ng0);
         a.prefilter      = 1;
-        a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(2u, last - first)); // >= clusters + 1 words: the redo list
+        a.hSave          = c->arena.get<float>("ns.hsave", std::max<uint32_t>(2u * ((last - first) / kCluster + 2u), last - first)); // the two redo lists
         a.policy         = &c->nsPolicy;
         a.clStats        = c->arena.get<uint4>("ns.clstats", (a.numGroups + kClusterWaves - 1) / kClusterWaves);
         a.active         = c->viewActive;

@@ -173,11 +173,11 @@ __device__ __forceinline__ uint32_t grabCluster(uint32_t* work, uint32_t numClus
 template<class Overlaps>
 __device__ __forceinline__ int clusterCollectLeaves(const int32_t* __restrict__ childOffsets, Overlaps&& overlaps,
                                                     int* queue, int* cand, uint2* s_cnt, int wave, int lane,
-                                                    bool& overflow)
+                                                    unsigned& overflow)
 {
     const uint64_t ltMask  = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int            numCand = 0, qh = 0, qt = 0;
-    overflow               = false;
+    overflow               = 0u; // bit 64: traversal queue, bit 32: candidate leaves (stats[0] bits)
     if (overlaps(0))
     {
         const int c0 = childOffsets[0];
@@ -222,13 +222,13 @@ __device__ __forceinline__ int clusterCollectLeaves(const int32_t* __restrict__ 
         numCand += (int)totL;
         qt += (int)totI;
         qh += consumed;
-        if (qt - qh > kQCap) overflow = true;
+        if (qt - qh > kQCap) overflow |= 64u;
         __syncthreads(); // the queue and cand writes are visible; s_cnt is rewritten by the next step
     }
     if (numCand > kCCap)
     {
-        overflow = true;
-        numCand  = kCCap;
+        overflow |= 32u;
+        numCand = kCCap;
     }
     return numCand;
 }
@@ -260,7 +260,9 @@ findNeighborsKernel(NsArgs a)
     const uint32_t numClusters =
         a.redoList ? __builtin_amdgcn_readfirstlane(a.redoList[0]) : (a.numGroups + kClusterWaves - 1) / kClusterWaves;
     if (numClusters == 0) return;
+#ifdef SX_NS_SMALL
     if (a.redo && blockIdx.x == 0 && threadIdx.x == 0) a.stats[11] = 1u; // the compact build ran first
+#endif
     const int      wave        = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: scalar
     const int      lane        = threadIdx.x & 63;
     NsWaveLds&     wl          = s_str.w[wave];
@@ -429,13 +431,17 @@ findNeighborsKernel(NsArgs a)
         if (threadIdx.x == 0) s_nreg = 0;
         __syncthreads();
         {
-            // regions: the wave box when it is coherent (no wider than 16 search radii), else its coherent
-            // 16-particle sub-group boxes and, for incoherent sub-groups, the spheres of their particles (all in
-            // registers: 16-lane then 64-lane shuffles over the valid lanes).  An SFC range can jump across empty
-            // space (the curve leaves and re-enters a sphere's surface), so a wave box may span a gap.
+            // regions: the wave box when it is coherent, else its coherent 16-particle sub-group boxes and, for
+            // incoherent sub-groups, the spheres of their particles (all in registers: 16-lane then 64-lane shuffles
+            // over the valid lanes).  Coherent: the box grown by the largest search radius is no wider than 20 of the
+            // group's smallest h (16 search radii for a uniform h) -- the box's candidates scale with the densest
+            // part's particles per volume, so a group spanning a density gradient (a collapsing core and its
+            // envelope) takes smaller boxes.  An SFC range can jump across empty space (the curve leaves and
+            // re-enters a sphere's surface), so a wave box may span a gap.
             double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
             double hb[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
             float  hq    = valid ? hi : 0.0f;
+            float  hqMin = valid ? hi : INFINITY;
 #pragma unroll
             for (int o = 8; o > 0; o >>= 1)
             {
@@ -444,10 +450,11 @@ findNeighborsKernel(NsArgs a)
                     lo[d] = fmin(lo[d], __shfl_xor(lo[d], o, 16));
                     hb[d] = fmax(hb[d], __shfl_xor(hb[d], o, 16));
                 }
-                hq = fmaxf(hq, __shfl_xor(hq, o, 16));
+                hq    = fmaxf(hq, __shfl_xor(hq, o, 16));
+                hqMin = fminf(hqMin, __shfl_xor(hqMin, o, 16));
             }
             double wlo[3] = {lo[0], lo[1], lo[2]}, whi[3] = {hb[0], hb[1], hb[2]};
-            float  hw     = hq;
+            float  hw     = hq, hwMin = hqMin;
 #pragma unroll
             for (int o = 16; o < 64; o <<= 1)
             {
@@ -456,7 +463,8 @@ findNeighborsKernel(NsArgs a)
                     wlo[d] = fmin(wlo[d], __shfl_xor(wlo[d], o, 64));
                     whi[d] = fmax(whi[d], __shfl_xor(whi[d], o, 64));
                 }
-                hw = fmaxf(hw, __shfl_xor(hw, o, 64));
+                hw    = fmaxf(hw, __shfl_xor(hw, o, 64));
+                hwMin = fminf(hwMin, __shfl_xor(hwMin, o, 64));
             }
             auto addRegion = [&](double x0, double x1, double y0, double y1, double z0, double z1, float h) {
                 const int k = atomicAdd(&s_nreg, 1);
@@ -468,15 +476,16 @@ findNeighborsKernel(NsArgs a)
                     s_reg[2 * k + 1] = make_double4(0.5 * (x1 - x0), 0.5 * (y1 - y0), 0.5 * (z1 - z0), (double)wave);
                 }
             };
+            const double coh  = a.coherence > 0.0f ? (double)a.coherence : 20.0;
             const double extW = fmax(whi[0] - wlo[0], fmax(whi[1] - wlo[1], whi[2] - wlo[2]));
-            if (extW <= 16.0 * (double)hw)
+            if (extW + 4.0 * (double)hw <= coh * (double)hwMin)
             {
                 if (lane == 0 && hw > 0.0f) addRegion(wlo[0], whi[0], wlo[1], whi[1], wlo[2], whi[2], hw);
             }
             else
             {
                 const double ext = fmax(hb[0] - lo[0], fmax(hb[1] - lo[1], hb[2] - lo[2]));
-                if (ext <= 16.0 * (double)hq)
+                if (ext + 4.0 * (double)hq <= coh * (double)hqMin)
                 {
                     if ((lane & 15) == 0 && hq > 0.0f) addRegion(lo[0], hb[0], lo[1], hb[1], lo[2], hb[2], hq);
                 }
@@ -501,13 +510,13 @@ findNeighborsKernel(NsArgs a)
             }
             return bits;
         };
-        bool      overflow = false;
+        unsigned  overflow = 0u;
         const int nCand    = clusterCollectLeaves(
             a.childOffsets, [&](int node) { return reachMask(node, true) != 0u; }, s_queue, s_cand, s_bfsCnt, wave,
             lane, overflow);
         if (wave == 0)
         {
-            if (lane == 0 && s_nreg > kMaxRegions) overflow = true; // regions dropped: the candidates may be short
+            if (lane == 0 && s_nreg > kMaxRegions) overflow |= 16u; // regions dropped: the candidates may be short
             // exclusive scan of the candidate leaf sizes
             uint32_t run = 0;
             for (int b = 0; b < nCand; b += kWave)
@@ -533,8 +542,9 @@ findNeighborsKernel(NsArgs a)
             if (lane == 0)
             {
                 s_cOff[nCand] = run;
-                // error bits: 2 = traversal queue / candidate-leaf list full, 4 = candidate space beyond u16
-                unsigned f = (overflow ? 2u : 0u) | ((local && run > (uint32_t)kCandSpace) ? 4u : 0u);
+                // error bits: 2 = traversal queue / candidate-leaf list full / regions dropped (which: 64 / 32 /
+                // 16), 4 = candidate space beyond u16
+                unsigned f = (overflow ? 2u | overflow : 0u) | ((local && run > (uint32_t)kCandSpace) ? 4u : 0u);
 #ifdef SX_NS_SMALL
                 if (a.forceOverflow) f |= 4u; // test hook (sx_set_search_mode 3): exercise the device-side fallback
 #endif
@@ -546,10 +556,19 @@ findNeighborsKernel(NsArgs a)
                 if (f && a.redo)
                 {
                     a.redo[1 + atomicAdd(&a.redo[0], 1u)] = c;
-                    atomicAdd(&a.stats[10], 1u);
+#ifdef SX_NS_SMALL
+                    atomicAdd(&a.stats[10], 1u); // compact -> large
+#else
+                    atomicAdd(&a.stats[17], 1u); // large -> large with smaller search regions
+#endif
                 }
                 else if (f && skinB) a.ucount[c] = 0xffffffffu;
-                else if (f) atomicOr(&a.stats[0], 1u | f);
+                else if (f)
+                {
+                    atomicOr(&a.stats[0], 1u | f);
+                    // a failing cluster for the error report: its index, candidate leaves and search regions
+                    if (atomicCAS(&a.stats[14], 0u, c + 1u) == 0u) a.stats[15] = (uint32_t)nCand, a.stats[16] = s_nreg;
+                }
                 s_numCand = f ? 0 : nCand;
             }
         }
@@ -1147,18 +1166,34 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
     // work counters: [0, 8) the first launch, [8, 16) the fallback launch
     if ((e = hipMemsetAsync(a.work, 0, 16 * sizeof(uint32_t), s))) return e;
     const int mode = a.policy ? a.policy->mode : 1;
+    const uint32_t ncl = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
     if (!a.hSave || mode == 1 || (mode == 0 && a.policy->useLarge()))
     {
-        NsArgs l   = a;
-        l.redoList = a.subset; // only the listed clusters, or all
+        NsArgs    l    = a;
+        uint32_t* over = a.hSave ? reinterpret_cast<uint32_t*>(a.hSave) : nullptr;
+        l.redoList     = a.subset; // only the listed clusters, or all
+        l.redo         = over;     // clusters over its capacities: again with smaller search regions (below)
+        if (over && (e = hipMemsetAsync(over, 0, sizeof(uint32_t), s))) return e;
         if ((e = findNeighborsOnce(l, s))) return e;
+        if (over)
+        {
+            NsArgs t    = a;
+            t.redoList  = over;
+            t.coherence = 10.0f;
+            t.work      = a.work + 8;
+            if ((e = findNeighborsOnce(t, s))) return e;
+        }
         return reduceClusterStats(a, s);
     }
     // compact build first: a cluster over its capacities is not written and goes to a redo list (in the hSave
     // scratch: clusters + 1 words fit in its last - first floats), which the large build then takes -- only those
-    // clusters, no host synchronisation, h untouched for them
-    uint32_t* redo = reinterpret_cast<uint32_t*>(a.hSave);
+    // clusters, no host synchronisation, h untouched for them; a cluster over the large build's capacities goes to
+    // a second list (after the first in the same scratch) that the large build takes again with smaller search
+    // regions (coherence 10: a group spanning a strong density gradient, e.g. a collapsing core and its envelope)
+    uint32_t*      redo  = reinterpret_cast<uint32_t*>(a.hSave);
+    uint32_t*      redo2 = redo + ncl + 1;
     if ((e = hipMemsetAsync(redo, 0, sizeof(uint32_t), s))) return e;
+    if ((e = hipMemsetAsync(redo2, 0, sizeof(uint32_t), s))) return e;
     NsArgs c        = a;
     c.forceOverflow = mode == 3;
     c.redo          = redo;
@@ -1166,8 +1201,15 @@ hipError_t findNeighbors(const NsArgs& a, hipStream_t s)
     if ((e = small::findNeighborsOnce(c, s))) return e;
     NsArgs b   = a;
     b.redoList = redo;
+    b.redo     = redo2;
     b.work     = a.work + 8;
     if ((e = findNeighborsOnce(b, s))) return e;
+    NsArgs t     = a;
+    t.redoList   = redo2;
+    t.coherence  = 10.0f;
+    t.work       = a.work; // the compact build's counters: reset below, after it finished (stream order)
+    if ((e = hipMemsetAsync(a.work, 0, 8 * sizeof(uint32_t), s))) return e;
+    if ((e = findNeighborsOnce(t, s))) return e;
     return reduceClusterStats(a, s);
 }
 #endif

@@ -2144,7 +2144,7 @@ extern "C"
             na.stats          = s->stats;
             na.powTab         = sx_ctx_powtab_internal(s->ctx, s->p.ng0);
             na.prefilter      = 1;
-            na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(2, s->last - s->first)); // the redo list
+            na.hSave          = s->mem.get<float>("ns.hsave", std::max<size_t>(2 * ((s->last - s->first) / kCluster + 2), s->last - s->first)); // the two redo lists
             na.policy         = &s->nsPolicy;
             na.clStats        = s->mem.get<uint4>("ns.clstats", (na.numGroups + kClusterWaves - 1) / kClusterWaves);
             na.work           = s->mem.get<uint32_t>("ns.work", 16);
@@ -2503,8 +2503,10 @@ extern "C"
         s->lastStats.build         = s->nsPolicy.lastBuild;
         if (s->statsHost[0] & 1u)
         {
-            fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 queue/candidate leaves, "
-                            "4 candidate space, 8 union)\n", s->statsHost[0]);
+            fprintf(stderr, "sx_sim_step: neighbor search capacity exceeded (flags 0x%x: 2 walk capacity -- 0x40 traversal "
+                            "queue, 0x20 candidate leaves, 0x10 search regions --, 4 candidate space, 8 union); cluster %d: %u "
+                            "candidate leaves, %u search regions\n",
+                    s->statsHost[0], (int)s->statsHost[14] - 1, s->statsHost[15], s->statsHost[16]);
             return SX_ERR_TRAVERSAL;
         }
         if (s->p.g != 0.0)

@@ -151,7 +151,10 @@ constexpr int kStatsWords = 28; //!< [0] error flags, [1] failures, [2] max coun
                                 //!< neighbors, [6] candidates tested, [8] union entries, [10] clusters the
                                 //!< compact build handed to the large one, [11] the compact build ran first,
                                 //!< [12] the largest cluster union (local lists), [13] clusters whose skin
-                                //!< the next step's drift would exhaust (sx_skin.hip), [14..27] spare
+                                //!< the next step's drift would exhaust (sx_skin.hip), [14] 1 + a cluster
+                                //!< over the large build's capacities, [15] its candidate leaves (capped),
+                                //!< [16] its search regions, [17] clusters the large build handed to its
+                                //!< smaller-region pass, [18..27] spare
 
 //! which search build runs: the compact one (four workgroups per CU) with a device-side fallback to the large one,
 //! or the large one directly.  Host state of one caller (context or sim), fed with the stats of each finished
@@ -231,6 +234,9 @@ struct NsArgs
     uint32_t*       redo;           // set by findNeighbors, compact build: [0] count, [1..] clusters it gave up
     const uint32_t* redoList;       // set by findNeighbors, large build: process only these clusters
     int             forceOverflow; // compact build only: report a capacity overflow for every cluster (mode 3)
+    // set by findNeighbors: a search region (group box) is coherent while the box grown by the group's largest search
+    // radius is no wider than `coherence` of its smallest h (0: 20); the last fallback takes 10 (smaller boxes)
+    float           coherence;
     // persistent-grid state (findNeighbors sets up both): 16 work counters (8 XCD ranges per launch) and the
     // per-workgroup hit-mask scratch, searchScratchBytes() bytes
     uint32_t*       work;
