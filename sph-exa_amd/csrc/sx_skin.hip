@@ -48,14 +48,17 @@ __global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* intern
                               int numNodes, const double* gc, const double* gs, const double* x, const double* y,
                               const double* z, DevBox box, double* centers, double* sizes)
 {
-    const int node = blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (node >= numNodes || childOffsets[node] != 0) return;
-    const int      leaf = internalToLeaf[node];
-    const uint32_t p0 = layout[leaf], p1 = layout[leaf + 1];
-    const double   c[3] = {gc[3 * node], gc[3 * node + 1], gc[3 * node + 2]};
+    // 16 lanes per node (a leaf holds at most the bucket size, 64 on the path; four nodes per wave)
+    constexpr int G    = 16;
+    const int     node = blockIdx.x * (blockDim.x / G) + (int)(threadIdx.x / G);
+    const int     sub  = threadIdx.x & (G - 1);
+    const bool    leafNode = node < numNodes && childOffsets[node] == 0;
+    const int      leaf = leafNode ? internalToLeaf[node] : 0;
+    const uint32_t p0 = leafNode ? layout[leaf] : 0u, p1 = leafNode ? layout[leaf + 1] : 0u;
+    const double   c[3] = {leafNode ? gc[3 * node] : 0.0, leafNode ? gc[3 * node + 1] : 0.0,
+                           leafNode ? gc[3 * node + 2] : 0.0};
     double         lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint32_t j = p0 + lane; j < p1; j += kWave)
+    for (uint32_t j = p0 + sub; j < p1; j += G)
     {
         const double q[3] = {x[j], y[j], z[j]};
         for (int d = 0; d < 3; ++d)
@@ -65,12 +68,14 @@ __global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* intern
             hi[d]          = fmax(hi[d], r);
         }
     }
-    for (int d = 0; d < 3; ++d)
-    {
-        lo[d] = -waveMax(-lo[d]);
-        hi[d] = waveMax(hi[d]);
-    }
-    if (lane == 0)
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1)
+        for (int d = 0; d < 3; ++d)
+        {
+            lo[d] = fmin(lo[d], __shfl_xor(lo[d], o, G));
+            hi[d] = fmax(hi[d], __shfl_xor(hi[d], o, G));
+        }
+    if (leafNode && sub == 0)
     {
         for (int d = 0; d < 3; ++d)
         {
@@ -581,7 +586,7 @@ hipError_t skinRefreshBoxes(const DevTree& t, const double* x, const double* y, 
 {
     if (t.numNodes <= 0) return hipSuccess;
     // leaves first (any level), then the inner nodes level by level from the deepest
-    leafBoxKernel<<<grid1(t.numNodes, 4), 256, 0, s>>>(t.childOffsets, t.internalToLeaf, t.layout, t.numNodes,
+    leafBoxKernel<<<grid1(t.numNodes, 16), 256, 0, s>>>(t.childOffsets, t.internalToLeaf, t.layout, t.numNodes,
                                                          t.centers, t.sizes, x, y, z, box, centers, sizes);
     for (int level = kMaxLevel; level >= 0; --level)
     {
