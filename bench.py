@@ -84,14 +84,19 @@ def load_pmc(key, particles, workload):
     return d
 
 
-def pmc_slot(pmc, slot):
-    """counters of one kernel-time slot, summed over the kernels it launches, per launch of the slot"""
+# kernels of a full search build: not part of a step the skin filter served (sx_skin.hpp)
+SEARCH_BUILD_KERNELS = ("findNeighborsKernel", "leafFrameKernel")
+
+
+def pmc_slot(pmc, slot, exclude=()):
+    """counters of one kernel-time slot, summed over the kernels it launches, per launch of the slot (kernels whose
+    name contains an `exclude` fragment left out)"""
     if pmc is None:
         return None
     frags = PMC_KERNELS.get(slot, ())
     tot, hit = {}, False
     for k, v in pmc.items():
-        if k == "_meta" or not any(f in k for f in frags):
+        if k == "_meta" or not any(f in k for f in frags) or any(f in k for f in exclude):
             continue
         hit = True
         calls = v.get("calls_per_step", 1.0)
@@ -105,14 +110,15 @@ def pmc_slot(pmc, slot):
 CALIB_FILE = os.path.join(ROOT, "profiles", "r3_fetch_calib.json")
 
 
-def step_traffic(pmc):
+def step_traffic(pmc, reuse_only=False):
     """HBM bytes of one whole step from the PMC summary: every kernel's (FETCH_SIZE x2 + WRITE_SIZE) x its launches
-    per step"""
+    per step.  reuse_only: the timed steps were all served by the skin filter, so the kernels the PMC run launched
+    less than once per step (its initial sync and full build) are left out"""
     if pmc is None:
         return None
     tot = 0.0
     for k, v in pmc.items():
-        if k == "_meta":
+        if k == "_meta" or (reuse_only and v.get("calls_per_step", 1.0) < 0.99):
             continue
         tot += (v.get("hbm_read_bytes_est", 0.0) + v.get("hbm_write_bytes_est", 0.0)) * v.get("calls_per_step", 1.0)
     return tot
@@ -128,7 +134,7 @@ def calibration():
     return {k: round(v["factor"], 3) for k, v in d.items() if v.get("factor")}
 
 
-def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
+def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc, exclude=()):
     """roofline entry of one kernel-time slot: HBM counter bytes / measured time vs the 8 TB/s peak, VALU issue and
     LDS conflict shares from the same counters, edge-model effective bandwidth"""
     own, edge = EDGE_MODEL.get(slot, (0, 0))
@@ -138,7 +144,7 @@ def kernel_roofline(slot, ms, n_local, ng, union_pp, pmc):
     if slot in COMPULSORY_OWN:
         r["algorithmic_bytes_per_launch"] = n_local * (COMPULSORY_OWN[slot] + 2 * ng + 4 * union_pp)
         r["algorithmic_frac"] = r["algorithmic_bytes_per_launch"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-    c = pmc_slot(pmc, slot)
+    c = pmc_slot(pmc, slot, exclude)
     if c and "hbm_read_bytes_est" in c and "hbm_write_bytes_est" in c:
         traffic = c["hbm_read_bytes_est"] + c["hbm_write_bytes_est"]
         r["traffic"] = traffic
@@ -367,7 +373,11 @@ def main():
     per_kernel = {}
     for k, ms in kern_ms.items():
         if ms > 0.01 and k in EDGE_MODEL:
-            per_kernel[k] = kernel_roofline(k, ms, n_local, ng, union_pp, pmc)
+            # every timed step served by the skin filter: the search slot's counters are the filter's alone (the
+            # PMC run's first step is a full build, whose kernels would be averaged in)
+            ex = SEARCH_BUILD_KERNELS if (k == "findNeighbors" and skin.get("builds", 1) == 0 and
+                                          skin.get("plain_steps", 1) == 0 and skin.get("reuse_steps", 0) > 0) else ()
+            per_kernel[k] = kernel_roofline(k, ms, n_local, ng, union_pp, pmc, ex)
         elif ms > 0.01 and k == "gravity":
             per_kernel[k] = gravity_roofline(ms, n_local, inter, pmc)
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["avg_launch_ms"]) if per_kernel else "momentumEnergy"
@@ -405,7 +415,8 @@ def main():
                                        "tflops", "flop_frac_impl_model", "p2p_per_target", "m2p_per_target",
                                        "valu_lane_ops_per_pair") if k in dom},
                 "per_kernel": per_kernel}
-    st_bytes = step_traffic(pmc)
+    st_bytes = step_traffic(pmc, skin.get("builds", 1) == 0 and skin.get("plain_steps", 1) == 0 and
+                            skin.get("reuse_steps", 0) > 0)
     if st_bytes:
         roofline["step_traffic"] = st_bytes
         roofline["step_hbm_gbs"] = st_bytes / (ms_step * 1e-3) / 1e9
