@@ -352,6 +352,31 @@ def main():
             for k, v in sim.skin_stats().items()}  # the timed steps'
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
+    # skin lists: a timed window of filter-served steps does not contain the full build that comes every max_reuse
+    # steps at the latest; one more step after the timed region, forced to be a build, gives its cost and the
+    # amortized step (the same decision on every rank: nothing differs between ranks here)
+    build_ms = None
+    if skin.get("reuse_steps", 0) > 0 and skin.get("builds", 1) == 0:
+        sim.rebuild_lists()
+        ctx.sync()
+        barrier()
+        tb = time.perf_counter()
+        sim.step()
+        ctx.sync()
+        barrier()
+        build_ms = (time.perf_counter() - tb) * 1e3
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([build_ms], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            build_ms = float(t.item())
+        R = max(1, int(args.skin_reuse))
+        skin["build_step_ms"] = build_ms
+        skin["amortized_ms_per_step"] = (ms_step * (R - 1) + build_ms) / R
+        skin["amortized_value"] = n_total / (skin["amortized_ms_per_step"] * 1e-3)
+        skin["amortized_note"] = (f"one full sync + build every {R} steps at the latest (max_reuse), the other steps "
+                                  "filter-served like the timed ones")
     inter = None
     if args.init == "evrard":  # self-gravity on (g = 1); the same decision on every rank: the extra step is collective
         # the interaction counts (BhStats) of one more step after the timed region: counting is a separate, slower
