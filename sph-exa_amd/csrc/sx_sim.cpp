@@ -1644,6 +1644,11 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     const uint32_t n1 = hl[0], nd = hl[1];
     uint32_t       n2 = nd;
     NsArgs         x  = na; // the exact search, for clusters whose h iteration outgrows even a fresh skin
+    // subset searches of a reuse step run the large build directly: on the refreshed (overlapping) boxes many of the
+    // few clusters overflow the compact one, whose launch then only adds a tail (Noh -n 300: 20.4 -> 20.1 ms/step)
+    NsPolicy large;
+    large.mode = 1;
+    if (reuse) b.policy = x.policy = &large;
     if ((n1 || nd) && reuse)
     {
         // particles have left the cells of the last full sync's tree: the walk takes boxes of the current positions
