@@ -484,7 +484,7 @@ def main():
                       else {}),
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)",
                    "neighbor_skin": {"initial_factor": args.skin, "max_reuse": args.skin_reuse,
-                                     "note": "one rank without gravity: steps between full builds filter the last "
+                                     "note": "one rank: steps between full builds filter the last "
                                              "build's lists within 2h(1+s) (sx_skin.hpp); same neighbor sets, nc, h",
                                      **skin}},
         "roofline": roofline,

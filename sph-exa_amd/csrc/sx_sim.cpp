@@ -1503,10 +1503,11 @@ void maxAccSq(sx_sim* s, hipStream_t st)
                                                                           &s->sc->maxAccSqBits);
 }
 
-//! skin lists serve this sim: one rank, no self-gravity (its tree is rebuilt every step), not ve-bdt, cluster lists
+//! skin lists serve this sim: one rank, not ve-bdt, cluster lists.  With self-gravity a reuse step traverses the last
+//! sync's tree, its multipoles formed from the current positions and its MAC geometry refreshed (cells + particles)
 bool skinUsable(const sx_sim* s)
 {
-    return s->skin.factor > 0.0f && !(s->comm && s->comm->size() > 1) && s->p.g == 0.0 && s->p.propagator != 2 &&
+    return s->skin.factor > 0.0f && !(s->comm && s->comm->size() > 1) && s->p.propagator != 2 &&
            NbLists::localPossible(s->p.ngmax);
 }
 
@@ -2431,6 +2432,16 @@ extern "C"
             ga.layout         = s->tree.layout;
             ga.geoCenters     = s->tree.centers;
             ga.geoSizes       = s->tree.sizes;
+            if (reuse)
+            {
+                // no sync this step: particles may have left their cells; the MAC takes boxes that hold both
+                double* gc3 = s->work.get<double>("grav.geoC", 3 * (size_t)s->tree.numNodes);
+                double* gs3 = s->work.get<double>("grav.geoS", 3 * (size_t)s->tree.numNodes);
+                if (!gc3 || !gs3) return SX_ERR_NOMEM;
+                SIM_HIP(skinRefreshBoxes(s->tree, s->x, s->y, s->z, s->dbox, gc3, gs3, st, true));
+                ga.geoCenters = gc3;
+                ga.geoSizes   = gs3;
+            }
             ga.leafToNode     = s->work.get<int32_t>("grav.leafToNode", (size_t)s->tree.numLeaves);
             ga.x = s->x, ga.y = s->y, ga.z = s->z, ga.m = s->m, ga.h = s->h;
             ga.centers4   = s->work.get<double>("grav.centers", 4 * (size_t)s->tree.numNodes);

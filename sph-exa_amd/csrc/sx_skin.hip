@@ -46,7 +46,7 @@ __device__ __forceinline__ float norm3up(float x, float y, float z)
 //! leaf boxes from their particles (relative to the geometric center, minimum image), one wave per leaf node
 __global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* internalToLeaf, const uint32_t* layout,
                               int numNodes, const double* gc, const double* gs, const double* x, const double* y,
-                              const double* z, DevBox box, double* centers, double* sizes)
+                              const double* z, DevBox box, double* centers, double* sizes, int withCells)
 {
     // 16 lanes per node (a leaf holds at most the bucket size, 64 on the path; four nodes per wave)
     constexpr int G    = 16;
@@ -79,6 +79,11 @@ __global__ void leafBoxKernel(const int32_t* childOffsets, const int32_t* intern
     {
         for (int d = 0; d < 3; ++d)
         {
+            if (withCells) // the box of the particles and the leaf's cell together
+            {
+                lo[d] = fmin(lo[d], -gs[3 * node + d]);
+                hi[d] = fmax(hi[d], gs[3 * node + d]);
+            }
             // an empty leaf keeps its cell (it contributes no candidates either way)
             const bool   empty = p1 <= p0;
             const double m     = empty ? 0.0 : 0.5 * (lo[d] + hi[d]);
@@ -582,12 +587,13 @@ hipError_t skinFilter(const SkinArgs& a, uint32_t numClusters, hipStream_t s)
 }
 
 hipError_t skinRefreshBoxes(const DevTree& t, const double* x, const double* y, const double* z, const DevBox& box,
-                            double* centers, double* sizes, hipStream_t s)
+                            double* centers, double* sizes, hipStream_t s, bool withCells)
 {
     if (t.numNodes <= 0) return hipSuccess;
     // leaves first (any level), then the inner nodes level by level from the deepest
     leafBoxKernel<<<grid1(t.numNodes, 16), 256, 0, s>>>(t.childOffsets, t.internalToLeaf, t.layout, t.numNodes,
-                                                         t.centers, t.sizes, x, y, z, box, centers, sizes);
+                                                          t.centers, t.sizes, x, y, z, box, centers, sizes,
+                                                          withCells ? 1 : 0);
     for (int level = kMaxLevel; level >= 0; --level)
     {
         const int b = t.levelRangeHost[level], e = t.levelRangeHost[level + 1];

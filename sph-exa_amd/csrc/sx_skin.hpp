@@ -89,9 +89,10 @@ struct SkinArgs
 
 hipError_t skinFilter(const SkinArgs& a, uint32_t numClusters, hipStream_t s);
 //! node boxes (center, half size) of the tree refreshed from the current positions: leaf boxes bound their particles,
-//! inner boxes their children (for a build between full syncs, when particles have left their cells)
+//! inner boxes their children (for a build between full syncs, when particles have left their cells); withCells:
+//! every box also contains the node's cell (the gravity MAC's geometry between syncs: never smaller than the cell's)
 hipError_t skinRefreshBoxes(const DevTree& t, const double* x, const double* y, const double* z, const DevBox& box,
-                            double* centers, double* sizes, hipStream_t s);
+                            double* centers, double* sizes, hipStream_t s, bool withCells = false);
 //! acc[c] = +inf for the listed clusters (their lists came from the exact search: the next step rebuilds their skin)
 hipError_t skinMarkStale(const uint32_t* list, uint32_t numClusters, float* acc, hipStream_t s);
 //! per-cluster statistics -> stats (the search's reduction)
