@@ -23,6 +23,7 @@ SOURCES = {
     "sx_gravity": ("csrc/sx_gravity.hip", ["-ffp-contract=off", "-fno-slp-vectorize"]),
     "sx_tree": ("csrc/sx_tree.hip", ["-ffp-contract=off"]),
     "sx_timestep": ("csrc/sx_timestep.hip", ["-ffp-contract=off"]),
+    "sx_skin": ("csrc/sx_skin.hip", ["-ffp-contract=off"]),
 }
 KEYS = {"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch", "Occupancy [waves/SIMD]": "occ",
         "SGPRs Spill": "sspill", "VGPRs Spill": "vspill", "LDS Size [bytes/block]": "lds"}
