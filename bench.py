@@ -198,6 +198,9 @@ def parse():
     ap.add_argument("--bucket", type=int, default=64)
     ap.add_argument("--exact", action="store_true", help="use the no-FMA (bit-reproducible) kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-build-step", action="store_true",
+                    help="skip the forced skin build step after the timed window (profiling runs: the PMC summary "
+                         "normalises its counters by steps + warmup)")
     ap.add_argument("--backend", default="rccl", help="rccl (one GPU per rank) or host (staged, tests)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--cpu-side", type=int, default=200, help="Sedov lattice side of the CPU baseline sample")
@@ -356,7 +359,7 @@ def main():
     # steps at the latest; one more step after the timed region, forced to be a build, gives its cost and the
     # amortized step (the same decision on every rank: nothing differs between ranks here)
     build_ms = None
-    if skin.get("reuse_steps", 0) > 0 and skin.get("builds", 1) == 0:
+    if skin.get("reuse_steps", 0) > 0 and skin.get("builds", 1) == 0 and not args.no_build_step:
         sim.rebuild_lists()
         ctx.sync()
         barrier()

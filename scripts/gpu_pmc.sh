@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${TAG:-x}
 mkdir -p $OUT
-ARGS=${ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-build-step}
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" "SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"; do
   i=$((i+1))

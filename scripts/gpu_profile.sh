@@ -11,9 +11,9 @@ KEY=${KEY:?KEY=<init>_n<side>}
 A=${ARGS:-}
 mkdir -p gpurun_out
 echo "== kernel stats $KEY"; date
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$KEY -o run -- python bench.py $A --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$KEY.log 2>&1 || { tail -5 gpurun_out/prof_$KEY.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$KEY -o run -- python bench.py $A --steps 3 --warmup 1 --no-cpu-baseline --no-build-step > gpurun_out/prof_$KEY.log 2>&1 || { tail -5 gpurun_out/prof_$KEY.log; exit 1; }
 if [ "${PMC:-1}" = "1" ]; then
-  TAG=$KEY ARGS="$A --steps 2 --warmup 1 --no-cpu-baseline" bash scripts/gpu_pmc.sh || exit 1
+  TAG=$KEY ARGS="$A --steps 2 --warmup 1 --no-cpu-baseline --no-build-step" bash scripts/gpu_pmc.sh || exit 1
   mkdir -p profiles && cp gpurun_out/pmc_$KEY/summary.json profiles/pmc_$KEY.json
 fi
 echo "== bench $KEY"; date
