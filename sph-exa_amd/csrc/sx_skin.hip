@@ -36,6 +36,12 @@ constexpr int kB       = kCluster;
 
 __device__ __forceinline__ int cellIndex(double v, const SkinGrid& g, int d) { return gridCell(v, g, d); }
 
+//! v if k, else +0 (an AND of the bits: no select the compiler could turn into a branch)
+__device__ __forceinline__ float keepOrZero(float v, bool k)
+{
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & (0u - (uint32_t)k));
+}
+
 //! |(x, y, z)| of float differences, rounded upwards (an upper bound of the exact length of the exact differences:
 //! each float difference is within 2^-24 relative, the sum of squares and the root within a few ulp more)
 __device__ __forceinline__ float norm3up(float x, float y, float z)
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     // LDS: 39.9 KB, four workgroups per CU
     __shared__ float4   s_rec[kSkinCap]; // U_s positions relative to the cluster origin, |p|^2; then the exact-union
                                          // ranks (u16) of the U_s entries, once pass A is done with the positions
-    __shared__ uint8_t  s_hit[kSkinCap]; // U_s entry hit by some target (exact union)
+    __shared__ uint8_t  s_hit[kSkinCap + 4]; // U_s entry hit by some target (exact union); [kSkinCap]: spare
     __shared__ uint16_t s_bm[kWalkBlocks][kB]; // pass A's stored hits per walk block and lane (bit e: entry e)
     uint16_t* const     s_rank = reinterpret_cast<uint16_t*>(s_rec);
     __shared__ float    s_red[kClusterWaves];
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         {
             const double o[3] = {ox, oy, oz};
             int          k0[3], nk[3];
-            long long    total = 1;
+            uint32_t     total = 1; // at most grid.n^3 (each nk within [1, grid.n]): 32-bit division below
             for (int d = 0; d < 3; ++d)
             {
                 k0[d]  = cellIndex(o[d] + lo[d] - (double)rmax, a.grid, d);
@@ -238,14 +244,15 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
                 total *= nk[d];
             }
             // a region of many cells (a wave spanning an SFC seam across the box) scans them all: rare
-            for (long long q = lane; q < total; q += kWave)
+            for (uint32_t q = lane; q < total; q += kWave)
             {
-                int       k[3];
-                long long r = q;
+                int      k[3];
+                uint32_t r = q;
                 for (int d = 0; d < 3; ++d)
                 {
-                    k[d] = k0[d] + (int)(r % nk[d]);
-                    r /= nk[d];
+                    const uint32_t rq = r / (uint32_t)nk[d];
+                    k[d]              = k0[d] + (int)(r - rq * (uint32_t)nk[d]);
+                    r                 = rq;
                     if (a.grid.pbc[d]) k[d] = wrapCell(k[d], a.grid.n);
                 }
                 const size_t nc   = (size_t)a.grid.n * a.grid.n * a.grid.n;
@@ -336,10 +343,12 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     bool            active    = valid;
     unsigned        count     = 0, stored = 0;
     //! one pass over this lane's skin list in blocks of kWalkPF words (16 entries): begin(b) starts block b,
-    //! test(p, e) decides entry e of the block (U_s position p), onHit(p, e) takes the accepted ones in list order,
-    //! end(b) closes the block.  List words are loaded a block ahead, every load unconditional (clamped to the lane's
-    //! last word, word 0 for an empty list): a load under a condition is waited for at the branch merge
-    auto walk = [&](auto&& begin, auto&& test, auto&& onHit, auto&& end) {
+    //! visit(p, e, inr) takes entry e of the block (U_s position p; inr: the entry is in the list, else p is a valid
+    //! position of no meaning), end(b) closes the block.  Every entry of a block is visited without a branch (a wave's
+    //! lanes take the hit and the miss paths of one entry together anyway; the branches only cost exec-mask traffic).
+    //! List words are loaded a block ahead, every load unconditional (clamped to the lane's last word, word 0 for an
+    //! empty list): a load under a condition is waited for at the branch merge
+    auto walk = [&](auto&& begin, auto&& visit, auto&& end) {
         if (!valid) return;
         const uint32_t nw   = (scount + 1) >> 1;
         const uint32_t last = nw ? nw - 1 : 0u;
@@ -361,17 +370,11 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
 #pragma unroll
             for (int u = 0; u < PF; ++u)
             {
+                // words past the list repeat its last word (valid positions); the upper half past an odd count is
+                // clamped into the staged range
                 const uint32_t w = w0 + u;
-                if (w < nw)
-                {
-                    const uint32_t p0 = cw[u] & 0xffffu;
-                    if (test(p0, 2 * u)) onHit(p0, 2 * u);
-                    if (2 * w + 1 < scount)
-                    {
-                        const uint32_t p1 = cw[u] >> 16;
-                        if (test(p1, 2 * u + 1)) onHit(p1, 2 * u + 1);
-                    }
-                }
+                visit(cw[u] & 0xffffu, 2 * u, 2 * w < scount);
+                visit(min(cw[u] >> 16, (uint32_t)kSkinCap - 1u), 2 * u + 1, 2 * w + 1 < scount);
             }
             end(b);
         }
@@ -379,16 +382,16 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     float          r2f = 0, tol = 0;
     double         radSq = 0;
     bool           safe = true, usePbc = false;
-    float          lastR2 = 0, lastM = 0; // r^2 and m_j of the entry test() accepted last (the fused XMass)
     //! t = |p - r|^2 - 4h^2 in float (p, r relative to the cluster origin), with the reference's double criterion
-    //! where |t| may be rounding (the bound of sx_neighbors.hip's |p|^2 + |r|^2 - 2p.r form, which covers this one)
-    auto test = [&](uint32_t p, int) -> bool {
-        const float4 q  = s_rec[p];
-        const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
-        float        r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-        const float  t  = r2 - r2f;
-        bool         hit = t < 0.0f;
-        if (!safe || fabsf(t) <= tol)
+    //! where |t| may be rounding (the bound of sx_neighbors.hip's |p|^2 + |r|^2 - 2p.r form, which covers this one);
+    //! r2 becomes the pair's r^2 (the fused XMass)
+    auto test = [&](uint32_t p, float4 q, bool inr, float& r2) -> bool {
+        const float dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+        r2             = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+        const float t  = r2 - r2f;
+        bool        hit = t < 0.0f;
+        // bitwise, not short-circuit: one branch per entry, around the (rare) double criterion
+        if (inr & ((!safe) | (fabsf(t) <= tol)))
         {
             const uint32_t j  = un[p];
             double         ex = a.x[j] - xi, ey = a.y[j] - yi, ez = a.z[j] - zi;
@@ -402,8 +405,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
             hit             = d2 < radSq;
             r2              = (float)d2;
         }
-        lastR2 = r2, lastM = q.w;
-        return hit; // j != i: the build's skin list never holds the target itself
+        return inr & hit; // j != i: the build's skin list never holds the target itself
     };
     const float mi   = a.m[iS];
     float       rho0 = mi, hInv2 = 0; // fused XMass (xmassJLoop, hydro_ve/xmass_kern.hpp:50-79) of the final pass
@@ -437,16 +439,18 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         // vmcnt counts stores too, in order, so a store between the prefetch and its use would be waited for as well
         unsigned cnt = 0, st = 0;
         uint32_t bits = 0;
-        walk([&](uint32_t) { bits = 0; }, test,
-             [&](uint32_t p, int e) {
-                 if (cnt < a.ngmax)
-                 {
-                     s_hit[p] = 1;
-                     bits |= 1u << e;
-                     ++st;
-                     if (a.xmOut) rho0 += kernelWt(lastR2 * hInv2) * lastM;
-                 }
-                 ++cnt;
+        walk([&](uint32_t) { bits = 0; },
+             [&](uint32_t p, int e, bool inr) {
+                 const float4 q = s_rec[p];
+                 float        r2;
+                 const bool   hit  = test(p, q, inr, r2);
+                 const bool   keep = hit & (cnt < a.ngmax); // the first ngmax hits in list order
+                 // no branch: a miss marks the spare byte; rho0 + (+0) == rho0
+                 s_hit[keep ? p : (uint32_t)kSkinCap] = 1;
+                 bits |= (uint32_t)keep << e;
+                 st += (uint32_t)keep;
+                 cnt += (uint32_t)hit;
+                 if (a.xmOut) rho0 += keepOrZero(kernelWt(r2 * hInv2) * q.w, keep);
              },
              [&](uint32_t b) { s_bm[b][threadIdx.x] = (uint16_t)bits; });
         count  = cnt;
@@ -521,12 +525,14 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     {
         unsigned st = 0;
         uint32_t pend = 0, bits = 0;
-        walk([&](uint32_t b) { bits = s_bm[b][threadIdx.x]; }, [&](uint32_t, int e) { return ((bits >> e) & 1u) != 0; },
-             [&](uint32_t p, int) {
-                 const uint32_t r = s_rank[p];
-                 if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend | (r << 16);
-                 else pend = r;
-                 ++st;
+        walk([&](uint32_t b) { bits = s_bm[b][threadIdx.x]; },
+             [&](uint32_t p, int e, bool) {
+                 const bool     keep = ((bits >> e) & 1u) != 0;
+                 const uint32_t r    = s_rank[p];
+                 const bool     odd  = (st & 1u) != 0;
+                 if (keep && odd) ll[(size_t)(st >> 1) * kWave] = pend | (r << 16);
+                 pend = (keep && !odd) ? r : pend;
+                 st += keep ? 1u : 0u;
              },
              [](uint32_t) {});
         if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend;
