@@ -336,9 +336,29 @@ int sx_gravity_upsweep(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, flo
  *  of 16, vector MAC, quadrupole M2P, P2P softened by h_i + h_j): adds G * acc to f->ax, ay, az and returns the
  *  potential energy 0.5 sum G m phi in *egrav.  With explicit groups (g->groupStart, e.g. the active rungs of
  *  ve-bdt, MultipoleHolder::traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285) only the targets of those groups are
- *  traversed (the others keep their acceleration) and egrav sums over them.  Open boxes only (no Ewald replicas). */
+ *  traversed (the others keep their acceleration) and egrav sums over them.  Open boxes only: the replica shells of a
+ *  periodic walk (traversal.cuh:485-513) are not provided (SX_ERR_ARG). */
 int sx_gravity_traverse(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
                         const double* centers, const float* multipoles, float G, double* egrav);
+
+/*! ryoanji::EwaldSettings (nbody/ewald.h:15-22); the reference's defaults: 1, 2.6, 2.8, 2.0, 3e-3 */
+typedef struct
+{
+    int    numReplicaShells; /* image shells the tree walk covered (their -erf correction) */
+    double lCut;             /* real-space cutoff (box lengths) */
+    double hCut;             /* k-space cutoff, ceil(hCut) <= 3 */
+    double alphaScale;       /* Ewald splitting alpha = alphaScale / L */
+    double smallRScaleFactor;
+} sx_ewald_settings;
+
+/*! Ewald correction of periodic self-gravity (computeGravityEwaldGpu, ryoanji/interface/ewald.cu:60-95, i.e.
+ *  computeGravityEwald, nbody/ewald.hpp:380-413) for the targets of g: the root's expansion (centers[0..2],
+ *  multipoles[0..7], device arrays of sx_gravity_upsweep) summed over the images in real space and in k space; adds
+ *  G * correction to f->ax, ay, az and 0.5 G sum m phi to *egrav.  SX_ERR_ARG unless the box is cubic and
+ *  ceil(hCut) <= 3.  Only targets of g (explicit groups: their targets) are corrected.  The correction completes a
+ *  walk over numReplicaShells image shells, which sx_gravity_traverse does not provide: the caller supplies them. */
+int sx_gravity_ewald(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_box* box, const double* centers,
+                     const float* multipoles, float G, const sx_ewald_settings* settings, double* egrav);
 
 /* ---- multi-GPU transport (replaces the reference's MPI calls, see sph-exa_amd/csrc/sx_comm.hpp) ---------- */
 typedef struct sx_comm sx_comm;
@@ -402,7 +422,8 @@ int sx_domain_halo_layout(const uint64_t* recvCounts, int nranks, int rank, uint
 
 /* ---- device-resident simulation: one HydroVeProp step per call ----------------------------------------- */
 typedef struct sx_sim sx_sim;
-/*! Sedov lattice (sedov_init.hpp:48-130) of side^3 particles; with nranks > 1 only this rank's SFC share. */
+/*! a simulation of up to capacity particles in box.  SX_ERR_ARG for self-gravity (p->g != 0) in a periodic box: the
+ *  replica shells it needs are not provided (sx_gravity_traverse). */
 int    sx_sim_create(sx_sim** sim, sx_ctx* ctx, size_t capacity, const sx_params* p, const sx_box* box,
                      uint32_t bucketSize);
 void   sx_sim_destroy(sx_sim* sim);

@@ -1144,8 +1144,10 @@ extern "C"
     {
         if (!g || !f || !tree || !box || !centers || !multipoles || g->lastBody > f->n)
             return fail(c, SX_ERR_ARG, "sx_gravity_traverse: bad arguments");
+        // a periodic box needs the replica shells of the walk (traversal.cuh:485-513, numReplicaShells >= 1: the
+        // Ewald correction's -erf term of the central image is accurate only next to them), not provided here
         if (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)
-            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic gravity (Ewald replicas) is not provided");
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic gravity (replica shells) is not provided");
         // explicit groups (mHolder_.traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285): only their targets
         sx_groups tmp;
         if (int rc = resolveView(c, g, tmp, f->n, false)) return rc;
@@ -1172,6 +1174,46 @@ extern "C"
         SX_HIP(c, hipStreamSynchronize(c->stream));
         if (eb) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in Barnes-Hut");
         if (egrav) *egrav = eh;
+        return SX_OK;
+    }
+
+    int sx_gravity_ewald(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_box* box, const double* centers,
+                         const float* multipoles, float G, const sx_ewald_settings* st, double* egrav)
+    {
+        if (!g || !f || !box || !centers || !multipoles || !st || g->lastBody > f->n)
+            return fail(c, SX_ERR_ARG, "sx_gravity_ewald: bad arguments");
+        const double lx = box->lim[1] - box->lim[0], ly = box->lim[3] - box->lim[2], lz = box->lim[5] - box->lim[4];
+        if (std::min(lx, std::min(ly, lz)) != std::max(lx, std::max(ly, lz)))
+            return fail(c, SX_ERR_ARG, "Ewald gravity requires cubic bounding boxes");
+        sx_groups tmp;
+        if (int rc = resolveView(c, g, tmp, f->n, false)) return rc;
+        // the root's expansion, as the reference reads it (gravity_wrapper.hpp:149-152: two D2H copies)
+        double center4[4];
+        float  Mroot[8];
+        SX_HIP(c, hipMemcpyAsync(center4, centers, sizeof(center4), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipMemcpyAsync(Mroot, multipoles, sizeof(Mroot), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        EwaldArgs a{};
+        std::vector<double> hs;
+        if (ewaldInit(a.p, hs, center4, Mroot, lx, st->numReplicaShells, st->lCut, st->hCut, st->alphaScale,
+                      st->smallRScaleFactor))
+            return fail(c, SX_ERR_ARG, "sx_gravity_ewald: ceil(hCut) > 3");
+        if (a.p.numEwaldShells == 0) return SX_OK;
+        double* hd = c->arena.get<double>("ewald.hsum", std::max<size_t>(hs.size(), 5));
+        double* us = c->arena.get<double>("ewald.usum", 1);
+        if (!hd || !us) return fail(c, SX_ERR_NOMEM, "sx_gravity_ewald: out of memory");
+        if (!hs.empty())
+            SX_HIP(c, hipMemcpyAsync(hd, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        SX_HIP(c, hipMemsetAsync(us, 0, sizeof(double), c->stream));
+        a.first = g->firstBody, a.last = g->lastBody;
+        a.x = f->x, a.y = f->y, a.z = f->z, a.m = f->m;
+        a.ax = f->ax, a.ay = f->ay, a.az = f->az;
+        a.G = G, a.active = c->viewActive, a.hsum = hd, a.usum = us;
+        SX_HIP(c, ewaldCorrection(a, c->stream));
+        double u = 0;
+        SX_HIP(c, hipMemcpyAsync(&u, us, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        SX_HIP(c, hipStreamSynchronize(c->stream));
+        if (egrav) *egrav += 0.5 * G * u;
         return SX_OK;
     }
 } // extern "C"

@@ -3,6 +3,8 @@
  */
 #pragma once
 
+#include <vector>
+
 #include "sx_device.hpp"
 
 namespace sx
@@ -67,5 +69,34 @@ hipError_t farUpsweep(const GravArgs& a, const GCell* cells, const uint32_t* far
 hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipStream_t s);
 //! adds G * (M2P + P2P) to ax, ay, az of [first, last) and 0.5 sum G m phi to *egrav
 hipError_t gravityTraverse(const GravArgs& a, hipStream_t s);
+
+//! Ewald parameters of one evaluation (ryoanji EwaldParameters<double, float>, nbody/ewald.hpp:58-91): the root's
+//! expansion center and quadrupole (Cqi order), the shells, and computeEwaldRealSpace's constants
+struct EwaldParams
+{
+    double cx, cy, cz;
+    float  M[8];
+    int    numReplicaShells, numEwaldShells, numH;
+    double L, lCut2, alpha, alpha2, k1, ka, smallR2;
+};
+
+struct EwaldArgs
+{
+    uint32_t       first, last; // targets
+    const double * x, *y, *z;
+    const float*   m;
+    float *        ax, *ay, *az; // G * correction is added
+    float          G;
+    const uint8_t* active; // nullable: only targets with active[i] != 0
+    const double*  hsum;   // numH x {hr_scaled x, y, z, hfac_cos, hfac_sin} (device)
+    double*        usum;   // device accumulator of sum m phi (atomic)
+    EwaldParams    p;
+};
+
+//! ewaldInitParameters (ewald.hpp:149-214) on the host: p and the k-space table (numH x 5); -1 if ceil(hCut) > 3
+int ewaldInit(EwaldParams& p, std::vector<double>& hsum, const double center[3], const float Mroot[8], double L,
+              int numReplicaShells, double lCut, double hCut, double alphaScale, double smallR);
+//! computeEwaldRealSpace + computeEwaldKSpace per target (ewald.hpp:380-413): a += G (real + k), *usum += sum m phi
+hipError_t ewaldCorrection(const EwaldArgs& a, hipStream_t s);
 
 } // namespace sx

@@ -1764,6 +1764,8 @@ extern "C"
                       uint32_t bucketSize)
     {
         if (p->propagator < 0 || p->propagator > 2) return SX_ERR_ARG;
+        // self-gravity in a periodic box needs the walk's replica shells (sx_gravity_traverse): refused, not run open
+        if (p->g != 0.0 && (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)) return SX_ERR_ARG;
         auto* s   = new sx_sim;
         s->ctx    = ctx;
         s->p      = *p;

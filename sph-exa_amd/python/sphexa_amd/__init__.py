@@ -55,6 +55,15 @@ class SxTree(C.Structure):
                 ("sizes", _P), ("searchExtFactor", C.c_float)]
 
 
+class SxEwaldSettings(C.Structure):
+    """sx_ewald_settings (ryoanji::EwaldSettings, nbody/ewald.h:15-22); the reference's defaults"""
+    _fields_ = [("numReplicaShells", C.c_int), ("lCut", C.c_double), ("hCut", C.c_double), ("alphaScale", C.c_double),
+                ("smallRScaleFactor", C.c_double)]
+
+    def __init__(self, numReplicaShells=1, lCut=2.6, hCut=2.8, alphaScale=2.0, smallRScaleFactor=3.0e-3):
+        super().__init__(numReplicaShells, lCut, hCut, alphaScale, smallRScaleFactor)
+
+
 class SxGroups(C.Structure):
     _fields_ = [("firstBody", C.c_uint32), ("lastBody", C.c_uint32), ("numGroups", C.c_uint32),
                 ("groupStart", _P), ("groupEnd", _P)]
@@ -215,6 +224,8 @@ def lib():
         "sx_gravity_upsweep": (C.c_int, [vp, C.POINTER(SxFields), C.POINTER(SxTree), C.c_float, vp, vp]),
         "sx_gravity_traverse": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxTree),
                                           C.POINTER(SxBox), vp, vp, C.c_float, C.POINTER(C.c_double)]),
+        "sx_gravity_ewald": (C.c_int, [vp, C.POINTER(SxGroups), C.POINTER(SxFields), C.POINTER(SxBox), vp, vp,
+                                       C.c_float, C.POINTER(SxEwaldSettings), C.POINTER(C.c_double)]),
         "sx_domain_halo_layout": (C.c_int, [vp, C.c_int, C.c_int, C.c_uint64, vp, vp]),
     }
     for name, (res, args) in sig.items():
