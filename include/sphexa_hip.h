@@ -336,10 +336,18 @@ int sx_gravity_upsweep(sx_ctx* ctx, const sx_fields* f, const sx_tree* tree, flo
  *  of 16, vector MAC, quadrupole M2P, P2P softened by h_i + h_j): adds G * acc to f->ax, ay, az and returns the
  *  potential energy 0.5 sum G m phi in *egrav.  With explicit groups (g->groupStart, e.g. the active rungs of
  *  ve-bdt, MultipoleHolder::traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285) only the targets of those groups are
- *  traversed (the others keep their acceleration) and egrav sums over them.  Open boxes only: the replica shells of a
- *  periodic walk (traversal.cuh:485-513) are not provided (SX_ERR_ARG). */
+ *  traversed (the others keep their acceleration) and egrav sums over them.  Open boxes (a periodic box:
+ *  sx_gravity_traverse_pbc). */
 int sx_gravity_traverse(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
                         const double* centers, const float* multipoles, float G, double* egrav);
+/*! the walk over the periodic images (MultipoleHolder::compute(..., numShells, box, ...), gravity_wrapper.hpp:139-141;
+ *  traversal_cpu.hpp:200-216 / traversal.cuh:485-513): as sx_gravity_traverse, the targets shifted by every
+ *  (ix Lx, iy Ly, iz Lz), |ix|, |iy|, |iz| <= numShells (0..4); numShells 0 = the box alone.  Periodic self-gravity
+ *  is this walk with numShells = EwaldSettings::numReplicaShells followed by sx_gravity_ewald.  No interaction
+ *  counting on this path. */
+int sx_gravity_traverse_pbc(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_tree* tree,
+                            const sx_box* box, const double* centers, const float* multipoles, float G, int numShells,
+                            double* egrav);
 
 /*! ryoanji::EwaldSettings (nbody/ewald.h:15-22); the reference's defaults: 1, 2.6, 2.8, 2.0, 3e-3 */
 typedef struct
@@ -356,7 +364,7 @@ typedef struct
  *  multipoles[0..7], device arrays of sx_gravity_upsweep) summed over the images in real space and in k space; adds
  *  G * correction to f->ax, ay, az and 0.5 G sum m phi to *egrav.  SX_ERR_ARG unless the box is cubic and
  *  ceil(hCut) <= 3.  Only targets of g (explicit groups: their targets) are corrected.  The correction completes a
- *  walk over numReplicaShells image shells, which sx_gravity_traverse does not provide: the caller supplies them. */
+ *  walk over numReplicaShells image shells (sx_gravity_traverse_pbc). */
 int sx_gravity_ewald(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const sx_box* box, const double* centers,
                      const float* multipoles, float G, const sx_ewald_settings* settings, double* egrav);
 
@@ -422,8 +430,9 @@ int sx_domain_halo_layout(const uint64_t* recvCounts, int nranks, int rank, uint
 
 /* ---- device-resident simulation: one HydroVeProp step per call ----------------------------------------- */
 typedef struct sx_sim sx_sim;
-/*! a simulation of up to capacity particles in box.  SX_ERR_ARG for self-gravity (p->g != 0) in a periodic box: the
- *  replica shells it needs are not provided (sx_gravity_traverse). */
+/*! a simulation of up to capacity particles in box.  Self-gravity (p->g != 0) in a periodic box: the walk over one
+ *  image shell + the Ewald correction with the reference's EwaldSettings defaults (gravity_wrapper.hpp:135-157), one
+ *  rank, VE or std propagator (SX_ERR_ARG for ve-bdt; several ranks: at sx_sim_set_comm). */
 int    sx_sim_create(sx_sim** sim, sx_ctx* ctx, size_t capacity, const sx_params* p, const sx_box* box,
                      uint32_t bucketSize);
 void   sx_sim_destroy(sx_sim* sim);

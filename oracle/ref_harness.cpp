@@ -500,10 +500,13 @@ extern "C"
         sph::updateTempHost(first, last, d);
     }
 
+    //! periodic images of the walk (computeGravity's numShells, traversal_cpu.hpp:180); ref_set_gravity_shells
+    static int g_numShells = 0;
+
     /*! @brief self-gravity with the reference's own functions on the tree of the key-sorted state (single rank):
      *  expansion centers as FocusedOctree::updateCenters + setMacRadius(1/theta) (octree_focus_mpi.hpp:325-459),
      *  ryoanji::computeLeafMultipoles + upsweepMultipoles (global_multipole.hpp:44-71 without the MPI exchanges),
-     *  ryoanji::computeGravity (traversal_cpu.hpp:166-230, numShells 0).  cap < 0: return the node count. */
+     *  ryoanji::computeGravity (traversal_cpu.hpp:166-230, numShells: g_numShells).  cap < 0: return the node count. */
     static double gravityOnTree(ox_state* s, const ox_params* p, const cstone::Box<double>& box, TreeArrays& t,
                                 unsigned first, unsigned last, double* centersOut, float* multipolesOut, int cap)
     {
@@ -531,11 +534,13 @@ extern "C"
         double egrav = 0;
         ryoanji::computeGravity(t.childOffsets.data(), t.internalToLeaf.data(), centers.data(), mp.data(),
                                 t.layout.data(), l0, l1, s->x, s->y, s->z, s->h, s->m, box, float(p->g),
-                                (double*)nullptr, s->ax, s->ay, s->az, &egrav, 0);
+                                (double*)nullptr, s->ax, s->ay, s->az, &egrav, g_numShells);
         if (centersOut && cap >= nTot) std::memcpy(centersOut, centers.data(), sizeof(double) * 4 * nTot);
         if (multipolesOut && cap >= nTot) std::memcpy(multipolesOut, mp.data(), sizeof(float) * 8 * nTot);
         return egrav;
     }
+
+    void ref_set_gravity_shells(int numShells) { g_numShells = numShells; }
 
     double ref_gravity(ox_state* s, const ox_params* p, const ox_box* b, unsigned bucket, unsigned first,
                        unsigned last, double* centersOut, float* multipolesOut, int cap)

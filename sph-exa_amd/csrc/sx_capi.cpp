@@ -1139,19 +1139,17 @@ extern "C"
         return SX_OK;
     }
 
-    int sx_gravity_traverse(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
-                            const double* centers, const float* multipoles, float G, double* egrav)
+    static int gravityTraverseShells(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_tree* tree,
+                                     const sx_box* box, const double* centers, const float* multipoles, float G,
+                                     int numShells, double* egrav)
     {
-        if (!g || !f || !tree || !box || !centers || !multipoles || g->lastBody > f->n)
-            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: bad arguments");
-        // a periodic box needs the replica shells of the walk (traversal.cuh:485-513, numReplicaShells >= 1: the
-        // Ewald correction's -erf term of the central image is accurate only next to them), not provided here
-        if (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)
-            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic gravity (replica shells) is not provided");
         // explicit groups (mHolder_.traverse(gravGroup, ...), ve_hydro_bdt.hpp:279-285): only their targets
         sx_groups tmp;
         if (int rc = resolveView(c, g, tmp, f->n, false)) return rc;
         GravArgs a   = gravArgs(c, f, tree);
+        a.numShells  = numShells;
+        a.boxL[0] = box->lim[1] - box->lim[0], a.boxL[1] = box->lim[3] - box->lim[2];
+        a.boxL[2] = box->lim[5] - box->lim[4];
         a.first      = g->firstBody;
         a.last       = g->lastBody;
         a.active     = c->viewActive;
@@ -1175,6 +1173,27 @@ extern "C"
         if (eb) return fail(c, SX_ERR_TRAVERSAL, "GPU traversal stack exhausted in Barnes-Hut");
         if (egrav) *egrav = eh;
         return SX_OK;
+    }
+
+    int sx_gravity_traverse(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_tree* tree, const sx_box* box,
+                            const double* centers, const float* multipoles, float G, double* egrav)
+    {
+        if (!g || !f || !tree || !box || !centers || !multipoles || g->lastBody > f->n)
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: bad arguments");
+        // a periodic box needs the walk's image shells (sx_gravity_traverse_pbc) and the Ewald correction
+        if (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse: periodic box (use sx_gravity_traverse_pbc)");
+        return gravityTraverseShells(c, g, f, tree, box, centers, multipoles, G, 0, egrav);
+    }
+
+    int sx_gravity_traverse_pbc(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_tree* tree,
+                                const sx_box* box, const double* centers, const float* multipoles, float G,
+                                int numShells, double* egrav)
+    {
+        if (!g || !f || !tree || !box || !centers || !multipoles || g->lastBody > f->n || numShells < 0 ||
+            numShells > 4)
+            return fail(c, SX_ERR_ARG, "sx_gravity_traverse_pbc: bad arguments");
+        return gravityTraverseShells(c, g, f, tree, box, centers, multipoles, G, numShells, egrav);
     }
 
     int sx_gravity_ewald(sx_ctx* c, const sx_groups* g, const sx_fields* f, const sx_box* box, const double* centers,
@@ -1208,7 +1227,7 @@ extern "C"
         a.first = g->firstBody, a.last = g->lastBody;
         a.x = f->x, a.y = f->y, a.z = f->z, a.m = f->m;
         a.ax = f->ax, a.ay = f->ay, a.az = f->az;
-        a.G = G, a.active = c->viewActive, a.hsum = hd, a.usum = us;
+        a.G = G, a.active = c->viewActive, a.hsum = hd, a.usum = us, a.uscale = 1.0;
         SX_HIP(c, ewaldCorrection(a, c->stream));
         double u = 0;
         SX_HIP(c, hipMemcpyAsync(&u, us, sizeof(double), hipMemcpyDeviceToHost, c->stream));

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kEwaldBlock) void ewaldKernel(EwaldArgs a)
         double t = 0;
         for (int w = 0; w < kEwaldBlock / kWave; ++w)
             t += s_red[w];
-        atomicAdd(a.usum, t);
+        atomicAdd(a.usum, a.uscale * t);
     }
 }
 

@@ -17,6 +17,8 @@
  *             175-201) and P2P (kernel.hpp:514-535) in double with 1/sqrt like the reference's host path; only the
  *             summation order differs from the reference's depth-first walk.
  */
+#include <type_traits>
+
 #include "sx_gravity.hpp"
 
 namespace sx
@@ -244,8 +246,10 @@ struct __attribute__((aligned(16))) GSrc
 #define SX_GRAV_WPE 5 // 96 VGPRs: five waves per SIMD (a few spills, outside the evaluation loops)
 #endif
 //! COUNT: the per-target interaction counts (GravArgs::interactions, BhStats) -- a separate instantiation because the
-//! counters' registers cost the traversal 9 SGPR and 4 VGPR spills and 3.6 ms at Evrard n=300 (A/B)
-template<bool FAST, bool COUNT>
+//! counters' registers cost the traversal 9 SGPR and 4 VGPR spills and 3.6 ms at Evrard n=300 (A/B).  PBC: the walk
+//! over the periodic images (GravArgs::numShells) -- likewise its own instantiation (the loop's state took the open
+//! walk from 14 to 48 VGPR spills)
+template<bool FAST, bool COUNT, bool PBC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE))) void gravityTraverseKernel(GravArgs args)
 {
     // the fields the traversal reads, as scalars: with the many closures below capturing the kernel argument by
@@ -298,28 +302,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
     const double ox = readfirstlaneD(xi), oy = readfirstlaneD(yi), oz = readfirstlaneD(zi); // lane 0's target
     const float  txr = (float)(xi - ox), tyr = (float)(yi - oy), tzr = (float)(zi - oz);
 
-    // target box of each 16-lane quarter (computeCenterAndSize, traversal_cpu.hpp:43-59), over its valid targets
-    double lo[3] = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
-    double hiB[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1)
-        for (int d = 0; d < 3; ++d)
-        {
-            lo[d]  = fmin(lo[d], __shfl_xor(lo[d], o, 16));
-            hiB[d] = fmax(hiB[d], __shfl_xor(hiB[d], o, 16));
-        }
     // the quarters' target boxes (center, half size): wave-uniform, read by every node test; in LDS (broadcast reads)
     // -- as registers they did not stay scalar and were spilled to scratch inside the traversal loop
     double* const tb = &s_tbox[wave][0][0];
+    // target box of each 16-lane quarter (computeCenterAndSize, traversal_cpu.hpp:43-59), over its valid targets
+    // shifted by -(sx, sy, sz) (a periodic image, traversal_cpu.hpp:205-212)
+    auto setBoxes = [&](double sx, double sy, double sz) {
+        const double t0 = xi - sx, t1 = yi - sy, t2 = zi - sz;
+        double       lo[3]  = {valid ? t0 : INFINITY, valid ? t1 : INFINITY, valid ? t2 : INFINITY};
+        double       hiB[3] = {valid ? t0 : -INFINITY, valid ? t1 : -INFINITY, valid ? t2 : -INFINITY};
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-        for (int d = 0; d < 3; ++d)
-        {
-            const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
-            if (lane == 0) tb[6 * qq + d] = (h + l) * 0.5, tb[6 * qq + 3 + d] = (h - l) * 0.5;
-        }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+        for (int o = 8; o > 0; o >>= 1)
+            for (int d = 0; d < 3; ++d)
+            {
+                lo[d]  = fmin(lo[d], __shfl_xor(lo[d], o, 16));
+                hiB[d] = fmax(hiB[d], __shfl_xor(hiB[d], o, 16));
+            }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+            for (int d = 0; d < 3; ++d)
+            {
+                const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
+                if (lane == 0) tb[6 * qq + d] = (h + l) * 0.5, tb[6 * qq + 3 + d] = (h - l) * 0.5;
+            }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    };
+    if constexpr (!PBC) // the box itself, once (inline: as a call of the lambda the open walk took two more spills)
+    {
+        double lo[3]  = {valid ? xi : INFINITY, valid ? yi : INFINITY, valid ? zi : INFINITY};
+        double hiB[3] = {valid ? xi : -INFINITY, valid ? yi : -INFINITY, valid ? zi : -INFINITY};
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1)
+            for (int d = 0; d < 3; ++d)
+            {
+                lo[d]  = fmin(lo[d], __shfl_xor(lo[d], o, 16));
+                hiB[d] = fmax(hiB[d], __shfl_xor(hiB[d], o, 16));
+            }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+            for (int d = 0; d < 3; ++d)
+            {
+                const double l = __shfl(lo[d], 16 * qq), h = __shfl(hiB[d], 16 * qq);
+                if (lane == 0) tb[6 * qq + d] = (h + l) * 0.5, tb[6 * qq + 3 + d] = (h - l) * 0.5;
+            }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the image being walked: the targets' coordinates and the fast variant's origin, shifted
+    using Shifted = std::conditional_t<PBC, double, const double>; // the open walk: plain copies of xi, ox
+    Shifted xs = xi, ys = yi, zs = zi, oxs = ox, oys = oy, ozs = oz;
     const uint64_t bv     = __ballot(valid); // quarters with at least one valid target (lanes fill in order)
     const unsigned qValid = ((bv & 0xffffull) ? 1u : 0u) | (((bv >> 16) & 0xffffull) ? 2u : 0u) |
                             (((bv >> 32) & 0xffffull) ? 4u : 0u) | (((bv >> 48) & 0xffffull) ? 8u : 0u);
@@ -409,7 +441,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const double* c    = a.centers4 + 4 * (size_t)node;
                     const float*  M    = a.multipoles + 8 * (size_t)node;
                     em                 = (unsigned)(e & 15);
-                    sA[lane] = make_float4((float)(c[0] - ox), (float)(c[1] - oy), (float)(c[2] - oz), M[0]);
+                    sA[lane] = make_float4((float)(c[0] - oxs), (float)(c[1] - oys), (float)(c[2] - ozs), M[0]);
                     sB[lane] = make_float4(M[1], M[2], M[3], M[4]);
                     sC[lane] = make_float2(M[5], M[6]);
                 }
@@ -447,7 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                 const int node = e >> 4;
                 if constexpr (COUNT) numM2P += targetsOf((unsigned)(e & 15));
                 if (valid && (((e & 15) >> q) & 1))
-                    m2p(acc, xi, yi, zi, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
+                    m2p(acc, xs, ys, zs, a.centers4 + 4 * (size_t)node, a.multipoles + 8 * (size_t)node);
             }
         nM = 0;
     };
@@ -528,8 +560,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     const bool  in = (uint32_t)lane < cn;
                     const int   P = (lane >> 3) * 4 + (lane & 3), hf = (lane >> 2) & 1;
                     float*      d = reinterpret_cast<float*>(&s_srcF[wave][buf][0]) + P * 8 + hf;
-                    d[0] = in ? (float)(px - ox) : 1e18f, d[2] = in ? (float)(py - oy) : 1e18f;
-                    d[4] = in ? (float)(pz - oz) : 1e18f, d[6] = in ? pm : 0.0f;
+                    d[0] = in ? (float)(px - oxs) : 1e18f, d[2] = in ? (float)(py - oys) : 1e18f;
+                    d[4] = in ? (float)(pz - ozs) : 1e18f, d[6] = in ? pm : 0.0f;
                     s_hF[wave][buf][P * 2 + hf] = in ? ph : 0.0f;
                 }
             }
@@ -601,7 +633,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
                     for (uint32_t s = 0; s < cnt; ++s)
                     {
                         const GSrc src = s_src[wave][s];
-                        p2p(acc, xi, yi, zi, src.x, src.y, src.z, src.m, hi, src.h);
+                        p2p(acc, xs, ys, zs, src.x, src.y, src.z, src.m, hi, src.h);
                     }
             }
         }
@@ -614,6 +646,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         n += __popcll(b);
     };
 
+    // periodic images (computeGravity with numShells, traversal_cpu.hpp:200-216: iz, iy, ix; the targets shifted by
+    // -(ix Lx, iy Ly, iz Lz)); numShells 0: the box itself
+    const int ns = PBC ? args.numShells : 0;
+    for (int iz = -ns; iz <= ns; ++iz)
+    for (int iy = -ns; iy <= ns; ++iy)
+    for (int ix = -ns; ix <= ns; ++ix)
+    {
+    if constexpr (PBC)
+    {
+        const double sx = ix * args.boxL[0], sy = iy * args.boxL[1], sz = iz * args.boxL[2];
+        xs = xi - sx, ys = yi - sy, zs = zi - sz;
+        oxs = ox - sx, oys = oy - sy, ozs = oz - sz;
+        setBoxes(sx, sy, sz);
+    }
     // root (singleTraversal, traversal.hpp:69-80)
     {
         bool           massless;
@@ -660,6 +706,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SX_GRAV_WPE
         }
         __builtin_amdgcn_wave_barrier();
     }
+    } // images
     if (overflow && lane == 0) atomicOr(a.err, 1u);
 
     // output: ax += G * acc (computeGravity, traversal_cpu.hpp:218-228), egrav = 0.5 sum G m_i phi_i
@@ -872,7 +919,13 @@ hipError_t gravityTraverse(const GravArgs& a, hipStream_t s)
     if (a.last <= a.first) return hipSuccess;
     const uint32_t waves = (a.last - a.first + kWave - 1) / kWave;
     const unsigned g = (waves + 3) / 4;
-    if (a.interactions)
+    if (a.numShells > 0)
+    {
+        // periodic images: counting (BhStats) is not provided on this path
+        if (a.fast) gravityTraverseKernel<true, false, true><<<g, 256, 0, s>>>(a);
+        else gravityTraverseKernel<false, false, true><<<g, 256, 0, s>>>(a);
+    }
+    else if (a.interactions)
     {
         if (a.fast) gravityTraverseKernel<true, true><<<g, 256, 0, s>>>(a);
         else gravityTraverseKernel<false, true><<<g, 256, 0, s>>>(a);

@@ -37,6 +37,8 @@ struct GravArgs
     const uint8_t* active; // nullable: targets with active[i] == 0 (outside the group view) get no gravity
     unsigned long long* interactions; // nullable: [0] += P2P, [1] += M2P interactions summed over the targets (the
                                       // reference's BhStats sumP2P / sumM2P, nbody/traversal.cuh:346-357, 614-620)
+    int    numShells;  // periodic images walked per axis on each side (traversal_cpu.hpp:200-216); 0: the box itself
+    double boxL[3];    // box lengths (the image shifts)
 };
 
 //! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi
@@ -89,7 +91,8 @@ struct EwaldArgs
     float          G;
     const uint8_t* active; // nullable: only targets with active[i] != 0
     const double*  hsum;   // numH x {hr_scaled x, y, z, hfac_cos, hfac_sin} (device)
-    double*        usum;   // device accumulator of sum m phi (atomic)
+    double*        usum;   // device accumulator: += uscale * sum m phi (atomic)
+    double         uscale;
     EwaldParams    p;
 };
 

@@ -1764,8 +1764,10 @@ extern "C"
                       uint32_t bucketSize)
     {
         if (p->propagator < 0 || p->propagator > 2) return SX_ERR_ARG;
-        // self-gravity in a periodic box needs the walk's replica shells (sx_gravity_traverse): refused, not run open
-        if (p->g != 0.0 && (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1)) return SX_ERR_ARG;
+        // self-gravity in a periodic box: the image walk + Ewald correction of the VE / std step (single rank); the
+        // ve-bdt driver's gravity has no image walk
+        if (p->g != 0.0 && p->propagator == 2 && (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1))
+            return SX_ERR_ARG;
         auto* s   = new sx_sim;
         s->ctx    = ctx;
         s->p      = *p;
@@ -1821,6 +1823,10 @@ extern "C"
 
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
+        // periodic self-gravity runs on one rank only (the multi-rank far field has no image walk)
+        if (s->p.g != 0.0 && s->box.bnd[0] == 1 && sx_comm_transport_internal(c) &&
+            sx_comm_transport_internal(c)->size() > 1)
+            return SX_ERR_ARG;
         s->keysFresh  = false;
         s->skin.valid = false;
         s->comm       = sx_comm_transport_internal(c);
@@ -2457,7 +2463,39 @@ extern "C"
             ga.interactions = inter;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
             ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
+            const bool pbc = s->box.bnd[0] == 1 || s->box.bnd[1] == 1 || s->box.bnd[2] == 1;
+            if (pbc)
+            {
+                // periodic (gravity_wrapper.hpp:135-157): the walk over one image shell, then the Ewald correction
+                // with the reference's EwaldSettings defaults (ewald.h:17-21)
+                ga.numShells = 1;
+                ga.boxL[0] = s->box.lim[1] - s->box.lim[0], ga.boxL[1] = s->box.lim[3] - s->box.lim[2];
+                ga.boxL[2] = s->box.lim[5] - s->box.lim[4];
+                ga.interactions = nullptr;
+            }
             SIM_HIP(gravityTraverse(ga, st));
+            if (pbc)
+            {
+                if (ga.boxL[0] != ga.boxL[1] || ga.boxL[0] != ga.boxL[2]) return SX_ERR_ARG; // Ewald: cubic boxes
+                double c4[4];
+                float  m8[8];
+                SIM_HIP(hipMemcpyAsync(c4, ga.centers4, sizeof(c4), hipMemcpyDeviceToHost, st));
+                SIM_HIP(hipMemcpyAsync(m8, ga.multipoles, sizeof(m8), hipMemcpyDeviceToHost, st));
+                SIM_HIP(hipStreamSynchronize(st));
+                EwaldArgs ea{};
+                std::vector<double> hs;
+                if (ewaldInit(ea.p, hs, c4, m8, ga.boxL[0], 1, 2.6, 2.8, 2.0, 3.0e-3)) return SX_ERR_ARG;
+                double* hd = s->work.get<double>("ewald.hsum", std::max<size_t>(hs.size(), 5));
+                if (!hd) return SX_ERR_NOMEM;
+                SIM_HIP(hipMemcpyAsync(hd, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, st));
+                ea.first = ga.first, ea.last = ga.last;
+                ea.x = s->x, ea.y = s->y, ea.z = s->z, ea.m = s->m;
+                ea.ax = s->ax, ea.ay = s->ay, ea.az = s->az;
+                ea.G = ga.G, ea.hsum = hd, ea.usum = &s->sc->egrav, ea.uscale = 0.5 * (double)ga.G;
+                SIM_HIP(ewaldCorrection(ea, st));
+                // the host table must outlive the copy
+                SIM_HIP(hipStreamSynchronize(st));
+            }
             }
             maxAccSq(s, st);
         }

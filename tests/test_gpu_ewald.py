@@ -7,8 +7,12 @@ against the reference's own outputs and the restatement pinned to it bit for bit
 * physics: a uniform lattice in its periodic box feels no net force -- the 27 images summed directly (numpy, softened
   like P2P) plus the GPU correction with numReplicaShells = 1 leave < 2e-3 of the direct sum's largest |a| (the
   restatement: 7.9e-4);
-* a non-cubic box is refused (the reference throws, ewald.hpp:386); so is a simulation with self-gravity in a periodic
-  box (the walk's replica shells are not provided)."""
+* a non-cubic box is refused (the reference throws, ewald.hpp:386);
+* the walk over the periodic images (sx_gravity_traverse_pbc, numShells 1) against the reference's computeGravity with
+  numShells = 1 (tests/golden/grav_pbc_ref.npz, oracle/gen_grav_pbc.py): upsweep bit-identical, accelerations as the
+  open walk's test (exact variant: 1e-6 |a| + 1e-7 max|a|; fast: 1e-5, 1e-6), egrav 1e-10 / 1e-6;
+* the whole step in a periodic box with self-gravity (walk + Ewald): a uniform medium at rest feels no force (< 1e-2
+  of the open box's largest gravity); ve-bdt with periodic self-gravity is refused."""
 import ctypes as C
 import os
 import sys
@@ -132,7 +136,83 @@ def test_ewald_refuses_non_cubic_box(ctx):
     ctx.free_all()
 
 
-def test_sim_refuses_periodic_self_gravity(ctx):
+@pytest.mark.parametrize("exact", [True, False])
+def test_periodic_walk_vs_reference(ctx, exact):
+    import gen_grav_pbc as gp
+    import gpu_util as gutil
+    import pyoracle as po
+    d = gu.load("grav_pbc_ref.npz")
+    ora = po.load_oracle()
+    st, obox = gp.state()
+    keys = ora.sfc_keys(st, obox).copy()
+    o = np.argsort(keys, kind="stable")
+    for k in po.CONSERVED:
+        st.arrays[k][:] = st.arrays[k][o]
+    st.keys[:] = keys[o]
+    assert np.array_equal(st.x, d["x"]) and np.array_equal(st.m, d["m"])
+    ctx.set_exact(exact)
+    try:
+        box = gutil.box_to_sx(obox)
+        ds = sx.DeviceState(ctx, gutil.host_dict(st))
+        tree, _ = gutil.device_tree(ctx, ds.dev["keys"], st.n, 64, box)
+        nn = tree.numNodes
+        cen = ctx.alloc(4 * nn, np.float64)
+        mp = ctx.alloc(8 * nn, np.float32)
+        ctx.check(ctx.L.sx_gravity_upsweep(ctx.h, C.byref(ds.fields), C.byref(tree), 0.5, cen.ptr, mp.ptr), "upsweep")
+        g = sx.SxGroups(firstBody=0, lastBody=st.n, numGroups=(st.n + 63) // 64)
+        eg = C.c_double()
+        assert ctx.L.sx_gravity_traverse(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(tree), C.byref(box), cen.ptr,
+                                         mp.ptr, 1.0, C.byref(eg)) == sx.SX_ERR_ARG  # periodic: the image walk only
+        ctx.check(ctx.L.sx_gravity_traverse_pbc(ctx.h, C.byref(g), C.byref(ds.fields), C.byref(tree), C.byref(box),
+                                                cen.ptr, mp.ptr, 1.0, 1, C.byref(eg)), "traverse_pbc")
+        assert np.array_equal(cen.get().reshape(-1, 4), d["centers"])
+        assert np.array_equal(mp.get().reshape(-1, 8), d["multipoles"])
+        acc = np.stack([ds.get("ax"), ds.get("ay"), ds.get("az")]).astype(np.float64)
+    finally:
+        ctx.set_exact(False)
+    ref = d["shells1_acc"].astype(np.float64)
+    rtol, afrac = (1e-6, 1e-7) if exact else (1e-5, 1e-6)
+    # complete 16-target groups only: the reference pads the last group's target array with zeros
+    # (traversal_cpu.hpp:190-197), which its shifted images carry to -(ix Lx, iy Ly, iz Lz) and into that group's box
+    n = st.n - st.n % 16
+    err = np.abs(acc - ref) - (rtol * np.abs(ref) + afrac * np.abs(ref).max())
+    print("periodic walk", "exact" if exact else "fast", "max |a - a_ref| complete groups",
+          f"{np.abs(acc - ref)[:, :n].max():.3g}", "last group", f"{np.abs(acc - ref)[:, n:].max():.3g}",
+          "worst index", int(np.argmax(np.abs(acc - ref).max(0))), "of", st.n, "max|a|", f"{np.abs(ref).max():.3g}")
+    assert err[:, :n].max() <= 0, err[:, :n].max()
+    assert np.abs(acc - ref)[:, n:].max() <= 1e-3 * np.abs(ref).max()
+    assert eg.value == pytest.approx(float(d["shells1_egrav"][0]), rel=1e-5)
+    ctx.free_all()
+
+
+def test_sim_periodic_gravity_uniform_medium(ctx):
+    """a uniform lattice at rest with uniform temperature in its periodic box: no pressure gradient and, with the image
+    walk + Ewald correction, no net gravity; the same medium in an open box falls inwards"""
+    import pyoracle as po
+    res = {}
+    for bnd in (1, 0):
+        st, obox = po.sedov_state(12)
+        st.temp[:] = np.float64(st.temp.min())
+        for k in ("vx", "vy", "vz"):
+            st.arrays[k][:] = 0
+        for k in ("x", "y", "z"):
+            st.arrays[k + "_m1"][:] = 0
+        box = sx.make_box(list(obox.lim), [bnd] * 3)
+        sim = sx.Sim(ctx, st.n, box, params=sx.default_params(g=1.0))
+        try:
+            sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+            sim.step()
+            assert sim.stats()["numFailed"] == 0
+            f = sim.get(["ax", "ay", "az"])
+            res[bnd] = np.sqrt(f["ax"].astype(float) ** 2 + f["ay"] ** 2 + f["az"] ** 2).max()
+            assert np.isfinite(sim.conserved()["egrav"])
+        finally:
+            sim.close()
+    print("uniform medium: max |a| periodic", f"{res[1]:.3g}", "open", f"{res[0]:.3g}")
+    assert res[1] < 1e-2 * res[0], res
+
+
+def test_sim_refuses_periodic_self_gravity_bdt(ctx):
     box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
     with pytest.raises(Exception):
-        sx.Sim(ctx, 1000, box, params=sx.default_params(g=1.0))
+        sx.Sim(ctx, 1000, box, params=sx.default_params(g=1.0, bdt=True))
