@@ -9,6 +9,8 @@ Inputs are generated and kept in HBM; nothing leaves the device inside the timed
 4-byte tree-level counts and stats.  The workload is the metric's own: Sedov -n 400 (64M particles) in total at every
 N (strong scaling: N=1 holds all 64M particles on one MI355X, N=8 holds 8M + halos per GPU); --side 200 gives
 BASELINE config 2.
+With skin lists (one rank, the default) the timed window starts with a forced full sync + skin build, so the headline
+carries the builds' cost (1 per K steps; the steady state has 1 per max_reuse = 24, reported as amortized_*).
 Rank 0 prints ONE JSON line.  Its "roofline" is the dominant kernel's (largest share of the step): HBM bytes per
 launch from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_<init>_n<side>.json) over the kernel's
 average launch time measured here with HIP events on its stream.
@@ -191,7 +193,7 @@ def gravity_roofline(ms, n_local, inter, pmc):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=24, help="timed steps (default: one skin cycle, max_reuse)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--side", type=int, default=0,
                     help="total lattice side (default: the metric's Sedov -n 400 at every N; noh/evrard 300)")
@@ -199,8 +201,8 @@ def parse():
     ap.add_argument("--exact", action="store_true", help="use the no-FMA (bit-reproducible) kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-build-step", action="store_true",
-                    help="skip the forced skin build step after the timed window (profiling runs: the PMC summary "
-                         "normalises its counters by steps + warmup)")
+                    help="do not force a full sync + skin build at the start of the timed window (profiling runs of "
+                         "filter-served steps only: the PMC summary normalises its counters by steps + warmup)")
     ap.add_argument("--backend", default="rccl", help="rccl (one GPU per rank) or host (staged, tests)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--cpu-side", type=int, default=200, help="Sedov lattice side of the CPU baseline sample")
@@ -330,13 +332,22 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # skin lists (one rank): the timed window starts with a full sync + build of every cluster's skin, so `value` and
+    # `ms_per_step` carry at least their share of the builds that come every max_reuse steps at the latest (a window
+    # shorter than max_reuse carries more than its share: 1 build in K steps, against 1 in max_reuse)
+    skin_window = args.skin > 0 and world == 1 and not args.no_build_step
+    if skin_window:
+        sim.rebuild_lists()
     ctx.sync()
     barrier()
     skin0 = sim.skin_stats()
     stage_sum, kern_sum = {}, {}
+    step_s = []  # host time of every timed step (sx_sim_step returns after its stream synchronisation)
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        ts = time.perf_counter()
         sim.step()
+        step_s.append(time.perf_counter() - ts)
         for k, v in sim.stage_times().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
         for k, v in sim.kernel_times().items():
@@ -355,31 +366,20 @@ def main():
             for k, v in sim.skin_stats().items()}  # the timed steps'
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
-    # skin lists: a timed window of filter-served steps does not contain the full build that comes every max_reuse
-    # steps at the latest; one more step after the timed region, forced to be a build, gives its cost and the
-    # amortized step (the same decision on every rank: nothing differs between ranks here)
-    build_ms = None
-    if skin.get("reuse_steps", 0) > 0 and skin.get("builds", 1) == 0 and not args.no_build_step:
-        sim.rebuild_lists()
-        ctx.sync()
-        barrier()
-        tb = time.perf_counter()
-        sim.step()
-        ctx.sync()
-        barrier()
-        build_ms = (time.perf_counter() - tb) * 1e3
-        if dist is not None:
-            import torch
-
-            t = torch.tensor([build_ms], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            build_ms = float(t.item())
+    if skin_window and args.steps > 1 and skin.get("builds", 0) >= 1:
+        # the window's first step was the full sync + build, the others (up to max_reuse) filter-served
         R = max(1, int(args.skin_reuse))
+        build_ms = step_s[0] * 1e3
+        filt_ms = sum(step_s[1:]) / (len(step_s) - 1) * 1e3
         skin["build_step_ms"] = build_ms
-        skin["amortized_ms_per_step"] = (ms_step * (R - 1) + build_ms) / R
+        skin["filter_step_ms"] = filt_ms
+        skin["filter_step_value"] = n_total / (filt_ms * 1e-3)
+        skin["amortized_ms_per_step"] = (filt_ms * (R - 1) + build_ms) / R
         skin["amortized_value"] = n_total / (skin["amortized_ms_per_step"] * 1e-3)
-        skin["amortized_note"] = (f"one full sync + build every {R} steps at the latest (max_reuse), the other steps "
-                                  "filter-served like the timed ones")
+        skin["amortized_note"] = (f"value/ms_per_step: the timed window starts with a full sync + skin build "
+                                  f"({skin['builds']} build(s) in {args.steps} steps); amortized: one build every {R} "
+                                  "steps (max_reuse), the other steps filter-served; both from the same window's "
+                                  "per-step host times")
     inter = None
     if args.init == "evrard":  # self-gravity on (g = 1); the same decision on every rank: the extra step is collective
         # the interaction counts (BhStats) of one more step after the timed region: counting is a separate, slower

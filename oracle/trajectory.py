@@ -124,6 +124,9 @@ CASES = {
     # (made with the -O3 build of the reference, libsphexa_ref_fast.so: ~1 h each on 8 cores)
     "noh300": ("traj_noh300.npz", "noh", 300, 100, (25, 50, 100), 0.5, 50),
     "evrard300": ("traj_evrard300.npz", "evrard", 300, 100, (50, 100), 1.0, 50),
+    # the metric's own workload (BASELINE config 4, Sedov -n 400, 64M particles): the reference's run for 30 steps,
+    # long enough that the GPU's skin lists go through a forced full rebuild (max_reuse 24) inside the compared window
+    "sedov400": ("traj_sedov400.npz", "sedov", 400, 30, (10, 20, 30), 0.5, 50),
 }
 # propagator / physics options of a case (pyoracle.default_params keywords; both the reference run and the GPU run)
 CASE_PARAMS = {"sedov_std": {"std": True}, "evrard": {"g": 1.0}, "evrard300": {"g": 1.0}}

@@ -423,16 +423,18 @@ __global__ void cellCountCheckKernel(const uint32_t* total, uint32_t expected, u
     if (*total != expected) *err = 1u;
 }
 
+//! the buffers hold nCells (+1) entries, sized from the sync's histogram; a scan that disagrees (cellCountCheckKernel
+//! reports it) writes nothing out of range
 __global__ void cellScatterKernel(const uint64_t* keys, const uint32_t* flag, const uint32_t* scan, size_t n,
-                                  uint32_t* cellBeg, uint32_t* cellIds)
+                                  uint32_t nCells, uint32_t* cellBeg, uint32_t* cellIds)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i < n && flag[i])
+    if (i < n && flag[i] && scan[i] < nCells)
     {
         cellBeg[scan[i]] = (uint32_t)i;
         cellIds[scan[i]] = (uint32_t)(keys[i] >> kCellShift);
     }
-    if (i == n) cellBeg[scan[n]] = (uint32_t)n;
+    if (i == n && scan[n] <= nCells) cellBeg[scan[n]] = (uint32_t)n;
 }
 
 __global__ void nearToFarKernel(const uint32_t* nearFlag, size_t n, uint32_t* farFlag, uint32_t* reqFlag)
@@ -960,9 +962,11 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     }
     if (int e = sortLocals(s, nl, st)) return e;
 
-    // --- 2. global histogram -> splitters
+    // --- 2. global histogram -> splitters (the small per-rank buffers of the sync were allocated by sx_sim_set_comm,
+    //        so nothing here fails on one rank alone between two collectives)
     const size_t nb   = size_t(1) << kHistBits;
     uint32_t*    bins = s->work.get<uint32_t>("dom.bins", nb);
+    if (!bins) return SX_ERR_NOMEM; // allocated by set_comm: cannot fail here
     SIM_HIP(hipMemsetAsync(bins, 0, nb * 4, st));
     if (nl) histKernel<<<grid(nl), 256, 0, st>>>(s->keys, nl, bins);
     SIM_COMM(T->allreduceSumU32(bins, nb, st));
@@ -986,7 +990,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     uint64_t* dsplit = s->work.get<uint64_t>("dom.split", P + 1);
     uint64_t* dseg   = s->work.get<uint64_t>("dom.seg", P + 1);
     s->cntBuf = s->work.get<uint64_t>("dom.cnt", 2 * P);
-    if (!dsplit || !dseg || !s->cntBuf) return SX_ERR_NOMEM; // 16 B per rank, kept from the first sync on
+    if (!dsplit || !dseg || !s->cntBuf) return SX_ERR_NOMEM; // allocated by set_comm: cannot fail here
     // the send counts stay on the device: segments of the sorted keys -> counts -> the count exchange, read back
     // together with the receive counts (one synchronisation)
     SIM_HIP(hipMemcpyAsync(dsplit, split.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
@@ -1008,12 +1012,21 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     bool moved = false;
     for (int q = 0; q < P; ++q)
         moved |= (q != r) && (sendCnt[q] || recvCnt[q]);
+    // a local count that disagrees with the histogram cannot happen (the splitters are bin boundaries of the histogram
+    // of these same keys); should it, this rank still takes part in every collective up to the halo count exchange,
+    // sized by the histogram as its peers expect, and aborts all ranks there together (countsOrAbort)
+    bool broken = false;
     if (moved)
     {
         uint64_t nNew = 0;
         for (int q = 0; q < P; ++q)
             nNew += recvCnt[q];
-        if (nNew != nlOf[r]) return SX_ERR_ARG; // cannot happen: the splitters are histogram-bin boundaries
+        broken = nNew != nlOf[r];
+        if (broken)
+        {
+            rbuf   = s->work.get<PRec>("dom.precv", nNew);
+            broken = true;
+        }
         if (nl) packPRecKernel<<<grid(nl), 256, 0, st>>>(s->fields(), nl, sbuf);
         std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
         uint64_t              acc = 0;
@@ -1025,21 +1038,31 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
             ro[q] = acc * sizeof(PRec);
             acc += recvCnt[q];
         }
+        if (!rbuf) // only on the broken path: receive nothing (the peers abort with this rank below)
+            for (int q = 0; q < P; ++q)
+                rb[q] = 0;
         SIM_COMM(T->alltoallv(sbuf, sb.data(), so.data(), rbuf, rb.data(), ro.data(), st));
-        nl = nNew;
-        if (nl) unpackPRecKernel<<<grid(nl), 256, 0, st>>>(rbuf, nl, s->fields());
-        SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, nl, s->dbox, st));
-        if (int e = sortLocals(s, nl, st)) return e;
+        if (!broken)
+        {
+            nl = nNew;
+            if (nl) unpackPRecKernel<<<grid(nl), 256, 0, st>>>(rbuf, nl, s->fields());
+            SIM_HIP(launchSfcKeys(s->x, s->y, s->z, s->keys, nl, s->dbox, st));
+            if (int e = sortLocals(s, nl, st)) return e;
+        }
     }
 
     // --- 4. halo discovery: request boxes, exchange, mark, send lists
     // the exchange delivers exactly this rank's bins (the peers size their box receives from nlOf): the splitters
-    // are bin boundaries of the histogram of these same keys, so this holds on every rank by construction (checked
-    // after the exchange above); no agreement round trip
-    if (nl != nlOf[r]) return SX_ERR_ARG;
-    const size_t nChunks = (nl + kChunk - 1) / kChunk;
+    // are bin boundaries of the histogram of these same keys, so this holds on every rank by construction; a rank
+    // where it does not (`broken`) sends boxes of the size its peers expect and aborts them at the count exchange below
+    broken |= nl != nlOf[r];
+    if (broken) nl = std::min<size_t>(nl, nlOf[r]);
+    const size_t nChunks = (nlOf[r] + kChunk - 1) / kChunk;
     ReqBox*      myBoxes = s->work.get<ReqBox>("dom.mybox", nChunks);
-    if (nChunks) chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
+    if (!myBoxes) return SX_ERR_NOMEM;
+    if (broken) SIM_HIP(hipMemsetAsync(myBoxes, 0, nChunks * sizeof(ReqBox), st));
+    else if (nChunks)
+        chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x, s->y, s->z, s->h, nl, margin, qm, r, myBoxes);
     std::vector<uint64_t> boxCnt(P, nChunks), boxRecv(P);
     boxCnt[r] = 0;
     for (int q = 0; q < P; ++q)
@@ -1077,7 +1100,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
     const size_t     nf       = (size_t)Pb * (nl + 1);
     // scratch failures are not returned here (the peers would wait in the count exchange below): they skip the
     // send-list work and abort every rank at that exchange (countsOrAbort)
-    bool      fail = nf > (size_t)INT32_MAX; // one peer's segment alone beyond the scan's range
+    bool      fail = broken || nf > (size_t)INT32_MAX; // one peer's segment alone beyond the scan's range
     uint32_t* flag = fail ? nullptr : s->work.get<uint32_t>("dom.flag", nf);
     uint32_t* scan = fail ? nullptr : s->work.get<uint32_t>("dom.scan", nf);
     uint32_t* segs = s->work.get<uint32_t>("dom.segs", Pb + 1);
@@ -1281,7 +1304,7 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     cellCountCheckKernel<<<1, 1, 0, st>>>(scan + nl, (uint32_t)nCells, &s->sc->gravErr);
     uint32_t* cellBeg = W.get<uint32_t>("g.cellBeg", nCells + 1);
     uint32_t* cellIds = W.get<uint32_t>("g.cellIds", nCells);
-    cellScatterKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, flag, scan, nl, cellBeg, cellIds);
+    cellScatterKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, flag, scan, nl, (uint32_t)nCells, cellBeg, cellIds);
     GCell* mine = W.get<GCell>("g.mine", nCells);
     SIM_HIP(cellMoments(s->x + s->first, s->y + s->first, s->z + s->first, s->m + s->first, cellBeg, cellIds, nCells,
                         farL2N, s->farTree.centers, s->farTree.sizes, invTheta, mine, st));
@@ -1503,12 +1526,19 @@ void maxAccSq(sx_sim* s, hipStream_t st)
                                                                           &s->sc->maxAccSqBits);
 }
 
+//! self-gravity with periodic images (the reference's test, gravity_wrapper.hpp:77,135: boundaryX; sx_sim_create
+//! admits only boxes periodic along all three axes with self-gravity)
+bool periodicGravity(const sx_sim* s) { return s->p.g != 0.0 && s->box.bnd[0] == 1; }
+
 //! skin lists serve this sim: one rank, not ve-bdt, cluster lists.  With self-gravity a reuse step traverses the last
-//! sync's tree, its multipoles formed from the current positions and its MAC geometry refreshed (cells + particles)
+//! sync's tree, its multipoles formed from the current positions and its MAC geometry refreshed (cells + particles).
+//! Not with periodic self-gravity: between syncs a particle that crossed a periodic face is wrapped to the far side of
+//! the box while it stays in its old leaf, so the leaf's multipole (raw coordinates) would spread across the box
+//! while its refreshed MAC box (minimum image) covers only the old cell -- every step syncs there
 bool skinUsable(const sx_sim* s)
 {
     return s->skin.factor > 0.0f && !(s->comm && s->comm->size() > 1) && s->p.propagator != 2 &&
-           NbLists::localPossible(s->p.ngmax);
+           NbLists::localPossible(s->p.ngmax) && !periodicGravity(s);
 }
 
 //! widest skin the adaptation goes to: skin lists (1.16)^3 = 1.56x the neighbors; wider unions outgrow the filter's LDS
@@ -1764,10 +1794,16 @@ extern "C"
                       uint32_t bucketSize)
     {
         if (p->propagator < 0 || p->propagator > 2) return SX_ERR_ARG;
-        // self-gravity in a periodic box: the image walk + Ewald correction of the VE / std step (single rank); the
-        // ve-bdt driver's gravity has no image walk
-        if (p->g != 0.0 && p->propagator == 2 && (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1))
-            return SX_ERR_ARG;
+        // self-gravity in a periodic box: the image walk + Ewald correction of the VE / std step (single rank).  The
+        // reference decides on boundaryX alone (gravity_wrapper.hpp:77,135) and walks images along all three axes;
+        // here a mixed box (some axes periodic, some not) is refused rather than given images along open axes, the
+        // Ewald sum needs a cubic box (ewald.hpp:149-214), and the ve-bdt driver's gravity has no image walk
+        if (p->g != 0.0 && (box->bnd[0] == 1 || box->bnd[1] == 1 || box->bnd[2] == 1))
+        {
+            const bool allPbc = box->bnd[0] == 1 && box->bnd[1] == 1 && box->bnd[2] == 1;
+            const double lx = box->lim[1] - box->lim[0], ly = box->lim[3] - box->lim[2], lz = box->lim[5] - box->lim[4];
+            if (!allPbc || lx != ly || lx != lz || p->propagator == 2) return SX_ERR_ARG;
+        }
         auto* s   = new sx_sim;
         s->ctx    = ctx;
         s->p      = *p;
@@ -1823,13 +1859,25 @@ extern "C"
 
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
+        sx::Transport* T = sx_comm_transport_internal(c);
         // periodic self-gravity runs on one rank only (the multi-rank far field has no image walk)
-        if (s->p.g != 0.0 && s->box.bnd[0] == 1 && sx_comm_transport_internal(c) &&
-            sx_comm_transport_internal(c)->size() > 1)
-            return SX_ERR_ARG;
+        if (periodicGravity(s) && T && T->size() > 1) return SX_ERR_ARG;
+        if (T && T->size() > 1)
+        {
+            // the sync's small per-rank buffers, allocated here so that no rank fails alone between two collectives
+            // of a step (its peers would wait in the next one)
+            const size_t P  = (size_t)T->size();
+            const bool   ok = s->work.get<uint32_t>("dom.bins", size_t(1) << kHistBits) &&
+                            s->work.get<uint64_t>("dom.split", P + 1) && s->work.get<uint64_t>("dom.seg", P + 1) &&
+                            s->work.get<uint64_t>("dom.cnt", 2 * P) && s->work.pinned<uint64_t>("dom.cnth", 2 * P) &&
+                            s->work.get<uint32_t>("dom.agree", 1) && s->work.pinned<uint32_t>("dom.agreeh", 1) &&
+                            s->work.get<unsigned>("dom.hflag", 1) && s->work.pinned<unsigned>("dom.hflagh", 1) &&
+                            s->work.pinned<uint32_t>("dom.errh", 1);
+            if (!ok) return SX_ERR_NOMEM;
+        }
         s->keysFresh  = false;
         s->skin.valid = false;
-        s->comm       = sx_comm_transport_internal(c);
+        s->comm       = T;
         s->commHandle = c;
         return SX_OK;
     }
@@ -2463,7 +2511,7 @@ extern "C"
             ga.interactions = inter;
             SIM_HIP(gravityUpsweep(ga, s->tree.levelRangeHost.data(), st));
             ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
-            const bool pbc = s->box.bnd[0] == 1 || s->box.bnd[1] == 1 || s->box.bnd[2] == 1;
+            const bool pbc = periodicGravity(s);
             if (pbc)
             {
                 // periodic (gravity_wrapper.hpp:135-157): the walk over one image shell, then the Ewald correction
@@ -2476,8 +2524,7 @@ extern "C"
             SIM_HIP(gravityTraverse(ga, st));
             if (pbc)
             {
-                if (ga.boxL[0] != ga.boxL[1] || ga.boxL[0] != ga.boxL[2]) return SX_ERR_ARG; // Ewald: cubic boxes
-                double c4[4];
+                double c4[4]; // (cubic box: checked by sx_sim_create)
                 float  m8[8];
                 SIM_HIP(hipMemcpyAsync(c4, ga.centers4, sizeof(c4), hipMemcpyDeviceToHost, st));
                 SIM_HIP(hipMemcpyAsync(m8, ga.multipoles, sizeof(m8), hipMemcpyDeviceToHost, st));

@@ -216,3 +216,52 @@ def test_sim_refuses_periodic_self_gravity_bdt(ctx):
     box = sx.make_box([-0.5, 0.5, -0.5, 0.5, -0.5, 0.5], [1, 1, 1])
     with pytest.raises(Exception):
         sx.Sim(ctx, 1000, box, params=sx.default_params(g=1.0, bdt=True))
+
+
+def test_sim_refuses_mixed_or_noncubic_periodic_gravity(ctx):
+    """self-gravity with periodic images needs a box periodic along every axis (the reference decides on boundaryX and
+    would walk images along open axes) and a cube (the Ewald sum): refused at creation, not half-way through a step"""
+    for lim, bnd in (([-0.5, 0.5] * 3, [1, 0, 1]), ([-0.5, 0.5] * 3, [0, 1, 1]), ([-0.5, 0.5, -0.5, 0.5, -1, 1], [1] * 3)):
+        with pytest.raises(Exception):
+            sx.Sim(ctx, 1000, sx.make_box(lim, bnd), params=sx.default_params(g=1.0))
+
+
+def test_sim_periodic_gravity_crossing_particles_skin_off(ctx):
+    """with periodic self-gravity every step syncs (no skin reuse step), so a particle that crossed a periodic
+    face is in the leaf of its wrapped position when the multipoles are formed.  A medium drifting through the box
+    (particles cross the faces every few steps) with the default skin gives the same accelerations and potential,
+    bit for bit by id, as the same run with the skin off"""
+    import pyoracle as po
+    out = {}
+    for skin in (0.08, 0.0):
+        st, obox = po.sedov_state(12)
+        st.temp[:] = np.float64(st.temp.min()) * (1 + 0.1 * np.sin(7 * st.x))
+        # a uniform drift of 0.4 lattice spacings (1/12) per first step in x, 0.2 in y: relative velocities stay zero,
+        # so the time-step grows by maxDtIncrease per step and the medium moves several spacings in six steps
+        v = 0.4 / 12 / st.minDt
+        st.arrays["vx"][:] = np.float32(v)
+        st.arrays["vy"][:] = np.float32(0.5 * v)
+        st.arrays["vz"][:] = 0
+        for k in ("x", "y", "z"):
+            st.arrays[k + "_m1"][:] = st.arrays["v" + k] * np.float32(st.minDt)
+        sim = sx.Sim(ctx, st.n, sx.make_box(list(obox.lim), [1, 1, 1]), params=sx.default_params(g=1.0))
+        try:
+            sim.set_skin(skin, 24)
+            sim.set_state(st.arrays, st.minDt, st.minDt_m1)
+            rec = []
+            for _ in range(6):
+                sim.step()
+                assert sim.stats()["numFailed"] == 0
+                f = sim.get(["id", "ax", "ay", "az", "x"])
+                o = np.argsort(f["id"])
+                rec.append(({k: f[k][o] for k in ("ax", "ay", "az", "x")}, sim.conserved()["egrav"]))
+            assert sim.skin_stats()["reuse_steps"] == 0
+            out[skin] = rec
+        finally:
+            sim.close()
+    x0 = out[0.0][0][0]["x"]
+    assert np.any(np.abs(out[0.0][-1][0]["x"] - x0) > 0.5), "no particle crossed a periodic face"
+    for (a, ea), (b, eb) in zip(out[0.08], out[0.0]):
+        for k in ("ax", "ay", "az"):
+            assert np.array_equal(a[k], b[k]), k
+        assert ea == eb
