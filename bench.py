@@ -215,7 +215,28 @@ def parse():
                     help="neighbor lists behind a skin 2h(1+s) between full builds (sx_sim_set_skin; 0: sync + "
                          "search every step, the reference's flow)")
     ap.add_argument("--skin-reuse", type=int, default=24, help="steps between full builds at most")
+    ap.add_argument("--seam", action="store_true",
+                    help="the drop-in path instead: whole VE steps through the C++ mirror of the reference seam "
+                         "(sph-exa_amd/lib/ve_seam_bench, every call synchronous, sync + search every step), "
+                         "default Sedov -n 200; prints that program's JSON line")
     return ap.parse_args()
+
+
+def seam_bench(args):
+    """the reference propagator's view of this library: ve_seam_bench (host/examples/ve_seam_bench.cpp) as a child
+    process on one GPU, its JSON line passed through with the sx_sim figure of the same workload for comparison"""
+    import subprocess
+
+    exe = os.path.join(ROOT, "sph-exa_amd", "lib", "ve_seam_bench")
+    if not os.path.exists(exe):
+        raise SystemExit("sph-exa_amd/lib/ve_seam_bench missing: make -C sph-exa_amd")
+    side = args.side or 200
+    r = subprocess.run([exe, str(side), str(args.steps), str(args.warmup)], capture_output=True, text=True,
+                       timeout=1200)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout[-2000:] + r.stderr[-2000:])
+        raise SystemExit(r.returncode)
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def cpu_model():
@@ -261,6 +282,9 @@ def cpu_baseline(seconds, side):
 
 def main():
     args = parse()
+    if args.seam:
+        print(json.dumps(seam_bench(args)))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

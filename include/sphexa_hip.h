@@ -371,7 +371,8 @@ int sx_gravity_ewald(sx_ctx* ctx, const sx_groups* g, const sx_fields* f, const 
 /* ---- multi-GPU transport (replaces the reference's MPI calls, see sph-exa_amd/csrc/sx_comm.hpp) ---------- */
 typedef struct sx_comm sx_comm;
 /*! host-staged collectives supplied by the caller (e.g. torch.distributed gloo): buffers are host memory,
- *  send/recv segments contiguous in rank order; return 0 on success. op: 0 = u32 sum, 1 = f64 min, 2 = f64 sum. */
+ *  send/recv segments contiguous in rank order; return 0 on success. op: 0 = u32 sum, 1 = f64 min, 2 = f64 sum,
+ *  3 = u32 min, 4 = u32 max. */
 typedef int (*sx_alltoallv_cb)(void* user, const void* sendHost, const uint64_t* sendBytes, void* recvHost,
                                const uint64_t* recvBytes);
 typedef int (*sx_allreduce_cb)(void* user, void* bufHost, uint64_t count, int op);

@@ -598,8 +598,18 @@ extern "C"
         d.neighbors = {nbr.data(), nbr.size()};
 
         // --- computeForces
-        sph::findNeighborsSph(s->x, s->y, s->z, s->h, 0u, unsigned(n), box, view, d.ng0, d.ngmax, nbr.data(),
-                              s->nc);
+        // findNeighborsSph addresses a target's list as neighbors + i * ngmax with i a 32-bit LocalIndex
+        // (find_neighbors.hpp:26): past 2^32 / ngmax targets (28.6M at ngmax 150) the offset wraps.  A reference run
+        // holds that many particles only on several ranks, each calling it over its own range with its own list
+        // (findNeighborsSfc, :54-55); the harness does the same per chunk of 2^24 targets on one rank (Sedov -n 400,
+        // 64M particles).  Every target's search is independent of the others, so the lists, nc and h are those of
+        // one call wherever it does not wrap.
+        for (size_t f = 0; f < n; f += size_t(1) << 24)
+        {
+            const size_t l = std::min(n, f + (size_t(1) << 24));
+            sph::findNeighborsSph(s->x, s->y, s->z, s->h, cstone::LocalIndex(f), cstone::LocalIndex(l), box, view,
+                                  d.ng0, d.ngmax, nbr.data() + f * size_t(d.ngmax), s->nc + f);
+        }
         if (p->prop == 1)
         {
             // HydroProp::computeForces (std_hydro.hpp:124-166): minDtRho is never set there

@@ -81,6 +81,14 @@ public:
     {
         return ncclAllReduce(dev, dev, count, ncclFloat64, ncclSum, comm_, s) == ncclSuccess;
     }
+    bool allreduceMinU32(uint32_t* dev, size_t count, hipStream_t s) override
+    {
+        return ncclAllReduce(dev, dev, count, ncclUint32, ncclMin, comm_, s) == ncclSuccess;
+    }
+    bool allreduceMaxU32(uint32_t* dev, size_t count, hipStream_t s) override
+    {
+        return ncclAllReduce(dev, dev, count, ncclUint32, ncclMax, comm_, s) == ncclSuccess;
+    }
 
 private:
     int          rank_, size_;
@@ -144,6 +152,8 @@ public:
     bool allreduceSumU32(uint32_t* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 4, 0, s); }
     bool allreduceMinF64(double* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 8, 1, s); }
     bool allreduceSumF64(double* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 8, 2, s); }
+    bool allreduceMinU32(uint32_t* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 4, 3, s); }
+    bool allreduceMaxU32(uint32_t* dev, size_t count, hipStream_t s) override { return allreduce(dev, count, 4, 4, s); }
 
 private:
     int               rank_, size_;
@@ -208,6 +218,8 @@ extern "C"
             case 0: ok = c->t->allreduceSumU32(static_cast<uint32_t*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
             case 1: ok = c->t->allreduceMinF64(static_cast<double*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
             case 2: ok = c->t->allreduceSumF64(static_cast<double*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
+            case 3: ok = c->t->allreduceMinU32(static_cast<uint32_t*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
+            case 4: ok = c->t->allreduceMaxU32(static_cast<uint32_t*>(dev), count, static_cast<hipStream_t>(hipStream)); break;
             default: return SX_ERR_ARG;
         }
         return ok ? SX_OK : SX_ERR_HIP;

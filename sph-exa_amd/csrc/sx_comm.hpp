@@ -6,7 +6,8 @@
  * sph/ts_global.hpp:106) with two operations on device buffers:
  *   alltoallv  -- every rank sends sendBytes[q] from send+sendOff[q] to rank q, receiving recvBytes[q] at
  *                 recv+recvOff[q] (recv may be a field array: halos land in place, no unpack pass);
- *   allreduce  -- u32 sum (global key histogram) and f64 min (time-step).
+ *   allreduce  -- u32 sum (global key histogram), f64 min (time-step), u32 min/max (displacement grid of the skin
+ *                 lists).
  * Backends: RCCL (one communicator per node, grouped ncclSend/ncclRecv per peer over xGMI, collectives on device
  * buffers, all on the compute stream) and a host-staged backend that calls back into the caller (used with
  * torch.distributed/gloo to run several ranks on one GPU in the tests).
@@ -32,6 +33,9 @@ public:
     virtual bool allreduceSumU32(uint32_t* dev, size_t count, hipStream_t s)                  = 0;
     virtual bool allreduceMinF64(double* dev, size_t count, hipStream_t s)                    = 0;
     virtual bool allreduceSumF64(double* dev, size_t count, hipStream_t s)                    = 0;
+    //! u32 min / max (the skin lists' displacement grid: per cell the component ranges of every rank's particles)
+    virtual bool allreduceMinU32(uint32_t* dev, size_t count, hipStream_t s)                  = 0;
+    virtual bool allreduceMaxU32(uint32_t* dev, size_t count, hipStream_t s)                  = 0;
 
     //! host-count convenience: exchange one u64 per peer (counts), synchronous
     bool exchangeCounts(const std::vector<uint64_t>& send, std::vector<uint64_t>& recv, hipStream_t s, uint64_t* devBuf);

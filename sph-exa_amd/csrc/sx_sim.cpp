@@ -323,6 +323,27 @@ __global__ void chunkCoverKernel(const double* x, const double* y, const double*
     if (out) atomicOr(flag, 1u);
 }
 
+/*! several ranks, a reuse step: the clusters list[1 .. list[0]] were searched again this step (a skin rebuilt from the
+ *  current positions, or the exact search), over the locals and the halos of the last build only.  That search saw
+ *  every particle within a target's radius only if the target's sphere lies inside its chunk's request box of that
+ *  build: radius 2 r_i scale, r = hb (rebuilt skins: the h of their build, scale 1 + s) or h (exact search, scale 1).
+ *  One workgroup per listed cluster; flag |= 1 when some sphere leaves its box (then every rank redoes the step from
+ *  a full sync) */
+__global__ void coverListKernel(const uint32_t* list, uint32_t maxList, uint32_t first, uint32_t last, const double* x,
+                                const double* y, const double* z, const float* r, float scale, const ReqBox* boxes,
+                                DevBox box, double qmargin, unsigned* flag)
+{
+    const uint32_t k = blockIdx.x;
+    if (k >= min(list[0], maxList)) return;
+    const uint32_t i = first + list[1 + k] * kCluster + threadIdx.x;
+    if (i >= last) return;
+    const ReqBox& b = boxes[(i - first) / kChunk];
+    const double  R = 2.0 * (double)r[i] * (double)scale * (1.0 + 1e-6) + qmargin;
+    const bool    out = fabs(foldPbc(x[i] - b.c[0], box, 0)) + R > b.s[0] ||
+                     fabs(foldPbc(y[i] - b.c[1], box, 1)) + R > b.s[1] || fabs(foldPbc(z[i] - b.c[2], box, 2)) + R > b.s[2];
+    if (out) atomicOr(flag, 1u);
+}
+
 /*! one wave per peer request box: traverse the local tree, mark local particles inside the box (minimum image)
  *  for the box owner.  mark: one bit per rank (<= 64 ranks). */
 __global__ __launch_bounds__(256) void markHalosKernel(const ReqBox* boxes, int numBoxes, const int32_t* childOffsets,
@@ -1535,9 +1556,14 @@ bool periodicGravity(const sx_sim* s) { return s->p.g != 0.0 && s->box.bnd[0] ==
 //! Not with periodic self-gravity: between syncs a particle that crossed a periodic face is wrapped to the far side of
 //! the box while it stays in its old leaf, so the leaf's multipole (raw coordinates) would spread across the box
 //! while its refreshed MAC box (minimum image) covers only the old cell -- every step syncs there
+//! Several ranks (without self-gravity): the halo set of a full build is requested with the skin radius, a reuse step
+//! refreshes the halos' x, y, z, h, m over the build's send lists and reduces the displacement grid over all ranks, and
+//! every decision about builds is taken on all ranks together (skinHaloRefresh, the decision exchange in sx_sim_step).
+//! Multi-rank self-gravity would traverse near/far trees whose request boxes drift away from the locals: not used.
 bool skinUsable(const sx_sim* s)
 {
-    return s->skin.factor > 0.0f && !(s->comm && s->comm->size() > 1) && s->p.propagator != 2 &&
+    const bool dist = s->comm && s->comm->size() > 1;
+    return s->skin.factor > 0.0f && !(dist && s->p.g != 0.0) && s->p.propagator != 2 &&
            NbLists::localPossible(s->p.ngmax) && !periodicGravity(s);
 }
 
@@ -1597,18 +1623,28 @@ bool skinParticleBuffers(sx_sim* s, PosArgs& q, hipStream_t st)
 
 constexpr int kSkinResync = 1000; //!< skinSearch: redo this step's search from a full sync (not an error code)
 
+//! a step's skin search on this rank: clusters, stale ones (rebuilt at once or sent to the exact search directly),
+//! those rebuilt, and those that took the exact search
+struct SkinCounts
+{
+    uint32_t clusters{0}, stale{0}, rebuilt{0}, exact{0};
+};
+
 /*! The step's neighbor search through skin lists (sx_skin.hpp).  A full build (after a full sync) builds every
  *  cluster's skin and filters it; a reuse step only filters.  Stale clusters are rebuilt at once on node boxes refreshed
  *  from the current positions (reuse steps) and filtered; clusters stale again take the exact search (on a reuse step
  *  over the refreshed boxes: should it outgrow a capacity there, kSkinResync makes the caller restore h and redo the
  *  step's search from a full sync).  na: the step's search arguments (exact lists, h, nc, tree).  One host read of the
  *  stale count, two or three when some cluster is stale. */
-int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* xmOut, RecT* rtXm)
+int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* xmOut, RecT* rtXm, SkinCounts& out)
 {
     auto&          K   = s->skin;
     const uint32_t ncl = (na.numGroups + kClusterWaves - 1) / kClusterWaves;
+    out                = SkinCounts{};
+    out.clusters       = ncl;
+    if (!reuse) K.built = K.cur; // (also with no local cluster: every rank's skin state stays the same)
     if (!ncl) return SX_OK;
-    if (!reuse) K.built = K.cur, K.ngmaxS = skinCapacity(s->p.ngmax, K.built);
+    if (!reuse) K.ngmaxS = skinCapacity(s->p.ngmax, K.built);
     const size_t G    = kSkinGridN;
     float*       rel  = s->mem.get<float>("skin.rel", s->cap);
     float*       dx   = s->mem.get<float>("skin.dx", s->cap);
@@ -1674,6 +1710,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     SIM_HIP(hipStreamSynchronize(st));
     const uint32_t n1 = hl[0], nd = hl[1];
     uint32_t       n2 = nd;
+    out.rebuilt = n1, out.stale = n1 + nd, out.exact = nd;
     NsArgs         x  = na; // the exact search, for clusters whose h iteration outgrows even a fresh skin
     // subset searches of a reuse step run the large build directly: on the refreshed (overlapping) boxes many of the
     // few clusters overflow the compact one, whose launch then only adds a tail (Noh -n 300: 20.4 -> 20.1 ms/step)
@@ -1704,6 +1741,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         SIM_HIP(hipStreamSynchronize(st));
         n2 = hl[2];
     }
+    out.exact = n2;
     {
         if (n2)
         {
@@ -1733,8 +1771,16 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         fprintf(stderr, "skin: reuse %d s %.3f clusters %u stale %u exact %u flags 0x%x mode %d\n", (int)reuse,
                 K.built, ncl, n1 + nd, n2, f, s->nsPolicy.mode);
     }
-    K.lastStale = n1 + nd, K.lastExact = n2;
-    K.staleClusters += n1 + nd, K.exactClusters += n2;
+    return SX_OK;
+}
+
+/*! the skin's bookkeeping after a step's search: statistics of this rank, and the build decisions from the stale share
+ *  of all ranks (staleAll of clustersAll: with several ranks the sums over every rank, so that every rank takes the
+ *  same decisions and the next step is a full sync + build on all of them or on none) */
+void skinDecide(SkinState& K, bool reuse, const SkinCounts& c, uint64_t staleAll, uint64_t clustersAll)
+{
+    K.lastStale = c.stale, K.lastExact = c.exact;
+    K.staleClusters += c.stale, K.exactClusters += c.exact;
     if (reuse)
     {
         K.reuseSteps++;
@@ -1750,7 +1796,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     // many clusters rebuilt one by one: the next step syncs (SFC order restored) and builds them all at once.  A
     // stale-heavy step costs about a build; a skin with fewer than two clean reuse steps since its build saved
     // nothing, so the next steps search without it (backoff, doubling up to 32 steps with every such skin)
-    const bool clean = (double)(n1 + nd) <= K.staleLimit * ncl;
+    const bool clean = (double)staleAll <= K.staleLimit * (double)clustersAll;
     if (!reuse) K.cleanSinceBuild = 0;
     else if (clean) K.cleanSinceBuild++;
     if (!clean)
@@ -1759,6 +1805,21 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         if (!reuse || K.cleanSinceBuild < 2) skinTooThin(K);
     }
     if (clean && K.cleanSinceBuild >= 2) K.backoffLen = 4;
+}
+
+//! a reuse step with several ranks: the halos of the last build get their owners' current x, y, z, h, m over the
+//! build's send lists (the particles stay where they are: no exchange to the SFC owners until the next build), and
+//! the displacement grid of the last position update becomes the grid of every rank's particles (u32 min / max of the
+//! ordered-float component ranges): a particle that was no halo at the build can only reach a target's 2h sphere
+//! through the region around its cluster, where its steps now count in the filter's drift bound (sx_skin.hpp)
+int skinHaloRefresh(sx_sim* s, hipStream_t st)
+{
+    if (int e = haloExchange(s, {{s->x, 8}, {s->y, 8}, {s->z, 8}, {s->h, 4}, {s->m, 4}}, st)) return e;
+    const size_t nc    = (size_t)kSkinGridN * kSkinGridN * kSkinGridN;
+    uint32_t*    cells = s->mem.get<uint32_t>("skin.cells", kGridWords * nc);
+    if (!cells) return SX_ERR_NOMEM;
+    SIM_COMM(s->comm->allreduceMinU32(cells, 3 * nc, st));
+    SIM_COMM(s->comm->allreduceMaxU32(cells + 3 * nc, 3 * nc, st));
     return SX_OK;
 }
 
@@ -2141,7 +2202,7 @@ extern "C"
 
         // skin lists (sx_skin.hpp): a reuse step keeps the order and tree of the last full build and filters the
         // skin lists instead of syncing and searching
-        bool skinOn = !dist && skinUsable(s);
+        bool skinOn = skinUsable(s);
         if (skinOn && s->skin.backoff > 0)
         {
             s->skin.backoff--;
@@ -2159,20 +2220,23 @@ extern "C"
         float* h0     = dist ? s->work.get<float>("h0", s->cap) : nullptr;
         double margin = kHaloMargin;
         NsArgs na{};
+        bool   restoreH0 = false; // a retry with a larger halo margin: the locals' h as before the last search
+        SkinCounts skc{};
         for (int attempt = 0;; ++attempt)
         {
-            if (dist)
+            // a skin build requests its halos within the skin radius: the build's lists see every particle within
+            // 2 h (1 + s) of a target (several ranks)
+            const double skinMargin = skinOn ? 1.0 + (double)s->skin.cur : 1.0;
+            if (dist && reuse)
             {
-                if (attempt == 0)
-                {
-                    if (int e = distributedSync(s, st, margin)) return e;
-                }
-                else
-                {
-                    // restore pre-iteration h of the locals, then rediscover halos with a larger margin
+                if (int e = skinHaloRefresh(s, st)) return e;
+            }
+            else if (dist)
+            {
+                // restore pre-iteration h of the locals, then rediscover halos with a larger margin
+                if (restoreH0)
                     SIM_HIP(hipMemcpyAsync(s->h + s->first, h0, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
-                    if (int e = distributedSync(s, st, margin)) return e;
-                }
+                if (int e = distributedSync(s, st, margin * skinMargin)) return e;
                 SIM_HIP(hipMemcpyAsync(h0, s->h + s->first, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
             }
             else if (!reuse && !synced)
@@ -2239,24 +2303,31 @@ extern "C"
             SIM_HIP(hipMemsetAsync(s->stats, 0, kStatsWords * 4, st));
             resetScalarsKernel<<<1, 1, 0, st>>>(s->sc);
             SIM_HIP(hipEventRecord(s->kev[0], st));
+            bool resync = false; // this rank's reuse step must be redone from a full sync + build
             if (skinOn)
             {
                 // the fast variant's XMass (or the std density's xmass pass) rides on the filter's final pass
                 const bool fastXm = !sx_ctx_exact_internal(s->ctx);
                 float*     xmOut  = fastXm ? (s->p.propagator == 1 ? s->rho : s->xm) : nullptr;
                 RecT*      rtXm   = (fastXm && s->p.propagator != 1 && H.clusterLists) ? s->rt : nullptr;
-                const int e = skinSearch(s, na, reuse, st, xmOut, rtXm);
-                if (e == kSkinResync)
+                const int e = skinSearch(s, na, reuse, st, xmOut, rtXm, skc);
+                resync      = e == kSkinResync;
+                if (e && !resync) return e;
+                if (!dist)
                 {
-                    // h as before the filter, then this step's search again after a full sync + build
-                    SIM_HIP(hipMemcpyAsync(s->h + s->first, hReuse, (s->last - s->first) * 4, hipMemcpyDeviceToDevice,
-                                           st));
-                    s->skin.resyncs++;
-                    if (s->skin.cleanSinceBuild < 2) skinTooThin(s->skin);
-                    reuse = false;
-                    continue;
+                    if (resync)
+                    {
+                        // h as before the filter, then this step's search again after a full sync + build
+                        SIM_HIP(hipMemcpyAsync(s->h + s->first, hReuse, (s->last - s->first) * 4,
+                                               hipMemcpyDeviceToDevice, st));
+                        s->skin.resyncs++;
+                        if (s->skin.cleanSinceBuild < 2) skinTooThin(s->skin);
+                        reuse = false;
+                        continue;
+                    }
+                    skinDecide(s->skin, reuse, skc, skc.stale, skc.clusters);
+                    s->skin.stepClusters = skc.clusters;
                 }
-                if (e) return e;
             }
             else
             {
@@ -2267,17 +2338,41 @@ extern "C"
             SIM_HIP(hipMemcpyAsync(s->statsHost, s->stats, kStatsWords * 4, hipMemcpyDeviceToHost, st));
             if (s->evStats) SIM_HIP(hipEventRecord(s->evStats, st));
             if (!dist) break;
-            // halo sufficiency: every local particle's final h within its chunk's request margin
+            // halo sufficiency: every local particle's final h within its chunk's request margin (a build or a plain
+            // search); on a reuse step, the spheres of the clusters searched again this step (coverListKernel).
+            // One exchange of five words carries every decision the ranks take together: [0] halo margin too small,
+            // [1] the reuse step must be redone from a full sync + build, [2] stale clusters, [3] clusters, [4] clusters
+            // whose skin would not survive another such drift (the filter's stats[13])
             const size_t nl  = s->last - s->first;
-            auto*        flg = s->work.get<unsigned>("dom.hflag", 1);
-            SIM_HIP(hipMemsetAsync(flg, 0, 4, st));
-            if (nl)
-                chunkCheckKernel<<<grid(nl), 256, 0, st>>>(s->h + s->first, nl, s->work.get<ReqBox>("dom.mybox", 1),
-                                                         margin, flg);
+            auto*        flg = s->work.get<unsigned>("dom.hflag", 5);
+            uint32_t*    dec = s->work.pinned<uint32_t>("dom.dech", 8);
+            if (!flg || !dec) return SX_ERR_NOMEM;
+            dec[0] = 0, dec[1] = resync ? 1u : 0u, dec[2] = skc.stale, dec[3] = skc.clusters, dec[4] = 0;
+            SIM_HIP(hipMemcpyAsync(flg, dec, 5 * 4, hipMemcpyHostToDevice, st));
+            const ReqBox* myBoxes = s->work.get<ReqBox>("dom.mybox", 1);
+            if (!reuse)
+            {
+                if (nl)
+                    chunkCheckKernel<<<grid(nl), 256, 0, st>>>(s->h + s->first, nl, myBoxes, margin * skinMargin, flg);
+            }
+            else
+            {
+                const double qm = quantMargin(s->dbox);
+                if (skc.rebuilt)
+                    coverListKernel<<<skc.rebuilt, kCluster, 0, st>>>(
+                        s->mem.get<uint32_t>("skin.l1", 1), skc.rebuilt, (uint32_t)s->first, (uint32_t)s->last, s->x,
+                        s->y, s->z, s->mem.get<float>("skin.hb", 1), 1.0f + s->skin.built, myBoxes, s->dbox, qm,
+                        flg + 1);
+                if (skc.exact)
+                    coverListKernel<<<skc.exact, kCluster, 0, st>>>(s->mem.get<uint32_t>("skin.l2", 1), skc.exact,
+                                                                    (uint32_t)s->first, (uint32_t)s->last, s->x, s->y,
+                                                                    s->z, s->h, 1.0f, myBoxes, s->dbox, qm, flg + 1);
+            }
+            if (skinOn) SIM_HIP(hipMemcpyAsync(flg + 4, s->stats + 13, 4, hipMemcpyDeviceToDevice, st));
             unsigned hf = 0;
             // the retry decision must be global: a rank redoing the sync alone would deadlock the collectives
-            SIM_COMM(s->comm->allreduceSumU32(flg, 1, st));
-            SIM_HIP(hipMemcpyAsync(s->statsHost + 3, flg, 4, hipMemcpyDeviceToHost, st));
+            SIM_COMM(s->comm->allreduceSumU32(flg, 5, st));
+            SIM_HIP(hipMemcpyAsync(dec, flg, 5 * 4, hipMemcpyDeviceToHost, st));
             if (overlapping(s, H))
             {
                 const uint32_t ncl = (uint32_t)((nl + kCluster - 1) / kCluster);
@@ -2294,11 +2389,34 @@ extern "C"
             SIM_HIP(hipStreamSynchronize(st));
             if (syncErrFailed(s)) return SX_ERR_TRAVERSAL;
             if (overlapping(s, H)) s->nInterior = s->clsHost[0], s->nBoundary = s->clsHost[1];
-            hf = s->statsHost[3];
-            if (!hf) break;
-            if (attempt >= 3) return SX_ERR_NOT_CONVERGED;
-            margin *= 1.5;
-            s->haloRetries++;
+            hf                = dec[0];
+            s->statsHost[3]   = hf;
+            if (skinOn && dec[1])
+            {
+                // some rank's reuse step cannot stand (a sphere searched again outside the build's halo region, or
+                // the exact search over capacity): every rank restores h and redoes the step from a full sync + build
+                SIM_HIP(hipMemcpyAsync(s->h + s->first, hReuse, (s->last - s->first) * 4, hipMemcpyDeviceToDevice, st));
+                s->skin.resyncs++;
+                if (s->skin.cleanSinceBuild < 2) skinTooThin(s->skin);
+                reuse     = false;
+                restoreH0 = false;
+                continue;
+            }
+            if (hf)
+            {
+                if (attempt >= 3) return SX_ERR_NOT_CONVERGED;
+                margin *= 1.5;
+                restoreH0 = true;
+                s->haloRetries++;
+                continue;
+            }
+            if (skinOn)
+            {
+                skinDecide(s->skin, reuse, skc, dec[2], dec[3]);
+                s->skin.stepClusters = dec[3];
+                s->skin.stepS13      = dec[4];
+            }
+            break;
         }
         SIM_HIP(hipEventRecord(s->ev[ev++], st));
 
@@ -2599,9 +2717,10 @@ extern "C"
         if (reuse && s->skin.cleanSinceBuild <= 1 && !s->skin.forceBuild)
         {
             // the first clean step after a build, but most clusters would not survive another such drift: the skin
-            // cannot outlast two steps; stop using it now rather than after a stale-heavy step
-            const uint32_t ncl = (uint32_t)((s->last - s->first + kCluster - 1) / kCluster);
-            if ((double)s->statsHost[13] > s->skin.staleLimit * ncl) skinTooThin(s->skin);
+            // cannot outlast two steps; stop using it now rather than after a stale-heavy step (several ranks: the
+            // counts of all ranks, exchanged with the step's decisions)
+            const double s13 = dist ? (double)s->skin.stepS13 : (double)s->statsHost[13];
+            if (s13 > s->skin.staleLimit * (double)s->skin.stepClusters) skinTooThin(s->skin);
         }
         s->lastStats.build         = s->nsPolicy.lastBuild;
         if (s->statsHost[0] & 1u)

@@ -86,6 +86,8 @@ struct SkinState
     // the exact search on the drifted tree's boxes could outgrow its capacities)
     uint64_t resyncs{0};
     uint32_t lastStale{0}, lastExact{0};
+    // this step's clusters and stats[13] count (over all ranks with several; the "outlast two steps" test)
+    uint64_t stepClusters{0}, stepS13{0};
     // this step: the filter computed XMass of every cluster but the exact-search ones (exactList[1 ..], lastExact)
     bool      xmFused{false};
     uint32_t* exactList{nullptr};

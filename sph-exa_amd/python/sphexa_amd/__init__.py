@@ -459,10 +459,10 @@ class Comm:
 
             def allreduce(user, buf, count, op):
                 try:
-                    if op == 0:
+                    if op in (0, 3, 4):  # u32 sum, min, max
                         a = np.ctypeslib.as_array((C.c_uint32 * count).from_address(buf))
                         t = torch.from_numpy(a.astype(np.int64))
-                        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                        dist.all_reduce(t, op={0: dist.ReduceOp.SUM, 3: dist.ReduceOp.MIN, 4: dist.ReduceOp.MAX}[op])
                         a[:] = t.numpy().astype(np.uint32)
                     else:
                         a = np.ctypeslib.as_array((C.c_double * count).from_address(buf))
@@ -489,7 +489,7 @@ class Comm:
         if rc != SX_OK:
             raise SxError(f"sx_comm_alltoallv failed: {rc}")
 
-    ALLREDUCE_OPS = {"sum_u32": 0, "min_f64": 1, "sum_f64": 2}
+    ALLREDUCE_OPS = {"sum_u32": 0, "min_f64": 1, "sum_f64": 2, "min_u32": 3, "max_u32": 4}
 
     def allreduce(self, dev, count, op, stream=None):
         """sx_comm_allreduce in place on a device buffer: op 'sum_u32', 'min_f64' or 'sum_f64'"""

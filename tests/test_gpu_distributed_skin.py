@@ -1,0 +1,70 @@
+"""Skin lists with several ranks: filter-served steps between full builds on an SFC decomposition.
+
+A full build requests its halos within the skin radius 2 h (1 + s); a reuse step keeps the decomposition, refreshes
+the halos' x, y, z, h, m over the build's send lists and reduces the displacement grid over all ranks; the decision to
+rebuild, and to redo a step whose re-searched spheres left the build's halo region, is taken by every rank together.
+The step's neighbor search result must not change: after every step the nc and h of each particle (by id, merged over
+the ranks) equal those of a fresh distributed sync + search of the same state (tests/dist_skin_worker.py: a second
+simulation with the skin off, handed the state before every step).  nc counts every neighbor within 2h, and the filter
+only ever tests candidates with the reference's exact criterion, so equal nc means equal neighbor sets.  The fields the
+pair kernels produce agree within float summation order (the two unions order the neighbors differently), and every
+rank takes the same build decisions (identical skin statistics).  Host-staged transport, every rank on the one GPU.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SKIN = ["builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps", "resyncs"]
+
+
+def run(tmp_path, nproc, port, ic, side, steps, skin=0.08, max_reuse=24):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tests", "dist_skin_worker.py"), "--out",
+           str(tmp_path), "--ic", ic, "--side", str(side), "--steps", str(steps), "--skin", str(skin),
+           "--max-reuse", str(max_reuse)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return [dict(np.load(os.path.join(tmp_path, f"rank{q}.npz"))) for q in range(nproc)]
+
+
+def merged(ranks, s, tag, keys):
+    out = {k: np.concatenate([d[f"s{s}_{tag}_{k}"] for d in ranks]) for k in keys}
+    o = np.argsort(out["id"])
+    return {k: v[o] for k, v in out.items()}
+
+
+@pytest.mark.parametrize("nproc,port,ic,side,steps,skin", [(2, 29651, "sedov", 20, 10, 0.08),
+                                                           (3, 29652, "sedov", 20, 8, 0.08),
+                                                           (2, 29653, "noh", 20, 8, 0.08),
+                                                           (3, 29654, "noh", 22, 8, 0.3),
+                                                           (8, 29655, "sedov", 24, 6, 0.08)])
+def test_distributed_skin_equals_fresh_search(tmp_path, nproc, port, ic, side, steps, skin):
+    ranks = run(tmp_path, nproc, port, ic, side, steps, skin)
+    keys = ["id", "nc", "h", "xm", "kx", "divv", "alpha", "ax", "ay", "az", "du", "x", "vx"]
+    n = None
+    for s in range(steps):
+        ga, gb = merged(ranks, s, "a", keys), merged(ranks, s, "b", keys)
+        n = ga["id"].size
+        assert np.array_equal(ga["id"], gb["id"]) and np.array_equal(ga["id"], np.arange(n))
+        bad = np.nonzero(ga["nc"] != gb["nc"])[0]
+        assert bad.size == 0, (ic, nproc, s, bad.size, ga["nc"][bad[:8]], gb["nc"][bad[:8]])
+        assert np.array_equal(ga["h"], gb["h"]), (ic, nproc, s)
+        for k in ("xm", "kx", "divv", "alpha", "ax", "ay", "az", "du", "x", "vx"):
+            x, y = ga[k].astype(np.float64), gb[k].astype(np.float64)
+            tol = 2e-4 * np.abs(y) + 2e-5 * np.max(np.abs(y))
+            assert np.all(np.abs(x - y) <= tol), (ic, nproc, s, k, float(np.max(np.abs(x - y) / (np.abs(y) + 1e-30))))
+        dts = {float(d[f"s{s}_a_dt"][0]) for d in ranks}
+        assert len(dts) == 1
+        # every rank takes the same build decisions
+        sk = np.array([d[f"s{s}_skin"] for d in ranks])
+        for col in (0, 1, 4, 5, 6, 7):  # builds, reuse steps, plain steps, resyncs, skin factor, next factor
+            assert np.all(sk[:, col] == sk[0, col]), (s, col, sk[:, col])
+    last = np.array([d[f"s{steps - 1}_skin"] for d in ranks])
+    print(ic, nproc, side, skin, dict(zip(SKIN, last[0][:6])), "stale per rank", last[:, 2])
+    assert last[0][SKIN.index("reuse_steps")] > 0, last[0]

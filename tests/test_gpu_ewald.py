@@ -230,7 +230,7 @@ def test_sim_periodic_gravity_crossing_particles_skin_off(ctx):
     """with periodic self-gravity every step syncs (no skin reuse step), so a particle that crossed a periodic
     face is in the leaf of its wrapped position when the multipoles are formed.  A medium drifting through the box
     (particles cross the faces every few steps) with the default skin gives the same accelerations and potential,
-    bit for bit by id, as the same run with the skin off"""
+    bit for bit by id, and the same potential to rounding, as the same run with the skin off"""
     import pyoracle as po
     out = {}
     for skin in (0.08, 0.0):
@@ -264,4 +264,4 @@ def test_sim_periodic_gravity_crossing_particles_skin_off(ctx):
     for (a, ea), (b, eb) in zip(out[0.08], out[0.0]):
         for k in ("ax", "ay", "az"):
             assert np.array_equal(a[k], b[k]), k
-        assert ea == eb
+        assert abs(ea - eb) <= 1e-12 * abs(eb)  # the Ewald energy is summed with device atomics (order varies)
