@@ -356,10 +356,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # skin lists (one rank): the timed window starts with a full sync + build of every cluster's skin, so `value` and
-    # `ms_per_step` carry at least their share of the builds that come every max_reuse steps at the latest (a window
-    # shorter than max_reuse carries more than its share: 1 build in K steps, against 1 in max_reuse)
-    skin_window = args.skin > 0 and world == 1 and not args.no_build_step
+    # skin lists: the timed window starts with a full sync + build of every cluster's skin (on every rank: the build
+    # decisions are collective), so `value` and `ms_per_step` carry at least their share of the builds that come every
+    # max_reuse steps at the latest (a window shorter than max_reuse carries more than its share: 1 build in K steps,
+    # against 1 in max_reuse).  Several ranks with self-gravity sync + search every step (sx_sim.cpp skinUsable)
+    skin_window = args.skin > 0 and not args.no_build_step
     if skin_window:
         sim.rebuild_lists()
     ctx.sync()
@@ -390,6 +391,12 @@ def main():
             for k, v in sim.skin_stats().items()}  # the timed steps'
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
+    if dist is not None:  # per-step times: the slowest rank's
+        import torch
+
+        t = torch.tensor(step_s, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_s = [float(v) for v in t]
     if skin_window and args.steps > 1 and skin.get("builds", 0) >= 1:
         # the window's first step was the full sync + build, the others (up to max_reuse) filter-served
         R = max(1, int(args.skin_reuse))
@@ -511,8 +518,10 @@ def main():
                       else {}),
                    "kernels": "exact (no FMA)" if args.exact else "fast (FMA)",
                    "neighbor_skin": {"initial_factor": args.skin, "max_reuse": args.skin_reuse,
-                                     "note": "one rank: steps between full builds filter the last "
-                                             "build's lists within 2h(1+s) (sx_skin.hpp); same neighbor sets, nc, h",
+                                     "note": "steps between full builds filter the last build's lists within "
+                                             "2h(1+s) (sx_skin.hpp; several ranks: halos of the build refreshed, "
+                                             "displacement grid all-reduced, not with self-gravity); same neighbor "
+                                             "sets, nc, h",
                                      **skin}},
         "roofline": roofline,
         "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_ms.items()

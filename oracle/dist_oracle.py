@@ -423,3 +423,122 @@ def distributed_gravity(d, full, G, theta):
     stats = {"halos": nlow + nh, "far_cells": int(far.shape[0]), "remote_cells": int(sum(x.shape[0] for x in remote))
              - mine.shape[0]}
     return acc, eg, stats
+
+
+# ---- skin lists on several ranks: the argument behind reuse steps (sx_skin.hpp, DESIGN 4c, sx_sim.cpp skinHaloRefresh)
+
+SKIN_GRID_N = 16  # displacement-grid cells per axis here (the GPU's 64^3; any resolution gives a valid bound)
+
+
+def _grid_cells(pos, box, n):
+    """cell index per particle of an n^3 grid over the box (gridCell: floor, periodic axes wrapped, others clamped)"""
+    idx = []
+    for k in range(3):
+        lo, L = box.lim[2 * k], box.lim[2 * k + 1] - box.lim[2 * k]
+        c = np.floor((pos[:, k] - lo) * (n / L)).astype(np.int64)
+        idx.append(np.mod(c, n) if box.bnd[k] == 1 else np.clip(c, 0, n - 1))
+    return idx
+
+
+def _mi_dist2(a, b, box):
+    d2 = 0.0
+    for k in range(3):
+        d2 = d2 + _fold(a[..., k] - b[..., k], box, k) ** 2
+    return d2
+
+
+def skin_premise(d, full, glob_pos0, h_of, s, disps, global_grid=True):
+    """Restatement of the multi-rank skin argument on this rank (test infrastructure).
+
+    Build: the halos of `full` were requested with the skin radius (d._discover(..., HALO_MARGIN * (1 + s))); every
+    local target a gets its skin list S_a = the particles of locals + halos within R_a = 2 h_a (1 + s).  Returned check
+    1: S_a equals the global truth within R_a (the halo set of the build holds every skin neighbour).
+    Reuse steps t = 1, 2, ...: every particle moves by disps[t-1] (rows by id, the same on every rank); this rank
+    scatters its LOCALS' displacements into a grid of per-cell component ranges (cells of the end-of-step positions),
+    reduced over all ranks with min / max when global_grid (the GPU's all-reduce of the grid) or left local; per
+    cluster of 256 consecutive locals, with u = the displacement of its first particle, the filter's bound
+    2 h_a + d_a + A_C <= R_a (1 - 2^-16) (d_a = sum_t |d_a(t) - u(t)|, A_C = sum_t max over the cells around the
+    cluster's targets grown by max R of the largest |d - u|).  Check 2: every target of every cluster the bound admits
+    has all its current neighbours (global truth within 2 h_a, minimum image) in S_a.
+    Returns (skin_mismatch, admitted clusters per step, violations per step)."""
+    import torch
+
+    dist = _dist()
+    box, f, l = d.box, d.first, d.last
+    d.halo_exchange(["id"])  # the halos' ids (the sync's setup exchange carries x, y, z, h, m only)
+    ids_full = full.id.astype(np.int64)
+    loc = ids_full[f:l]
+    n_glob = glob_pos0.shape[0]
+    # skin lists at the build, by id, over locals + halos; the truth over every particle
+    R = 2.0 * h_of[loc] * (1.0 + s)
+    pf = glob_pos0[ids_full]
+    skin, mismatch = [], 0
+    for q, a in enumerate(loc):
+        d2 = _mi_dist2(pf, glob_pos0[a][None, :], box)
+        sa = set(ids_full[(d2 < R[q] ** 2)].tolist()) - {int(a)}
+        dg = _mi_dist2(glob_pos0, glob_pos0[a][None, :], box)
+        truth = set(np.nonzero(dg < R[q] ** 2)[0].tolist()) - {int(a)}
+        mismatch += sa != truth
+        skin.append(sa)
+    pos = glob_pos0.copy()
+    rel = np.zeros(len(loc))
+    ncl = (len(loc) + DistOracle.CLUSTER - 1) // DistOracle.CLUSTER
+    acc = np.zeros(ncl)
+    G = SKIN_GRID_N
+    admitted, violations = [], []
+    for disp in disps:
+        pos = pos + disp
+        for k in range(3):
+            if box.bnd[k] == 1:
+                lo, L = box.lim[2 * k], box.lim[2 * k + 1] - box.lim[2 * k]
+                pos[:, k] = lo + np.mod(pos[:, k] - lo, L)
+        # this rank's grid of its locals' displacements, reduced over the ranks
+        cx, cy, cz = _grid_cells(pos[loc], box, G)
+        cell = (cz * G + cy) * G + cx
+        lo_ = np.full((3, G ** 3), np.inf)
+        hi_ = np.full((3, G ** 3), -np.inf)
+        for k in range(3):
+            np.minimum.at(lo_[k], cell, disp[loc, k])
+            np.maximum.at(hi_[k], cell, disp[loc, k])
+        if global_grid:
+            tl, th = torch.from_numpy(lo_), torch.from_numpy(hi_)
+            dist.all_reduce(tl, op=dist.ReduceOp.MIN)
+            dist.all_reduce(th, op=dist.ReduceOp.MAX)
+            lo_, hi_ = tl.numpy(), th.numpy()
+        n_ok, n_bad = 0, 0
+        for c in range(ncl):
+            sel = np.arange(c * DistOracle.CLUSTER, min(len(loc), (c + 1) * DistOracle.CLUSTER))
+            ids = loc[sel]
+            u = disp[ids[0]]
+            rel[sel] += np.sqrt(np.sum((disp[ids] - u) ** 2, axis=1))
+            # cells around the targets (minimum image relative to the cluster's first particle) grown by max R
+            o = pos[ids[0]]
+            rr = np.stack([_fold(pos[ids, k] - o[k], box, k) for k in range(3)], axis=1)
+            Rm = float(R[sel].max())
+            ranges = []
+            for k in range(3):
+                lo, L = box.lim[2 * k], box.lim[2 * k + 1] - box.lim[2 * k]
+                k0 = int(np.floor((o[k] + rr[:, k].min() - Rm - lo) * (G / L)))
+                k1 = int(np.floor((o[k] + rr[:, k].max() + Rm - lo) * (G / L)))
+                if box.bnd[k] == 1:
+                    ranges.append(np.mod(np.arange(k0, k1 + 1), G) if k1 - k0 + 1 < G else np.arange(G))
+                else:
+                    ranges.append(np.arange(max(0, k0), min(G - 1, k1) + 1))
+            cz_, cy_, cx_ = np.meshgrid(ranges[2], ranges[1], ranges[0], indexing="ij")
+            cells = ((cz_ * G + cy_) * G + cx_).ravel()
+            g = 0.0
+            for q_ in cells:
+                if np.isfinite(lo_[0, q_]):
+                    e = [max(abs(lo_[k, q_] - u[k]), abs(hi_[k, q_] - u[k])) for k in range(3)]
+                    g = max(g, float(np.sqrt(e[0] ** 2 + e[1] ** 2 + e[2] ** 2)))
+            acc[c] += g
+            if not np.all(2.0 * h_of[ids] + rel[sel] + acc[c] <= R[sel] * (1.0 - 2.0 ** -16)):
+                continue
+            n_ok += 1
+            for q_, a in zip(sel, ids):
+                dg = _mi_dist2(pos, pos[a][None, :], box)
+                truth = set(np.nonzero(dg < (2.0 * h_of[a]) ** 2)[0].tolist()) - {int(a)}
+                n_bad += not truth <= skin[q_]
+        admitted.append(n_ok)
+        violations.append(n_bad)
+    return mismatch, admitted, violations

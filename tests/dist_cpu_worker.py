@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--gravity", action="store_true", help="only the multi-rank gravity of the IC (G = 1)")
     ap.add_argument("--overlap", action="store_true", help="interior clusters before each halo exchange")
     ap.add_argument("--converge-h", action="store_true", help="h after the first search's h iteration (pyoracle)")
+    ap.add_argument("--skin-premise", type=float, default=0.0,
+                    help="skin factor s: check the multi-rank skin argument (dist_oracle.skin_premise) over --steps "
+                         "displacement steps of a sliding + sheared lattice instead of running VE steps")
+    ap.add_argument("--premise-speed", type=float, default=0.04, help="slide per step in lattice spacings")
     args = ap.parse_args()
     import torch.distributed as dist
 
@@ -46,6 +50,31 @@ def main():
     local.minDt, local.minDt_m1 = st.minDt, st.minDt_m1
     d = do.DistOracle(po.load_oracle(), box, local, overlap=args.overlap)
     out = {}
+    if args.skin_premise > 0:
+        s = args.skin_premise
+        full = d._discover(d._exchange_particles(d._sort(d.local)), do.HALO_MARGIN * (1.0 + s))
+        pos0 = np.stack([st.x, st.y, st.z], axis=1).astype(np.float64)  # rows by id (the IC's ids are 0 .. n-1)
+        # a slab x > 0 sliding towards -x through the rest of the lattice (relative motion across rank boundaries),
+        # plus a shear: --premise-speed lattice spacings per step
+        V = args.premise_speed / args.side
+        disps, pos = [], pos0.copy()
+        for _ in range(args.steps):
+            dsp = np.zeros_like(pos)
+            dsp[:, 0] = -V * (pos[:, 0] > 0) + 0.3 * V * np.sin(2 * np.pi * pos[:, 1])
+            dsp[:, 1] = 0.2 * V * np.cos(2 * np.pi * pos[:, 2])
+            disps.append(dsp)
+            pos = pos + dsp
+            pos = -0.5 + np.mod(pos + 0.5, 1.0)
+        for tag, glob in (("global", True), ("local", False)):
+            mm, adm, vio = do.skin_premise(d, full, pos0, st.h.astype(np.float64), s, disps, global_grid=glob)
+            out[f"{tag}_mismatch"] = np.array([mm])
+            out[f"{tag}_admitted"] = np.array(adm)
+            out[f"{tag}_violations"] = np.array(vio)
+        out["halos"] = np.array([d.total - (d.last - d.first)])
+        np.savez(os.path.join(args.out, f"rank{args.rank}.npz"), **out)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if args.gravity:
         full = d._discover(d._exchange_particles(d._sort(d.local)), do.HALO_MARGIN)
         acc, eg, stats = do.distributed_gravity(d, full, 1.0, 0.5)

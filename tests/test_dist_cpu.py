@@ -174,3 +174,25 @@ def test_decomposed_gravity_matches_reference_two_ranks(tmp_path):
     assert np.median(err) < 1e-3 and np.max(err) < 1e-2, (np.median(err), np.max(err))
     eg = sum(float(d["egrav"][0]) for d in ranks)  # each rank's share of 0.5 sum G m phi
     assert abs(eg / fx["egrav_p2"][0] - 1) < 1e-3, (eg, fx["egrav_p2"][0])
+
+
+@pytest.mark.parametrize("nproc,side,speed", [(2, 14, 0.04), (3, 14, 0.04), (3, 14, 0.12)])
+def test_skin_premise_several_ranks(tmp_path, nproc, side, speed):
+    """the argument behind multi-rank skin lists (sx_sim.cpp skinHaloRefresh; dist_oracle.skin_premise), on gloo
+    ranks: halos requested with the skin radius hold every particle of every local's skin sphere, and with the
+    displacement grid reduced over all ranks every cluster the filter's drift bound admits has all its current
+    neighbours in its build-time skin lists -- also the particles of other ranks that were no halo at the build.
+    With a rank-local grid the bound admits clusters whose new neighbours slid in from another rank (the fast case:
+    the all-reduce is needed, not only sufficient)"""
+    ranks = run_ranks(tmp_path, nproc, side, 6, extra=("--skin-premise", "0.08", "--premise-speed", str(speed)))
+    adm = sum(int(r["global_admitted"].sum()) for r in ranks)
+    loc_vio = sum(int(r["local_violations"].sum()) for r in ranks)
+    print("admitted clusters (global grid)", [r["global_admitted"].tolist() for r in ranks],
+          "violations with a rank-local grid", [r["local_violations"].tolist() for r in ranks])
+    for r in ranks:
+        assert int(r["global_mismatch"][0]) == 0
+        assert int(r["global_violations"].sum()) == 0
+        assert int(r["halos"][0]) > 0
+    assert adm > 0
+    if speed > 0.1:
+        assert loc_vio > 0
