@@ -215,11 +215,24 @@ __device__ __forceinline__ void m2pRec(float (&acc)[4], float tx, float ty, floa
     const float Qry      = fmaf(r0, B.y, fmaf(r1, B.w, r2 * C.x));
     const float Qrz      = fmaf(r0, B.z, fmaf(r1, C.x, r2 * C.y));
     const float rQr      = fmaf(r0, Qrx, fmaf(r1, Qry, r2 * Qrz));
+#ifdef SX_M2P_V0
     const float rQrAndMonopole = (-2.5f * rQr * r_minus5 - A.w * r_minus1) * r_minus2;
     acc[0] -= fmaf(A.w, r_minus1, 0.5f * r_minus5 * rQr);
     acc[1] += fmaf(r_minus5, Qrx, rQrAndMonopole * r0);
     acc[2] += fmaf(r_minus5, Qry, rQrAndMonopole * r1);
     acc[3] += fmaf(r_minus5, Qrz, rQrAndMonopole * r2);
+#else
+    // the same expansion with the shared factors formed once (X = rQr r^-5, M0 r^-1) and every accumulation a fused
+    // multiply-add into the running sum: 35 instead of 41 VALU per interaction (the reference's operation order is
+    // kept by the exact variant, m2p(); this fast form agrees to float rounding)
+    const float X    = rQr * r_minus5;
+    const float M0r  = A.w * r_minus1;
+    const float K    = fmaf(-2.5f, X, -M0r) * r_minus2; // rQrAndMonopole
+    acc[0] -= fmaf(0.5f, X, M0r);
+    acc[1] = fmaf(r_minus5, Qrx, fmaf(K, r0, acc[1]));
+    acc[2] = fmaf(r_minus5, Qry, fmaf(K, r1, acc[2]));
+    acc[3] = fmaf(r_minus5, Qrz, fmaf(K, r2, acc[3]));
+#endif
 }
 
 typedef float v2f __attribute__((ext_vector_type(2)));
