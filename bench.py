@@ -437,7 +437,7 @@ def main():
             ex = SEARCH_BUILD_KERNELS if (k == "findNeighbors" and skin.get("builds", 1) == 0 and
                                           skin.get("plain_steps", 1) == 0 and skin.get("reuse_steps", 0) > 0) else ()
             per_kernel[k] = kernel_roofline(k, ms, n_local, ng, union_pp, pmc, ex)
-        elif ms > 0.01 and k == "gravity":
+        elif ms > 0.01 and k == "gravity" and inter is not None:  # (without self-gravity the slot times no kernel)
             per_kernel[k] = gravity_roofline(ms, n_local, inter, pmc)
     dominant = max(per_kernel, key=lambda k: per_kernel[k]["avg_launch_ms"]) if per_kernel else "momentumEnergy"
     dom = per_kernel.get(dominant, {})
