@@ -9,8 +9,9 @@ launch over a whole run, and the Evrard collapse over 100 steps):
     (Evrard: kinetic + internal + the step's potential) within 1e-5 of the reference's energy, the binned radial
     profiles of rho, p, |v|, u (oracle/trajectory.py) within 1 % at the profile steps; Noh also the reference's
     analytic check, the density L1 against nohRho (compare_noh.py:49-61,141-153), within 2 % of the reference run's;
-  * Sedov -n 400 -s 200 (config 4's workload, 64M particles, on one GPU): the reference cannot run 64M particles for
-    200 steps in test time, so size-independent properties: the energy drift within 1.5x the reference's own n=50
+  * Sedov -n 400 (config 4's workload, 64M particles, on one GPU) against the reference's own CPU run for 30 steps
+    (traj_sedov400.npz: a full skin rebuild falls inside them), and over the configured 200 steps, which the
+    reference cannot run in test time, through size-independent properties: the energy drift within 1.5x the reference's own n=50
     budget over 200 steps, and the density L1 against the reference's analytic solution (self-similar rescale to the
     fixture's time, as the config-2 test) below the n=200 run's 0.032 (test_gpu_trajectory.py, round 4): resolution
     convergence;
@@ -62,6 +63,7 @@ def _run_vs_reference(case):
                 prof[s] = tj.profiles(sim.get(tj.FIELDS), rmax, nbins)[1]
         final = sim.get(tj.FIELDS)
         _final_checks(sim, n)
+        skin = sim.skin_stats()
     finally:
         sim.close()
         ctx.close()
@@ -84,11 +86,11 @@ def _run_vs_reference(case):
     for s, d in l1.items():
         for k, v in d.items():
             assert v <= 0.01, (case, s, k, v)
-    return fx, final, ttot[-1]
+    return fx, final, ttot[-1], skin
 
 
 def test_noh_n300_100_steps_vs_reference():
-    fx, final, t = _run_vs_reference("noh300")
+    fx, final, t, _ = _run_vs_reference("noh300")
     for key, rho0 in (("ref_l1_noh_density_attr", tj.NOH_RHO0_ATTR), ("ref_l1_noh_density_ic", tj.NOH_RHO0_IC)):
         l1, ref = tj.noh_l1(final, t, rho0), float(fx[key][0])
         print(f"Noh -n 300 -s 100 density L1 vs nohRho (rho0 = {rho0:.4g}) at t = {t:.6g}: GPU {l1:.4f}, "
@@ -98,6 +100,21 @@ def test_noh_n300_100_steps_vs_reference():
 
 def test_evrard_n300_gravity_100_steps_vs_reference():
     _run_vs_reference("evrard300")
+
+
+def test_sedov_n400_30_steps_vs_reference():
+    """the metric's own workload (Sedov -n 400, 64M particles) against the reference's CPU run of the same lattice
+    (tests/golden/traj_sedov400.npz, oracle/gen_trajectory.py --fast sedov400): 30 steps un-reseeded with the default
+    skin lists, so that the forced full sync + rebuild of every skin after max_reuse = 24 filter-served steps falls
+    inside the compared window; time, energy of every step, binned profiles at steps 10/20/30, and the density L1 against
+    the reference's analytic solution within 2 % of the reference run's"""
+    fx, final, t, skin = _run_vs_reference("sedov400")
+    assert skin["builds"] >= 2 and skin["reuse_steps"] >= 24, skin
+    rho, _ = tj.eos_rho_p(final)
+    l1 = tj.analytic_l1(tj.radii(final), rho.astype(np.float64), fx["sol"][:, 0], fx["sol"][:, 1])
+    ref = float(fx["ref_l1_density_subsampled"][0])
+    print(f"Sedov -n 400 -s 30: t = {t:.6g}, density L1 vs analytic GPU {l1:.4f}, reference {ref:.4f}; skin {skin}")
+    assert abs(l1 / ref - 1) <= 0.02, (l1, ref)
 
 
 def test_sedov_n400_200_steps_full_size():
