@@ -211,7 +211,7 @@ def parse():
     ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
     ap.add_argument("--prop", default="ve", choices=["ve", "std"],
                     help="ve (HydroVeProp, the BASELINE metric) or std (HydroProp, std_hydro.hpp)")
-    ap.add_argument("--skin", type=float, default=0.08,
+    ap.add_argument("--skin", type=float, default=0.05,
                     help="neighbor lists behind a skin 2h(1+s) between full builds (sx_sim_set_skin; 0: sync + "
                          "search every step, the reference's flow)")
     ap.add_argument("--skin-reuse", type=int, default=24, help="steps between full builds at most")

@@ -66,9 +66,9 @@ struct BdtState
 //! particle order and tree are kept and each step's search is the filter of the last build's skin lists
 struct SkinState
 {
-    float    factor{0.08f};     // s: skin radius 2 h (1 + s); 0 = every step syncs and searches (the reference's flow)
-    float    cur{0.08f};        // s of the next build: doubled (up to kMaxSkin) while skins cannot outlast two steps
-    float    built{0.08f};      // s of the current skin lists
+    float    factor{0.05f};     // s: skin radius 2 h (1 + s); 0 = every step syncs and searches (the reference's flow)
+    float    cur{0.05f};        // s of the next build: doubled (up to kMaxSkin) while skins cannot outlast two steps
+    float    built{0.05f};      // s of the current skin lists
     int      maxReuse{24};      // steps after a full build before the next one at the latest
     float    staleLimit{0.125f}; // share of stale clusters in a step after which the next step does a full build
     bool     valid{false};      // every cluster's skin lists are current (a full build since the last state change)

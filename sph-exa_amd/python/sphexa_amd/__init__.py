@@ -648,7 +648,7 @@ class Sim:
         self.ctx.check(self.L.sx_sim_set_time(self.h, t), "set_time")
         return t
 
-    def set_skin(self, factor=0.08, max_reuse=24):
+    def set_skin(self, factor=0.05, max_reuse=24):
         """neighbor lists behind a skin of relative width `factor` (sx_sim_set_skin; 0: sync + search every step)"""
         self.ctx.check(self.L.sx_sim_set_skin(self.h, float(factor), int(max_reuse)), "set_skin")
 
