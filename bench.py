@@ -277,11 +277,18 @@ def cpu_baseline(seconds, side):
             "cpu_model": cpu_model(),
             "sample": f"Sedov lattice -n {side} ({st.n} particles, the metric's Sedov IC at 1/8 the particles), "
                       f"{steps} VE steps after 1 warm-up, {os.path.basename(path)} (the reference's own CPU "
-                      f"loops, -O3 -march=x86-64-v3), OMP threads={cores}"}
+                      f"loops, -O3 -march=x86-64-v3), OMP threads={cores}, "
+                      f"OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', 'unset')}, "
+                      f"OMP_PLACES={os.environ.get('OMP_PLACES', 'unset')}"}
 
 
 def main():
     args = parse()
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
+        # the reference CPU baseline's OpenMP threads pinned to cores, close together; set before any
+        # OpenMP runtime is loaded (the reference library is loaded only by cpu_baseline)
+        os.environ.setdefault("OMP_PROC_BIND", "close")
+        os.environ.setdefault("OMP_PLACES", "cores")
     if args.seam:
         print(json.dumps(seam_bench(args)))
         return
