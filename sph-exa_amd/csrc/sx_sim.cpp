@@ -1570,6 +1570,8 @@ bool skinUsable(const sx_sim* s)
 //! widest skin the adaptation goes to: skin lists (1.16)^3 = 1.56x the neighbors; wider unions outgrow the filter's LDS
 //! staging (kSkinCap) in dense regions (Noh at s = 0.25: 37% of the clusters)
 constexpr float kMaxSkin = 0.16f;
+//! reuse steps after which a skin has paid for its build several times over: a stale-forced build before them widens it
+constexpr int kShortSkin = 10;
 
 //! a skin that did not outlast two steps: the next build takes a twice wider one; at the widest, the next steps
 //! search without skin (backoff, doubling up to 32 steps)
@@ -1803,6 +1805,9 @@ void skinDecide(SkinState& K, bool reuse, const SkinCounts& c, uint64_t staleAll
     {
         K.forceBuild = true;
         if (!reuse || K.cleanSinceBuild < 2) skinTooThin(K);
+        // a skin used up by the flow in fewer than kShortSkin steps (Noh's shock at s = 0.05: a full build every ~6
+        // steps) is widened a little for the next build; one that lasts until maxReuse (Sedov) stays as it is
+        else if (K.sinceBuild < kShortSkin) K.cur = std::min(1.25f * K.cur, kMaxSkin);
     }
     if (clean && K.cleanSinceBuild >= 2) K.backoffLen = 4;
 }
