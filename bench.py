@@ -366,7 +366,7 @@ def main():
     # skin lists: the timed window starts with a full sync + build of every cluster's skin (on every rank: the build
     # decisions are collective), so `value` and `ms_per_step` carry at least their share of the builds that come every
     # max_reuse steps at the latest (a window shorter than max_reuse carries more than its share: 1 build in K steps,
-    # against 1 in max_reuse).  Several ranks with self-gravity sync + search every step (sx_sim.cpp skinUsable)
+    # against 1 in max_reuse)
     skin_window = args.skin > 0 and not args.no_build_step
     if skin_window:
         sim.rebuild_lists()
@@ -527,8 +527,7 @@ def main():
                    "neighbor_skin": {"initial_factor": args.skin, "max_reuse": args.skin_reuse,
                                      "note": "steps between full builds filter the last build's lists within "
                                              "2h(1+s) (sx_skin.hpp; several ranks: halos of the build refreshed, "
-                                             "displacement grid all-reduced, not with self-gravity); same neighbor "
-                                             "sets, nc, h",
+                                             "displacement grid all-reduced); same neighbor sets, nc, h",
                                      **skin}},
         "roofline": roofline,
         "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_ms.items()

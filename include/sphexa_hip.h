@@ -500,8 +500,8 @@ int    sx_sim_set_time(sx_sim* sim, double ttot);
  *  SX_ERR_ARG unless activeRung(ts->substep, ts->numRungs) == 0: restart files exist only at hierarchy boundaries
  *  (the reference writes them only when isSynced(), sphexa.cpp:165). */
 int    sx_sim_set_timestep(sx_sim* sim, const sx_timestep* ts, const uint8_t* rung);
-/*! neighbor lists behind a skin (VE or std propagator; one rank with or without self-gravity -- not with periodic
- *  self-gravity --, several ranks without self-gravity; sph-exa_amd/csrc/sx_skin.hpp):
+/*! neighbor lists behind a skin (VE or std propagator, one rank or several, with or without self-gravity -- not with
+ *  periodic self-gravity; sph-exa_amd/csrc/sx_skin.hpp):
  *  replaces the per-step Domain::sync + findNeighborsSph of ve_hydro.hpp:140-149 by a filter of the last build's
  *  lists within 2h(1 + factor) while no particle can have entered a target's 2h sphere since that build; stale
  *  clusters are rebuilt at once.  Neighbor sets, h and nc stay those of findNeighbors; between builds the particle

@@ -754,7 +754,7 @@ inline unsigned grid(size_t n, int b = 256) { return (unsigned)((n + b - 1) / b)
 __global__ void cellMomentsKernel(const double* x, const double* y, const double* z, const float* m,
                                   const uint32_t* cellBeg, const uint32_t* cellIds, int nCells,
                                   const int32_t* farLeafToNode, const double* geoC, const double* geoS, float invTheta,
-                                  GCell* out)
+                                  GCell* out, int drift)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nCells) return;
@@ -774,8 +774,28 @@ __global__ void cellMomentsKernel(const double* x, const double* y, const double
     const int     node = farLeafToNode[cellIds[k]];
     const double* gc   = geoC + 3 * (size_t)node;
     const double* gs   = geoS + 3 * (size_t)node;
-    const double  dx = g.com[0] - gc[0], dy = g.com[1] - gc[1], dz = g.com[2] - gc[2];
-    const double  smax = fmax(fmax(gs[0], gs[1]), gs[2]);
+    // the MAC box: the cell (a sync's cells hold their particles), or the cell and its drifted particles
+    double off[3] = {0.0, 0.0, 0.0}, hs[3] = {gs[0], gs[1], gs[2]};
+    if (drift)
+    {
+        double lo[3] = {-gs[0], -gs[1], -gs[2]}, hi[3] = {gs[0], gs[1], gs[2]};
+        for (uint32_t i = b; i < e; ++i)
+        {
+            const double r[3] = {x[i] - gc[0], y[i] - gc[1], z[i] - gc[2]};
+            for (int d = 0; d < 3; ++d)
+                lo[d] = fmin(lo[d], r[d]), hi[d] = fmax(hi[d], r[d]);
+        }
+        for (int d = 0; d < 3; ++d)
+        {
+            off[d] = 0.5 * (lo[d] + hi[d]);
+            // the float copy in GCell::box (far-tree refresh) rounded outwards
+            hs[d]  = (double)(float)(0.5 * (hi[d] - lo[d])) * (1.0 + 0x1p-20) + fabs((double)(float)off[d] - off[d]);
+        }
+    }
+    for (int d = 0; d < 3; ++d)
+        g.box[d] = (float)off[d], g.box[3 + d] = (float)hs[d];
+    const double  dx = g.com[0] - (gc[0] + off[0]), dy = g.com[1] - (gc[1] + off[1]), dz = g.com[2] - (gc[2] + off[2]);
+    const double  smax = fmax(fmax(hs[0], hs[1]), hs[2]);
     const double  mac  = 2.0 * smax * (double)invTheta + sqrt(dx * dx + (dy * dy + dz * dz));
     g.mac2             = c3 != 0.0 ? mac * mac : 0.0;
     float gv[8]        = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -830,6 +850,44 @@ __global__ void cellNearKernel(const GCell* cells, int nCells, const double* box
     if (lane == 0) near[k] = any ? 1u : 0u;
 }
 
+//! far-tree leaf boxes between syncs: a far cell's leaf takes the cell's MAC box (GCell::box, relative to the leaf's
+//! geometric center)
+__global__ void farLeafBoxKernel(GravArgs a, const GCell* cells, const uint32_t* far, int nCells, double* outC,
+                                 double* outS)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nCells || !far[k]) return;
+    const GCell& g    = cells[k];
+    const int    node = a.leafToNode[g.cell];
+    for (int d = 0; d < 3; ++d)
+    {
+        outC[3 * (size_t)node + d] = a.geoCenters[3 * (size_t)node + d] + (double)g.box[d];
+        outS[3 * (size_t)node + d] = (double)g.box[3 + d];
+    }
+}
+
+//! inner nodes of one level: the box holding their eight children's boxes (open box: no minimum image)
+__global__ void unionBoxKernel(const int32_t* childOffsets, int b, int e, double* c, double* sz)
+{
+    const int node = b + blockIdx.x * blockDim.x + threadIdx.x;
+    if (node >= e) return;
+    const int c0 = childOffsets[node];
+    if (c0 == 0) return;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = c0; k < c0 + 8; ++k)
+        for (int d = 0; d < 3; ++d)
+        {
+            lo[d] = fmin(lo[d], c[3 * (size_t)k + d] - sz[3 * (size_t)k + d]);
+            hi[d] = fmax(hi[d], c[3 * (size_t)k + d] + sz[3 * (size_t)k + d]);
+        }
+    for (int d = 0; d < 3; ++d)
+    {
+        // rounded outwards: the union must hold every child box
+        c[3 * (size_t)node + d]  = 0.5 * (lo[d] + hi[d]);
+        sz[3 * (size_t)node + d] = 0.5 * (hi[d] - lo[d]) * (1.0 + 0x1p-40);
+    }
+}
+
 //! far-tree leaves: cells with far[k] set get their mass center / mass and quadrupole, all other leaves are massless
 __global__ void farLeavesKernel(GravArgs a, const GCell* cells, const uint32_t* far, int nCells)
 {
@@ -848,11 +906,26 @@ __global__ void farLeavesKernel(GravArgs a, const GCell* cells, const uint32_t* 
 
 hipError_t cellMoments(const double* x, const double* y, const double* z, const float* m, const uint32_t* cellBeg,
                        const uint32_t* cellIds, int nCells, const int32_t* farLeafToNode, const double* geoC,
-                       const double* geoS, float invTheta, GCell* out, hipStream_t s)
+                       const double* geoS, float invTheta, GCell* out, hipStream_t s, bool drift)
 {
     if (nCells > 0)
         cellMomentsKernel<<<grid(nCells), 256, 0, s>>>(x, y, z, m, cellBeg, cellIds, nCells, farLeafToNode, geoC, geoS,
-                                                       invTheta, out);
+                                                       invTheta, out, drift ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t farRefreshBoxes(const GravArgs& a, const GCell* cells, const uint32_t* far, int nCells,
+                           const int32_t* levelRangeHost, double* outC, double* outS, hipStream_t s)
+{
+    if (a.numNodes <= 0) return hipSuccess;
+    (void)hipMemcpyAsync(outC, a.geoCenters, sizeof(double) * 3 * (size_t)a.numNodes, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(outS, a.geoSizes, sizeof(double) * 3 * (size_t)a.numNodes, hipMemcpyDeviceToDevice, s);
+    if (nCells > 0) farLeafBoxKernel<<<grid(nCells), 256, 0, s>>>(a, cells, far, nCells, outC, outS);
+    for (int level = kMaxLevel; level >= 0; --level)
+    {
+        const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
+        if (e > b) unionBoxKernel<<<grid(e - b), 256, 0, s>>>(a.childOffsets, b, e, outC, outS);
+    }
     return hipGetLastError();
 }
 

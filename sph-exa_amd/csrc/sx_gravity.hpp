@@ -42,21 +42,25 @@ struct GravArgs
 };
 
 //! a level-6 SFC cell of one rank's particles (multi-rank gravity): mass center, MAC radius^2, quadrupole (Cqi
-//! order, q[0] = mass), cell index (key >> 45) and particle count
+//! order, q[0] = mass), cell index (key >> 45) and particle count; box: the MAC geometry relative to the cell's
+//! geometric center (center offset, half sizes) -- the cell itself, or, between syncs (particles drifted out of their
+//! cells), the box holding the cell and its particles
 struct __attribute__((aligned(16))) GCell
 {
     double   com[3];
     double   mac2;
     float    q[8];
     uint32_t cell, count;
-    uint32_t pad[2];
+    float    box[6];
 };
-static_assert(sizeof(GCell) == 80, "GCell layout");
+static_assert(sizeof(GCell) == 96, "GCell layout");
 
-//! cells [cellBeg[k], cellBeg[k+1]) of key-sorted particles; geometry from the far tree's leaf nodes
+//! cells [cellBeg[k], cellBeg[k+1]) of key-sorted particles; geometry from the far tree's leaf nodes.  drift: the
+//! particles may have left their cells since the sync that formed the cells (skin-list reuse steps): the MAC box
+//! holds the cell and its particles (sx_skin.hpp skinRefreshBoxes(withCells) for one rank's tree)
 hipError_t cellMoments(const double* x, const double* y, const double* z, const float* m, const uint32_t* cellBeg,
                        const uint32_t* cellIds, int nCells, const int32_t* farLeafToNode, const double* geoC,
-                       const double* geoS, float invTheta, GCell* out, hipStream_t s);
+                       const double* geoS, float invTheta, GCell* out, hipStream_t s, bool drift = false);
 //! near[k] = 1 if cell k violates the vector MAC for any of the target boxes (center[3], half-size[3], stride 8)
 hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near,
                          hipStream_t s);
@@ -66,6 +70,10 @@ hipError_t farTreeLeafMap(const GravArgs& a, hipStream_t s);
 //! massless; then the mass-center / MAC / M2M upsweep
 hipError_t farUpsweep(const GravArgs& a, const GCell* cells, const uint32_t* far, int nCells,
                       const int32_t* levelRangeHost, hipStream_t s);
+//! the far tree's MAC geometry between syncs: every node's box (a.geoCenters / geoSizes -> outC / outS) with the far
+//! cells' leaves replaced by their GCell boxes and every inner node the union of its children's boxes (open box)
+hipError_t farRefreshBoxes(const GravArgs& a, const GCell* cells, const uint32_t* far, int nCells,
+                           const int32_t* levelRangeHost, double* outC, double* outS, hipStream_t s);
 
 //! expansion centers, MAC radii and multipoles of every node; levelRangeHost: kMaxLevel + 2 node offsets per level
 hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipStream_t s);

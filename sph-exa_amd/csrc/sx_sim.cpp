@@ -1282,7 +1282,7 @@ bool syncErrFailed(sx_sim* s)
  *  Each source is counted once (locals and near cells in the near tree, far cells in the far tree); every far-cell
  *  multipole is accepted by the same MAC the reference applies, so the result matches the single-rank
  *  Barnes-Hut field within its opening-angle error. */
-int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
+int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool drift)
 {
     sx::Transport* T  = s->comm;
     const int      P  = T->size(), r = T->rank();
@@ -1328,7 +1328,7 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     cellScatterKernel<<<grid(nl + 1), 256, 0, st>>>(lkeys, flag, scan, nl, (uint32_t)nCells, cellBeg, cellIds);
     GCell* mine = W.get<GCell>("g.mine", nCells);
     SIM_HIP(cellMoments(s->x + s->first, s->y + s->first, s->z + s->first, s->m + s->first, cellBeg, cellIds, nCells,
-                        farL2N, s->farTree.centers, s->farTree.sizes, invTheta, mine, st));
+                        farL2N, s->farTree.centers, s->farTree.sizes, invTheta, mine, st, drift));
 
     // --- 2. all-gather the cells (rank order = key order)
     std::vector<uint64_t> cnt(P, (uint64_t)nCells), rcnt(s->cellsOf);
@@ -1353,6 +1353,17 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     // --- 3. near / far classification against this rank's request boxes (distributedSync step 4)
     const size_t  nChunks = (nl + kChunk - 1) / kChunk;
     const ReqBox* boxes   = s->work.get<ReqBox>("dom.mybox", nChunks);
+    if (drift)
+    {
+        // the locals have moved since the sync's request boxes: boxes of their current positions (the same chunks)
+        ReqBox* cur = W.get<ReqBox>("g.curbox", nChunks);
+        if (!cur) return SX_ERR_NOMEM;
+        if (nChunks)
+            chunkBoxKernel<<<(unsigned)nChunks, 256, 0, st>>>(s->x + s->first, s->y + s->first, s->z + s->first,
+                                                             s->h + s->first, nl, kHaloMargin, quantMargin(s->dbox), r,
+                                                             cur);
+        boxes = cur;
+    }
     uint32_t*     nearF   = W.get<uint32_t>("g.near", nAll + 1);
     uint32_t*     farF    = W.get<uint32_t>("g.far", nAll + 1);
     uint32_t*     reqF    = W.get<uint32_t>("g.reqFlag", nAll + 1);
@@ -1452,6 +1463,16 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     ga.geoCenters     = s->nearTree.centers;
     ga.geoSizes       = s->nearTree.sizes;
     ga.leafToNode     = W.get<int32_t>("g.leafToNode", (size_t)s->nearTree.numLeaves);
+    if (drift)
+    {
+        // the near tree's cells come from the sync's keys: boxes holding each node's cell and its current particles
+        double* c3 = W.get<double>("g.geoC", 3 * (size_t)s->nearTree.numNodes);
+        double* s3 = W.get<double>("g.geoS", 3 * (size_t)s->nearTree.numNodes);
+        if (!c3 || !s3) return SX_ERR_NOMEM;
+        SIM_HIP(skinRefreshBoxes(s->nearTree, gx, gy, gz, s->dbox, c3, s3, st, true));
+        ga.geoCenters = c3;
+        ga.geoSizes   = s3;
+    }
     ga.x = gx, ga.y = gy, ga.z = gz, ga.m = gm, ga.h = gh;
     ga.centers4   = W.get<double>("g.centers", 4 * (size_t)s->nearTree.numNodes);
     ga.multipoles = W.get<float>("g.multipoles", 8 * (size_t)s->nearTree.numNodes);
@@ -1494,6 +1515,15 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active)
     fa.err   = &s->sc->gravErr;
     fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     fa.interactions = ga.interactions;
+    if (drift)
+    {
+        double* c3 = s->farMem.get<double>("far.geoC", 3 * (size_t)s->farTree.numNodes);
+        double* s3 = s->farMem.get<double>("far.geoS", 3 * (size_t)s->farTree.numNodes);
+        if (!c3 || !s3) return SX_ERR_NOMEM;
+        SIM_HIP(farRefreshBoxes(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), c3, s3, st));
+        fa.geoCenters = c3;
+        fa.geoSizes   = s3;
+    }
     SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
     fa.waveE = s->work.get<double>("grav.waveE", (fa.last - fa.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(fa, st));
@@ -1556,15 +1586,15 @@ bool periodicGravity(const sx_sim* s) { return s->p.g != 0.0 && s->box.bnd[0] ==
 //! Not with periodic self-gravity: between syncs a particle that crossed a periodic face is wrapped to the far side of
 //! the box while it stays in its old leaf, so the leaf's multipole (raw coordinates) would spread across the box
 //! while its refreshed MAC box (minimum image) covers only the old cell -- every step syncs there
-//! Several ranks (without self-gravity): the halo set of a full build is requested with the skin radius, a reuse step
-//! refreshes the halos' x, y, z, h, m over the build's send lists and reduces the displacement grid over all ranks, and
-//! every decision about builds is taken on all ranks together (skinHaloRefresh, the decision exchange in sx_sim_step).
-//! Multi-rank self-gravity would traverse near/far trees whose request boxes drift away from the locals: not used.
+//! Several ranks: the halo set of a full build is requested with the skin radius, a reuse step refreshes the halos'
+//! x, y, z, h, m over the build's send lists and reduces the displacement grid over all ranks, and every decision
+//! about builds is taken on all ranks together (skinHaloRefresh, the decision exchange in sx_sim_step); self-gravity
+//! on a reuse step splits near and far cells against boxes of the current positions and takes MAC boxes that hold
+//! each cell (node) and its drifted particles (distributedGravity with drift)
 bool skinUsable(const sx_sim* s)
 {
-    const bool dist = s->comm && s->comm->size() > 1;
-    return s->skin.factor > 0.0f && !(dist && s->p.g != 0.0) && s->p.propagator != 2 &&
-           NbLists::localPossible(s->p.ngmax) && !periodicGravity(s);
+    return s->skin.factor > 0.0f && s->p.propagator != 2 && NbLists::localPossible(s->p.ngmax) &&
+           !periodicGravity(s);
 }
 
 //! widest skin the adaptation goes to: skin lists (1.16)^3 = 1.56x the neighbors; wider unions outgrow the filter's LDS
@@ -2597,7 +2627,7 @@ extern "C"
             if (inter) SIM_HIP(hipMemsetAsync(inter, 0, 2 * sizeof(unsigned long long), st));
             if (dist)
             {
-                if (int e = distributedGravity(s, st, nullptr)) return e;
+                if (int e = distributedGravity(s, st, nullptr, reuse)) return e;
             }
             else
             {

@@ -212,7 +212,9 @@ int haloExchange(sx_sim* s, std::initializer_list<std::pair<void*, int>> fields,
 int halosOutgrown(sx_sim* s, hipStream_t st, unsigned& flag);
 //! multi-rank self-gravity onto ax, ay, az of the locals; active (nullable, indexed like the fields) restricts the
 //! targets
-int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active);
+//! drift: a skin-list reuse step (particles may have left the cells and request boxes of the last sync): the near/far
+//! split takes request boxes of the current positions and every MAC box holds its cell and its particles
+int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool drift = false);
 //! max |a|^2 of the locals into the device scalars (accelerationTimestep)
 void maxAccSq(sx_sim* s, hipStream_t st);
 

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--skin", type=float, default=0.08)
     ap.add_argument("--max-reuse", type=int, default=24)
+    ap.add_argument("--g", type=float, default=0.0, help="gravitational constant (self-gravity; evrard: 1)")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -42,10 +43,13 @@ def main():
 
     ctx = sx.Context(0)
     comm = sx.Comm("host")
-    st, obox = {"noh": po.noh_state}.get(args.ic, po.sedov_state)(args.side)
+    st, obox = {"noh": po.noh_state, "evrard": po.evrard_state}.get(args.ic, po.sedov_state)(args.side)
+    if args.ic in ("evrard", "noh"):
+        po.converge_h(po.load_oracle(), st, obox)  # the IC's h would iterate in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
     cap = 2 * st.n // size + 4096
-    a, b = sx.Sim(ctx, cap, box), sx.Sim(ctx, cap, box)
+    prm = sx.default_params(g=args.g)
+    a, b = sx.Sim(ctx, cap, box, params=prm), sx.Sim(ctx, cap, box, params=prm)
     for sim, f in ((a, args.skin), (b, 0.0)):
         sim.set_comm(comm)
         sim.set_skin(f, args.max_reuse if f > 0 else 1)
@@ -62,6 +66,7 @@ def main():
             for k, v in sim.get(FIELDS).items():
                 out[f"s{s}_{tag}_{k}"] = v
             out[f"s{s}_{tag}_dt"] = np.array([sim.scalars()["minDt"]])
+            out[f"s{s}_{tag}_egrav"] = np.array([sim.conserved()["egrav"]])
         ks = a.skin_stats()
         out[f"s{s}_skin"] = np.array([ks[k] for k in SKIN] + [ks["factor"], ks["next_factor"]], np.float64)
         out[f"s{s}_layout"] = np.array(list(a.layout().values()), np.int64)
