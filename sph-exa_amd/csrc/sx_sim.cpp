@@ -2729,7 +2729,11 @@ extern "C"
         qa.h       = s->h;
         qa.constCv = idealGasCv(s->p.muiConst, s->p.gamma);
         // one rank: the next localSync's keys come from this pass (the coordinates are in registers here)
-        qa.keys    = (!dist && s->p.propagator != 2) ? s->keys : nullptr;
+        // (not when the next step will be served by the skin filter: it does not sync; should it resync after all,
+        // localSync computes the keys itself, keysFresh being false)
+        const SkinState& K = s->skin;
+        const bool reuseNext = skinOn && K.valid && !K.forceBuild && K.sinceBuild < K.maxReuse && K.backoff == 0;
+        qa.keys    = (!dist && s->p.propagator != 2 && !reuseNext) ? s->keys : nullptr;
         if (skinOn && !skinParticleBuffers(s, qa, st)) return SX_ERR_NOMEM;
         H.positions(qa, st);
         s->keysFresh = qa.keys != nullptr;
