@@ -1043,11 +1043,7 @@ int distributedSync(sx_sim* s, hipStream_t st, double margin)
         for (int q = 0; q < P; ++q)
             nNew += recvCnt[q];
         broken = nNew != nlOf[r];
-        if (broken)
-        {
-            rbuf   = s->work.get<PRec>("dom.precv", nNew);
-            broken = true;
-        }
+        if (broken) rbuf = s->work.get<PRec>("dom.precv", nNew); // the peers send nNew records
         if (nl) packPRecKernel<<<grid(nl), 256, 0, st>>>(s->fields(), nl, sbuf);
         std::vector<uint64_t> sb(P), so(P), rb(P), ro(P);
         uint64_t              acc = 0;

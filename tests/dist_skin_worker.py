@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "sph-exa_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 STATE = ["x", "y", "z", "h", "m", "temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1", "alpha", "id"]
-FIELDS = ["id", "nc", "h", "xm", "kx", "divv", "alpha", "ax", "ay", "az", "du", "x", "vx"]
+FIELDS = ["id", "nc", "h", "ax", "ay", "az", "du", "x", "vx"]
 SKIN = ["builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps", "resyncs"]
 
 
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--skin", type=float, default=0.08)
     ap.add_argument("--max-reuse", type=int, default=24)
     ap.add_argument("--g", type=float, default=0.0, help="gravitational constant (self-gravity; evrard: 1)")
+    ap.add_argument("--std", action="store_true", help="std propagator (HydroProp)")
+    ap.add_argument("--av-clean", action="store_true", help="HydroVeProp<avClean=true>")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -48,7 +50,7 @@ def main():
         po.converge_h(po.load_oracle(), st, obox)  # the IC's h would iterate in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
     cap = 2 * st.n // size + 4096
-    prm = sx.default_params(g=args.g)
+    prm = sx.default_params(g=args.g, std=args.std, av_clean=args.av_clean)
     a, b = sx.Sim(ctx, cap, box, params=prm), sx.Sim(ctx, cap, box, params=prm)
     for sim, f in ((a, args.skin), (b, 0.0)):
         sim.set_comm(comm)
@@ -62,8 +64,9 @@ def main():
         b.set_state(g, sc["minDt"], sc["minDt_m1"])
         a.step()
         b.step()
+        fields = FIELDS + (["rho"] if args.std else ["xm", "kx", "divv", "alpha"])
         for tag, sim in (("a", a), ("b", b)):
-            for k, v in sim.get(FIELDS).items():
+            for k, v in sim.get(fields).items():
                 out[f"s{s}_{tag}_{k}"] = v
             out[f"s{s}_{tag}_dt"] = np.array([sim.scalars()["minDt"]])
             out[f"s{s}_{tag}_egrav"] = np.array([sim.conserved()["egrav"]])

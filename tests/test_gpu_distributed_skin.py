@@ -22,12 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SKIN = ["builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps", "resyncs"]
 
 
-def run(tmp_path, nproc, port, ic, side, steps, skin=0.08, max_reuse=24, g=0.0):
+def run(tmp_path, nproc, port, ic, side, steps, skin=0.08, max_reuse=24, g=0.0, extra=()):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tests", "dist_skin_worker.py"), "--out",
            str(tmp_path), "--ic", ic, "--side", str(side), "--steps", str(steps), "--skin", str(skin),
-           "--max-reuse", str(max_reuse), "--g", str(g)]
+           "--max-reuse", str(max_reuse), "--g", str(g), *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return [dict(np.load(os.path.join(tmp_path, f"rank{q}.npz"))) for q in range(nproc)]
@@ -97,4 +97,24 @@ def test_distributed_skin_with_gravity(tmp_path, nproc, port, side):
         assert abs(ea / eb - 1) <= 1e-3, (s, ea, eb)
     last = np.array([d[f"s{steps - 1}_skin"] for d in ranks])
     print("evrard", nproc, side, "gravity |da|/rms median, max", worst, dict(zip(SKIN, last[0][:6])))
+    assert last[0][SKIN.index("reuse_steps")] > 0, last[0]
+
+
+@pytest.mark.parametrize("opts,port", [(("--std",), 29658), (("--av-clean",), 29659)])
+def test_distributed_skin_std_and_avclean(tmp_path, opts, port):
+    """the std propagator (HydroProp: the filter's fused XMass writes rho) and VE with avClean (the dV halos) on skin
+    lists with 2 ranks, against the same ranks syncing every step: nc and h by id exactly, rates to float summation
+    order"""
+    steps = 8
+    ranks = run(tmp_path, 2, port, "sedov", 20, steps, 0.05, extra=opts)
+    fields = ["ax", "ay", "az", "du", "x", "vx"] + (["rho"] if "--std" in opts else ["xm", "kx", "divv", "alpha"])
+    for s in range(steps):
+        ga, gb = merged(ranks, s, "a", ["id", "nc", "h"] + fields), merged(ranks, s, "b", ["id", "nc", "h"] + fields)
+        assert np.array_equal(ga["id"], gb["id"])
+        assert np.array_equal(ga["nc"], gb["nc"]) and np.array_equal(ga["h"], gb["h"]), (opts, s)
+        for k in fields:
+            x, y = ga[k].astype(np.float64), gb[k].astype(np.float64)
+            tol = 2e-4 * np.abs(y) + 2e-5 * np.max(np.abs(y))
+            assert np.all(np.abs(x - y) <= tol), (opts, s, k)
+    last = np.array([d[f"s{steps - 1}_skin"] for d in ranks])
     assert last[0][SKIN.index("reuse_steps")] > 0, last[0]
