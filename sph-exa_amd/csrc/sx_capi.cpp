@@ -744,7 +744,7 @@ extern "C"
         packX(f->n, f->x, f->y, f->z, f->h, f->m, r.rx, c->stream);
         packV(f->n, f->vx, f->vy, f->vz, f->c, r.rv, c->stream);
         packT(f->n, f->xm, f->kx, nullptr, f->alpha, r.rt, c->stream);
-        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, f->divv, r.rc, c->stream);
+        packC(f->n, f->c11, f->c12, f->c13, f->c22, f->c23, f->c33, f->divv, r.rc, c->stream, f->xm, f->kx);
         PairArgs a = pairArgs(c, g, f, p, box, r);
         a.dt       = minDt;
         c->hydro().avSwitches(a, c->stream);

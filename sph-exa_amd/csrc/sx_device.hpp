@@ -57,9 +57,11 @@ struct __attribute__((aligned(16))) RecS
 {
     float rho, p, pad0, pad1;
 };
+//! IAD's outputs as a neighbor record; vol = xm / kx (the AV switches' neighbor volume, written where xm and kx are
+//! known: by IAD for its targets, by the packing pass for the halos)
 struct __attribute__((aligned(16))) RecC
 {
-    float c11, c12, c13, c22, c23, c33, divv, pad;
+    float c11, c12, c13, c22, c23, c33, divv, vol;
 };
 
 //! lt::lookup<float> (table_lookup.hpp:14-26) on a pair table {t[i], t[i+1]-t[i]}: one 8-byte gather.

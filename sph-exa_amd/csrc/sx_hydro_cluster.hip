@@ -452,7 +452,8 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         return;
     }
     const RecV  vi  = a.rv[cu.iSafe];
-    const float kxi = a.rt[cu.iSafe].kx;
+    const RecT  ti  = a.rt[cu.iSafe];
+    const float kxi = ti.kx;
 
     float dVx0 = 0, dVx1 = 0, dVx2 = 0, dVy0 = 0, dVy1 = 0, dVy2 = 0, dVz0 = 0, dVz1 = 0, dVz2 = 0;
     neighborLoop<CH, SPLIT>(
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvKernel(PairArgs a)
         const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
         const float divv_i   = norm_kxi * (dVx0 + dVy1 + dVz2);
         a.divv[i]            = divv_i;
-        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, 0.0f};
+        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, ti.xm / ti.kx};
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
@@ -525,7 +526,8 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
     const Clu   cu  = setup<SPLIT>(a, s_red);
     const RecX  ri  = a.rx[cu.iSafe];
     const RecV  vi  = a.rv[cu.iSafe];
-    const float kxi = a.rt[cu.iSafe].kx;
+    const RecT  ti  = a.rt[cu.iSafe];
+    const float kxi = ti.kx;
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
     const float hi = ri.h, hiInv = 1.0f / hi, hiInv2 = hiInv * hiInv, h2 = 2.0f * hi;
     float       t11 = 0, t12 = 0, t13 = 0, t22 = 0, t23 = 0, t33 = 0;
@@ -599,7 +601,7 @@ __global__ __launch_bounds__(kB * SPLIT) void iadDivvCurlvFusedKernel(PairArgs a
         const float norm_kxi = (float)(a.K * (double)(hiInv * hiInv * hiInv) / (double)kxi);
         const float divv_i   = norm_kxi * (dVx0 + dVy1 + dVz2);
         a.divv[i]            = divv_i;
-        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, 0.0f};
+        if (a.rcOut) a.rcOut[i] = RecC{c11i, c12i, c13i, c22i, c23i, c33i, divv_i, ti.xm / ti.kx};
         if (a.curlv)
         {
             const float cv0 = dVz1 - dVy2, cv1 = dVx2 - dVz0, cv2 = dVy0 - dVx1;
@@ -644,13 +646,14 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
     float       gx = 0, gy = 0, gz = 0;
     bool        res = false;
     auto        stage = [&](uint32_t j, uint32_t slot) {
-        const RecX r = a.rx[j];
-        const RecV v = a.rv[j];
-        const RecT t = a.rt[j];
+        const RecX   r  = a.rx[j];
+        const RecV   v  = a.rv[j];
+        // {divv, vol = xm / kx}: the last 8 bytes of the neighbor's RecC (IAD / the halo pack wrote vol)
+        const float2 dv = *reinterpret_cast<const float2*>(&a.rc[j].divv);
         sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2),
-                               t.xm / t.kx);
+                               dv.y);
         sV[slot] = make_float4(v.vx, v.vy, v.vz, v.c);
-        sD[slot] = a.rc[j].divv;
+        sD[slot] = dv.x;
     };
     auto loadRec = [&](uint32_t p) { return Rec9{sP[p], sV[p], sD[p]}; };
     neighborLoop<CH, SPLIT>(

@@ -2574,7 +2574,7 @@ extern "C"
                              [&](size_t u, size_t v)
                              {
                                  packC(v - u, s->c11 + u, s->c12 + u, s->c13 + u, s->c22 + u, s->c23 + u, s->c33 + u,
-                                       s->divv + u, s->rc + u, st);
+                                       s->divv + u, s->rc + u, st, s->xm + u, s->kx + u);
                              });
                     },
                     [&](const PairArgs& p)

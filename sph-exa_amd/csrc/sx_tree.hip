@@ -272,12 +272,13 @@ __global__ void packTKernel(size_t n, const float* xm, const float* kx, const fl
 }
 
 __global__ void packCKernel(size_t n, const float* c11, const float* c12, const float* c13, const float* c22,
-                            const float* c23, const float* c33, const float* divv, RecC* out)
+                            const float* c23, const float* c33, const float* divv, const float* xm, const float* kx,
+                            RecC* out)
 {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     out[i] = RecC{c11 ? c11[i] : 0.f, c12 ? c12[i] : 0.f, c13 ? c13[i] : 0.f, c22 ? c22[i] : 0.f,
-                  c23 ? c23[i] : 0.f, c33 ? c33[i] : 0.f, divv ? divv[i] : 0.f, 0.f};
+                  c23 ? c23[i] : 0.f, c33 ? c33[i] : 0.f, divv ? divv[i] : 0.f, (xm && kx) ? xm[i] / kx[i] : 0.f};
 }
 
 __global__ void tablePairKernel(const float* t, float2* out)
@@ -726,9 +727,9 @@ void packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s)
     if (n) packTKernel<<<grid(n), 256, 0, s>>>(n, rho, p, nullptr, nullptr, reinterpret_cast<RecT*>(out));
 }
 void packC(size_t n, const float* c11, const float* c12, const float* c13, const float* c22, const float* c23,
-           const float* c33, const float* divv, RecC* out, hipStream_t s)
+           const float* c33, const float* divv, RecC* out, hipStream_t s, const float* xm, const float* kx)
 {
-    if (n) packCKernel<<<grid(n), 256, 0, s>>>(n, c11, c12, c13, c22, c23, c33, divv, out);
+    if (n) packCKernel<<<grid(n), 256, 0, s>>>(n, c11, c12, c13, c22, c23, c33, divv, xm, kx, out);
 }
 void tablePairs(const float* t, float2* out, hipStream_t s) { tablePairKernel<<<grid(kTableSize), 256, 0, s>>>(t, out); }
 

@@ -305,8 +305,10 @@ void       packX(size_t n, const double* x, const double* y, const double* z, co
 void       packV(size_t n, const float* vx, const float* vy, const float* vz, const float* c, RecV* out, hipStream_t s);
 void       packT(size_t n, const float* xm, const float* kx, const float* prho, const float* alpha, RecT* out,
                  hipStream_t s);
+//! xm, kx (nullable): RecC::vol = xm / kx (the AV switches' neighbor volume)
 void       packC(size_t n, const float* c11, const float* c12, const float* c13, const float* c22, const float* c23,
-                 const float* c33, const float* divv, RecC* out, hipStream_t s);
+                 const float* c33, const float* divv, RecC* out, hipStream_t s, const float* xm = nullptr,
+                 const float* kx = nullptr);
 void       packS(size_t n, const float* rho, const float* p, RecS* out, hipStream_t s);
 void       tablePairs(const float* t, float2* out, hipStream_t s);
 
