@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
         [&](uint32_t j, uint32_t slot) {
             const RecX r = a.rx[j];
             sP[slot] = make_float4(relc(r.x, cu.ox, a.box, 0), relc(r.y, cu.oy, a.box, 1), relc(r.z, cu.oz, a.box, 2), r.m);
-            sX[slot] = a.rt[j].xm;
+            sX[slot] = a.xm[j]; // the dense field (a union run of consecutive particles shares its sectors), not RecT
         },
         [&](uint32_t p) { return Rec5{sP[p], sX[p]}; },
         [&](const Rec5& r) {
