@@ -394,7 +394,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = sim.stats()
-    skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps") else v)
+    skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps", "kept_clusters") else v)
             for k, v in sim.skin_stats().items()}  # the timed steps'
     n_local = sim.size()
     ms_step = el / args.steps * 1e3

@@ -1688,7 +1688,10 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint32_t*   l2    = s->mem.get<uint32_t>("skin.l2", ncl + 1);
     uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 3);
     uint8_t*    strk  = s->mem.get<uint8_t>("skin.streak", ncl);
-    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk)
+    uint32_t*   hmask = s->mem.get<uint32_t>("skin.hitmask", na.numGroups * (size_t)kSkinMaskWords * kWave);
+    uint8_t*    same  = s->mem.get<uint8_t>("skin.same", ncl);
+    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk ||
+        !hmask || !same)
         return SX_ERR_NOMEM;
 
     const SkinGrid g = skinGrid(s->dbox);
@@ -1706,6 +1709,13 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     K.xmFused   = xmOut != nullptr;
     K.exactList = l2;
     fa.box = na.box, fa.powTab = na.powTab, fa.stats = na.stats, fa.clStats = na.clStats;
+    // exact lists kept where no target's hits changed: only over the lists, masks and flags the last skin search of
+    // this simulation left (no other search or allocation since)
+    fa.hitMask   = hmask;
+    fa.same      = same;
+    fa.keepLists = reuse && K.listsKept && K.keptNloc == na.nloc && K.keptUni == na.uni && K.keptMask == hmask &&
+                   K.keptSame == same;
+    K.listsKept  = false; // until this search completes
 
     // the skin build: the search with radii 2 h (1 + s), no h iteration, skin lists and counts as its outputs
     NsArgs b   = na;
@@ -1791,6 +1801,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         }
     }
     SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
+    K.listsKept = true, K.keptNloc = na.nloc, K.keptUni = na.uni, K.keptMask = hmask, K.keptSame = same;
     if (getenv("SX_SKIN_DEBUG"))
     {
         uint32_t f = 0;
@@ -2005,14 +2016,14 @@ extern "C"
         return SX_OK;
     }
 
-    int sx_sim_skin_stats(sx_sim* s, uint64_t out[11])
+    int sx_sim_skin_stats(sx_sim* s, uint64_t out[12])
     {
         if (!s) return SX_ERR_ARG;
         const auto& K = s->skin;
         out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
         out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = K.plainSteps;
         out[8] = (uint64_t)std::lround(1e6 * K.built), out[9] = (uint64_t)std::lround(1e6 * K.cur);
-        out[10] = K.resyncs;
+        out[10] = K.resyncs, out[11] = K.keptClusters;
         return SX_OK;
     }
 
@@ -2319,6 +2330,7 @@ extern "C"
                 pol.mode = getenv("SX_SEARCH_LARGE") ? 1 : 2; // compact build first (as in the real search)
                 x.policy = &pol;
                 const int R  = std::max(1, atoi(reps));
+                s->skin.listsKept = false; // this search rewrites the exact lists
                 SIM_HIP(hipEventRecord(s->kev[0], st));
                 for (int r = 0; r < R; ++r)
                 {
@@ -2362,7 +2374,8 @@ extern "C"
             }
             else
             {
-                s->skin.xmFused = false;
+                s->skin.xmFused   = false;
+                s->skin.listsKept = false;
                 SIM_HIP(findNeighbors(na, st));
             }
             SIM_HIP(hipEventRecord(s->kev[1], st));
@@ -2748,6 +2761,7 @@ extern "C"
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->lastStats.maxUnion      = s->statsHost[12];
+        if (skinOn && reuse) s->skin.keptClusters += s->statsHost[18];
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         if (reuse && s->skin.cleanSinceBuild <= 1 && !s->skin.forceBuild)
         {

@@ -91,6 +91,11 @@ struct SkinState
     // this step: the filter computed XMass of every cluster but the exact-search ones (exactList[1 ..], lastExact)
     bool      xmFused{false};
     uint32_t* exactList{nullptr};
+    // the exact lists, hit masks and per-cluster flags the last skin search left (SkinArgs::keepLists), and the
+    // clusters whose lists a reuse step kept (statistics)
+    bool      listsKept{false};
+    const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr};
+    uint64_t  keptClusters{0};
 };
 
 } // namespace sx::sim

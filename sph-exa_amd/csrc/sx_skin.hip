@@ -131,25 +131,27 @@ __global__ void markStaleKernel(const uint32_t* list, uint32_t numClusters, floa
 
 __global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
 {
-    __shared__ uint32_t           s_max[2][16];
+    __shared__ uint32_t           s_max[3][16];
     __shared__ unsigned long long s_sum[3][16];
-    uint32_t                      mx = 0, mu = 0;
+    uint32_t                      mx = 0, mu = 0, kp = 0; // kp: clusters whose exact lists the filter kept
     unsigned long long            st = 0, te = 0, un = 0;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     {
         const uint4 v = cl[i];
-        mx = max(mx, v.x), st += v.y, te += v.z, un += v.w, mu = max(mu, v.w);
+        mx = max(mx, v.x), st += v.y & 0x7fffffffu, te += v.z, un += v.w, mu = max(mu, v.w), kp += v.y >> 31;
     }
-    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un);
+    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un), kp = waveSum(kp);
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) s_max[0][w] = mx, s_max[1][w] = mu, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
+    if ((threadIdx.x & 63) == 0)
+        s_max[0][w] = mx, s_max[1][w] = mu, s_max[2][w] = kp, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
     __syncthreads();
     if (threadIdx.x == 0)
     {
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), st += s_sum[0][k], te += s_sum[1][k],
-            un += s_sum[2][k];
+            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), kp += s_max[2][k], st += s_sum[0][k],
+            te += s_sum[1][k], un += s_sum[2][k];
         stats[2]                                          = mx;
+        stats[18]                                         = kp;
         stats[12]                                         = mu;
         *reinterpret_cast<unsigned long long*>(stats + 4) = st;
         *reinterpret_cast<unsigned long long*>(stats + 6) = te;
@@ -164,7 +166,9 @@ __device__ __forceinline__ void pushStale(const SkinArgs& a, uint32_t c)
     uint32_t* L = (a.direct && a.streak && a.streak[c]) ? a.direct : a.stale;
     L[1 + atomicAdd(&L[0], 1u)] = c;
     if (a.streak) a.streak[c] = 1;
+    if (a.same) a.same[c] = 0; // its lists are rewritten by a rebuild or the exact search
 }
+static_assert((kWalkBlocks + 1) / 2 <= (int)kSkinMaskWords, "hit-mask words per target");
 
 __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numClusters)
 {
@@ -481,8 +485,33 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         if (!blockAny(again)) break;
     }
 
+    // ---- 4b. every target kept the same hits as the pass that wrote this cluster's exact lists: the union and lists
+    //          in place are this step's (the skin lists are fixed between builds, so equal bits are equal sets)
+    const uint32_t   nbl = valid ? (((scount + 1) >> 1) + kWalkPF - 1) / kWalkPF : 0u; // walk blocks of this lane
+    uint32_t* const  hm  = a.hitMask ? a.hitMask + (size_t)gw * kSkinMaskWords * kWave + lane : nullptr;
+    auto             maskWord = [&](uint32_t k) {
+        const uint32_t lo = s_bm[2 * k][threadIdx.x];
+        return 2 * k + 1 < nbl ? lo | ((uint32_t)s_bm[2 * k + 1][threadIdx.x] << 16) : lo;
+    };
+    bool kept = false;
+    if (hm && a.keepLists && !a.fresh && a.same[c])
+    {
+        constexpr int MW = (kWalkBlocks + 1) / 2;
+        const uint32_t nmw = (nbl + 1) >> 1;
+        uint32_t       prev[MW];
+#pragma unroll
+        for (int k = 0; k < MW; ++k)
+            prev[k] = hm[(size_t)min((uint32_t)k, nmw ? nmw - 1 : 0u) * kWave]; // unconditional (clamped)
+        bool diff = false;
+#pragma unroll
+        for (int k = 0; k < MW; ++k)
+            if ((uint32_t)k < nmw) diff |= prev[k] != maskWord(k);
+        kept = !blockAny(diff);
+    }
+
     // ---- 5. exact union: ranks of the hit U_s entries (U_s order), the union at the slot's start, lists rewritten
-    uint32_t ue = 0;
+    uint32_t ue = kept ? __builtin_amdgcn_readfirstlane(a.ucount[c]) : 0u;
+    if (!kept)
     {
         // every thread a run of consecutive entries
         const uint32_t B  = (U + kB - 1) / kB;
@@ -521,7 +550,8 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         }
         __syncthreads();
     }
-    // pass B: the same walk, the first ngmax hits written as exact-union ranks (two per word)
+    // pass B: the same walk, the first ngmax hits written as exact-union ranks (two per word); the hit bits recorded
+    if (!kept)
     {
         unsigned st = 0;
         uint32_t pend = 0, bits = 0;
@@ -536,6 +566,12 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
              },
              [](uint32_t) {});
         if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend;
+        if (hm)
+        {
+            for (uint32_t k = 0; 2 * k < nbl; ++k)
+                hm[(size_t)k * kWave] = maskWord(k);
+            if (threadIdx.x == 0) a.same[c] = 1;
+        }
     }
 
     // ---- 6. outputs
@@ -577,6 +613,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         uint4 t = s_cst[0];
         for (int w = 1; w < kClusterWaves; ++w)
             t.x = max(t.x, s_cst[w].x), t.y += s_cst[w].y, t.z += s_cst[w].z;
+        t.y |= kept ? 0x80000000u : 0u; // (stored entries < 2^31)
         t.w          = ue;
         a.clStats[c] = t;
     }

@@ -38,6 +38,8 @@ namespace sx
 using SkinGrid = DispGrid; //!< per-step displacement maxima by cell (sx_device.hpp)
 
 constexpr int kSkinGridN = 64;
+//! u32 words of kept-hit bits per target (SkinArgs::hitMask): one u16 per 16-entry walk block, up to 256 entries
+constexpr uint32_t kSkinMaskWords = 8;
 
 //! filter arguments (one 256-thread workgroup per cluster)
 struct SkinArgs
@@ -76,6 +78,14 @@ struct SkinArgs
     // by a skin since; such a cluster, stale again, is listed in `direct` (the exact search) instead of `stale`
     uint8_t*        streak;
     uint32_t*       direct;
+    // nullable: per target the kept-hit bits of the last pass that wrote its cluster's exact lists (kSkinMaskWords u32
+    // words, lane-interleaved like nloc; bits 16 (k & 1) .. of word k / 2: walk block k), and per cluster 1 while the
+    // exact union and lists at uni / nloc are the ones those bits give (0 once the cluster is stale).  With keepLists
+    // (a reuse step after a skin search on the same lists) a cluster whose targets' bits are all unchanged keeps its
+    // union and lists: the rank pass and its second walk of the skin lists are skipped
+    uint32_t*       hitMask;
+    uint8_t*        same;
+    int             keepLists;
     DevBox          box;
     const float*    powTab;
     // nullable: the fused XMass (xmassJLoop on the final lists, as sx_hydro_cluster.hip's xmassKernel): xm of every

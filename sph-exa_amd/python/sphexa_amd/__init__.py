@@ -657,12 +657,13 @@ class Sim:
         self.ctx.check(self.L.sx_sim_rebuild_lists(self.h), "rebuild_lists")
 
     def skin_stats(self):
-        out = (C.c_uint64 * 11)()
+        out = (C.c_uint64 * 12)()
         self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
         d = dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
                       "capacity", "plain_steps"], list(out)[:8]))
         d["factor"], d["next_factor"] = out[8] * 1e-6, out[9] * 1e-6
         d["resyncs"] = out[10]
+        d["kept_clusters"] = out[11]
         return d
 
     def neighbor_sets(self):

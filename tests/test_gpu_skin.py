@@ -107,6 +107,8 @@ def test_skin_quiescent_lattice_reuses(ctx):
             assert sim.stats()["numFailed"] == 0
         ks = sim.skin_stats()
         assert ks["builds"] == 2 and ks["reuse_steps"] == 9 and ks["stale_clusters"] == 0, ks
+        # nothing moves: reuse steps whose hits equal the last step's keep the exact lists in place
+        assert ks["kept_clusters"] > 0, ks
     finally:
         sim.close()
 
