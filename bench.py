@@ -375,6 +375,9 @@ def main():
     skin0 = sim.skin_stats()
     stage_sum, kern_sum = {}, {}
     step_s = []  # host time of every timed step (sx_sim_step returns after its stream synchronisation)
+    search_ms, kept_steps = [], []  # per step: the search slot's kernel time, clusters whose exact lists were kept
+    # (of them frozen)
+    kept0, frz0 = skin0.get("kept_clusters", 0), skin0.get("frozen_clusters", 0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ts = time.perf_counter()
@@ -382,8 +385,14 @@ def main():
         step_s.append(time.perf_counter() - ts)
         for k, v in sim.stage_times().items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
-        for k, v in sim.kernel_times().items():
+        kt = sim.kernel_times()
+        for k, v in kt.items():
             kern_sum[k] = kern_sum.get(k, 0.0) + v
+        search_ms.append(round(kt.get("findNeighbors", 0.0), 3))
+        if args.skin > 0:
+            ks = sim.skin_stats()
+            kept_steps.append((int(ks["kept_clusters"] - kept0), int(ks["frozen_clusters"] - frz0)))
+            kept0, frz0 = ks["kept_clusters"], ks["frozen_clusters"]
     ctx.sync()
     barrier()
     el = time.perf_counter() - t0
@@ -394,8 +403,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     stats = sim.stats()
-    skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps", "kept_clusters") else v)
+    skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps",
+                                      "kept_clusters", "frozen_clusters") else v)
             for k, v in sim.skin_stats().items()}  # the timed steps'
+    if args.skin > 0:
+        skin["search_ms_per_step"] = search_ms
+        skin["kept_frozen_clusters_per_step"] = kept_steps
     n_local = sim.size()
     ms_step = el / args.steps * 1e3
     if dist is not None:  # per-step times: the slowest rank's

@@ -1690,8 +1690,9 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint8_t*    strk  = s->mem.get<uint8_t>("skin.streak", ncl);
     uint32_t*   hmask = s->mem.get<uint32_t>("skin.hitmask", na.numGroups * (size_t)kSkinMaskWords * kWave);
     uint8_t*    same  = s->mem.get<uint8_t>("skin.same", ncl);
+    float2*     frz   = s->mem.get<float2>("skin.frz", ncl);
     if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk ||
-        !hmask || !same)
+        !hmask || !same || !frz)
         return SX_ERR_NOMEM;
 
     const SkinGrid g = skinGrid(s->dbox);
@@ -1713,8 +1714,9 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     // this simulation left (no other search or allocation since)
     fa.hitMask   = hmask;
     fa.same      = same;
+    fa.frz       = getenv("SX_SKIN_NOFREEZE") ? nullptr : frz; // (A/B: every reuse step walks its skin lists)
     fa.keepLists = reuse && K.listsKept && K.keptNloc == na.nloc && K.keptUni == na.uni && K.keptMask == hmask &&
-                   K.keptSame == same;
+                   K.keptSame == same && K.keptFrz == frz;
     K.listsKept  = false; // until this search completes
 
     // the skin build: the search with radii 2 h (1 + s), no h iteration, skin lists and counts as its outputs
@@ -1801,7 +1803,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         }
     }
     SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
-    K.listsKept = true, K.keptNloc = na.nloc, K.keptUni = na.uni, K.keptMask = hmask, K.keptSame = same;
+    K.listsKept = true, K.keptNloc = na.nloc, K.keptUni = na.uni, K.keptMask = hmask, K.keptSame = same, K.keptFrz = frz;
     if (getenv("SX_SKIN_DEBUG"))
     {
         uint32_t f = 0;
@@ -2016,14 +2018,14 @@ extern "C"
         return SX_OK;
     }
 
-    int sx_sim_skin_stats(sx_sim* s, uint64_t out[12])
+    int sx_sim_skin_stats(sx_sim* s, uint64_t out[13])
     {
         if (!s) return SX_ERR_ARG;
         const auto& K = s->skin;
         out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
         out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = K.plainSteps;
         out[8] = (uint64_t)std::lround(1e6 * K.built), out[9] = (uint64_t)std::lround(1e6 * K.cur);
-        out[10] = K.resyncs, out[11] = K.keptClusters;
+        out[10] = K.resyncs, out[11] = K.keptClusters, out[12] = K.frozenClusters;
         return SX_OK;
     }
 
@@ -2761,7 +2763,7 @@ extern "C"
         s->lastStats.sumCandidates = *reinterpret_cast<uint64_t*>(s->statsHost + 6);
         s->lastStats.sumUnion      = *reinterpret_cast<uint64_t*>(s->statsHost + 8);
         s->lastStats.maxUnion      = s->statsHost[12];
-        if (skinOn && reuse) s->skin.keptClusters += s->statsHost[18];
+        if (skinOn && reuse) s->skin.keptClusters += s->statsHost[18], s->skin.frozenClusters += s->statsHost[19];
         s->nsPolicy.observe(s->statsHost, (uint32_t)(s->last - s->first));
         if (reuse && s->skin.cleanSinceBuild <= 1 && !s->skin.forceBuild)
         {

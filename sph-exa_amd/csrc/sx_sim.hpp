@@ -94,8 +94,8 @@ struct SkinState
     // the exact lists, hit masks and per-cluster flags the last skin search left (SkinArgs::keepLists), and the
     // clusters whose lists a reuse step kept (statistics)
     bool      listsKept{false};
-    const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr};
-    uint64_t  keptClusters{0};
+    const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr}, *keptFrz{nullptr};
+    uint64_t  keptClusters{0}, frozenClusters{0};
 };
 
 } // namespace sx::sim

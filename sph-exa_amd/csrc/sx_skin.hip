@@ -131,27 +131,29 @@ __global__ void markStaleKernel(const uint32_t* list, uint32_t numClusters, floa
 
 __global__ __launch_bounds__(1024) void reduceClusterStatsKernel(const uint4* cl, uint32_t n, uint32_t* stats)
 {
-    __shared__ uint32_t           s_max[3][16];
+    __shared__ uint32_t           s_max[4][16];
     __shared__ unsigned long long s_sum[3][16];
-    uint32_t                      mx = 0, mu = 0, kp = 0; // kp: clusters whose exact lists the filter kept
+    uint32_t                      mx = 0, mu = 0, kp = 0, fz = 0; // clusters whose exact lists the filter kept, frozen
     unsigned long long            st = 0, te = 0, un = 0;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
     {
         const uint4 v = cl[i];
-        mx = max(mx, v.x), st += v.y & 0x7fffffffu, te += v.z, un += v.w, mu = max(mu, v.w), kp += v.y >> 31;
+        mx = max(mx, v.x), st += v.y & 0x3fffffffu, te += v.z, un += v.w, mu = max(mu, v.w), kp += v.y >> 31,
+        fz += (v.y >> 30) & 1u;
     }
-    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un), kp = waveSum(kp);
+    mx = waveMax(mx), mu = waveMax(mu), st = waveSum(st), te = waveSum(te), un = waveSum(un), kp = waveSum(kp), fz = waveSum(fz);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
-        s_max[0][w] = mx, s_max[1][w] = mu, s_max[2][w] = kp, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
+        s_max[0][w] = mx, s_max[1][w] = mu, s_max[2][w] = kp, s_max[3][w] = fz, s_sum[0][w] = st, s_sum[1][w] = te, s_sum[2][w] = un;
     __syncthreads();
     if (threadIdx.x == 0)
     {
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), kp += s_max[2][k], st += s_sum[0][k],
+            mx = max(mx, s_max[0][k]), mu = max(mu, s_max[1][k]), kp += s_max[2][k], fz += s_max[3][k], st += s_sum[0][k],
             te += s_sum[1][k], un += s_sum[2][k];
         stats[2]                                          = mx;
         stats[18]                                         = kp;
+        stats[19]                                         = fz;
         stats[12]                                         = mu;
         *reinterpret_cast<unsigned long long*>(stats + 4) = st;
         *reinterpret_cast<unsigned long long*>(stats + 6) = te;
@@ -170,9 +172,11 @@ __device__ __forceinline__ void pushStale(const SkinArgs& a, uint32_t c)
 }
 static_assert((kWalkBlocks + 1) / 2 <= (int)kSkinMaskWords, "hit-mask words per target");
 
-__global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numClusters)
+//! four workgroups per CU by LDS: at most 128 VGPRs keep them all
+__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void skinFilterKernel(SkinArgs a,
+                                                                                              uint32_t numClusters)
 {
-    // LDS: 39.9 KB, four workgroups per CU
+    // LDS: 40960 B, exactly a quarter of the CU's 160 KB: four workgroups per CU (one more byte leaves three)
     __shared__ float4   s_rec[kSkinCap]; // U_s positions relative to the cluster origin, |p|^2; then the exact-union
                                          // ranks (u16) of the U_s entries, once pass A is done with the positions
     __shared__ uint8_t  s_hit[kSkinCap + 4]; // U_s entry hit by some target (exact union); [kSkinCap]: spare
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     __shared__ float    s_red[kClusterWaves];
     __shared__ int      s_vote[kClusterWaves];
     __shared__ uint32_t s_wsum[kClusterWaves];
-    __shared__ uint4    s_cst[kClusterWaves];
+    __shared__ uint4    s_cst[kClusterWaves]; // .w: the wave's freeze minimum K + 2h (s_wsum: K - 2h) at the end
 
     const uint32_t nWork = a.list ? __builtin_amdgcn_readfirstlane(a.list[0]) : numClusters;
     if (blockIdx.x >= nWork) return;
@@ -207,16 +211,24 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     const uint32_t scount = valid ? a.scnt[i] - 1u : 0u;
     const uint32_t U      = __builtin_amdgcn_readfirstlane(a.ucountS[c]);
     const float    kEps   = 0x1p-16f;
-    auto           blockAny = [&](bool v) -> bool {
-        const bool w = __ballot(v) != 0;
-        if (lane == 0) s_vote[wave] = w;
+    // the freeze reference (1b), loaded with the target's state: its latency off the vote's chain
+    const bool     mayFreeze = a.frz && a.keepLists && !a.fresh && a.same[c];
+    const float2   fref      = mayFreeze ? a.frz[c] : make_float2(-INFINITY, -INFINITY);
+    //! per bit k of v: whether any thread of the workgroup set it (one vote round for several decisions)
+    auto           blockBits = [&](uint32_t v) -> uint32_t {
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            w |= __ballot((v >> k) & 1u) != 0 ? 1u << k : 0u;
+        if (lane == 0) s_vote[wave] = (int)w;
         __syncthreads();
-        bool any = false;
+        uint32_t any = 0;
         for (int k = 0; k < kClusterWaves; ++k)
-            any |= s_vote[k] != 0;
+            any |= (uint32_t)s_vote[k];
         __syncthreads();
         return any;
     };
+    auto blockAny = [&](bool v) -> bool { return blockBits(v ? 1u : 0u) != 0; };
 
     // ---- 1. the region's displacement since the build: A = acc + this step's maximum over the grid cells around
     //         the wave boxes grown by the largest skin radius
@@ -284,30 +296,52 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     // a target's skin holds every current neighbor while 2h + d + A <= R (1 - eps); a build that overflowed a capacity
     // (skin list beyond ngmaxS, union beyond the slot) never serves, nor a union beyond the LDS capacity
     auto withinSkin = [&](float h) { return 2.0f * h + di + A <= Ri * (1.0f - kEps); };
+    // ---- 1b. frozen: since the last pass that walked this cluster (its reference: per target the smallest distance
+    //          g of a skin entry to the 2h sphere, and d_i + A_C, h then) no target and no entry has moved, nor has
+    //          2h changed, by enough for any entry to cross the sphere -- the relative motion of i and an entry is at
+    //          most the growth of d_i + A_C since (sx_skin.hpp's bound, also for entries outside the ball), so
+    //          2 |h - h_ref| + (d_i + A_C) - (d_i + A_C)_ref < g keeps every hit and miss.  The exact lists in place
+    //          are then this step's: no walk of the skin lists, the fused XMass over the exact lists
+    //          Per cluster the reference pass left fref = min over its targets of K_i + 2 h_i and of K_i - 2 h_i,
+    //          K_i = g_i + (d_i + A_C) then (-inf: never frozen); d_i + A_C + 2h_i below the first and d_i + A_C - 2h_i
+    //          below the second give 2 |h_i - h_i,ref| + (d_i + A_C) < K_i for every target.  One vote with 1.
+    bool frozen = false;
     {
-        const bool bad = valid && (scount > a.ngmaxS || !withinSkin(hi));
-        if (blockAny(bad) || U > (uint32_t)kSkinCap || U > a.ucap - a.uoff)
+        const bool bad  = valid && (scount > a.ngmaxS || !withinSkin(hi));
+        // one more drift like the one since the build would make the cluster stale (stats[13]: the host stops using
+        // skins that cannot outlast two steps, sx_sim.cpp)
+        const bool thin = !a.fresh && valid && 2.0f * hi + 2.0f * (di + A) > Ri * (1.0f - kEps);
+        const float e    = di + A + kEps * Ri;
+        const bool  melt = valid && !(e + 2.0f * hi < fref.x && e - 2.0f * hi < fref.y);
+        const uint32_t v = blockBits((bad ? 1u : 0u) | (thin ? 2u : 0u) | (melt ? 4u : 0u));
+        if ((v & 1u) || U > (uint32_t)kSkinCap || U > a.ucap - a.uoff)
         {
             if (threadIdx.x == 0) pushStale(a, c);
             return;
         }
-        // one more drift like the one since the build would make the cluster stale (stats[13]: the host stops using
-        // skins that cannot outlast two steps, sx_sim.cpp)
-        if (!a.fresh && blockAny(valid && 2.0f * hi + 2.0f * (di + A) > Ri * (1.0f - kEps)) && threadIdx.x == 0)
-            atomicAdd(&a.stats[13], 1u);
+        if ((v & 2u) && threadIdx.x == 0) atomicAdd(&a.stats[13], 1u);
+        frozen = mayFreeze && !(v & 4u);
     }
-
-    // ---- 2. stage U_s: every thread's entries, all loads in flight together
-    const uint32_t* un = a.uni + (size_t)c * a.ucap + a.uoff;
-    float           pmax;
-    {
+    int      iteration = 0;
+    unsigned count = 0, stored = 0;
+    const float mi   = a.m[iS];
+    float    rho0    = mi; // fused XMass (xmassJLoop, hydro_ve/xmass_kern.hpp:50-79) of the final pass
+    bool     kept    = frozen;
+    uint32_t ue      = 0;
+    float    frzK    = -INFINITY; // this pass's freeze reference (1b)
+    const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
+                zr = (float)foldPbc(zi - oz, a.box, 2);
+    uint32_t* const ll = a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane;
+    //! stages n union entries (global indices list[0 .. n)) as float positions relative to the cluster origin and
+    //! masses; returns the largest |p|_1 over them (all loads of a thread in flight together)
+    auto stage = [&](const uint32_t* list, uint32_t n) -> float {
         constexpr int S = (kSkinCap + kB - 1) / kB; // every entry of a union up to kSkinCap
         uint32_t      js[S];
 #pragma unroll
         for (int q = 0; q < S; ++q)
         {
             // unconditional (clamped): a load under a condition is waited for at the branch merge
-            js[q] = un[min(threadIdx.x + q * kB, U ? U - 1u : 0u)];
+            js[q] = list[min(threadIdx.x + q * kB, n ? n - 1u : 0u)];
         }
         double px[S], py[S], pz[S];
         float  mq[S];
@@ -319,7 +353,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         for (int q = 0; q < S; ++q)
         {
             const uint32_t u = threadIdx.x + q * kB;
-            if (u < U)
+            if (u < n)
             {
                 const float fx = (float)foldPbc(px[q] - ox, a.box, 0);
                 const float fy = (float)foldPbc(py[q] - oy, a.box, 1);
@@ -331,21 +365,65 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         pm = waveMax(pm);
         if (lane == 0) s_red[wave] = pm;
         __syncthreads();
-        pmax = s_red[0];
+        float r = s_red[0];
         for (int w = 1; w < kClusterWaves; ++w)
-            pmax = fmaxf(pmax, s_red[w]);
+            r = fmaxf(r, s_red[w]);
+        return r;
+    };
+
+    if (frozen)
+    {
+        // ---- 2'/3'. the exact union staged, the fused XMass over the exact lists (count, h, lists unchanged)
+        ue = __builtin_amdgcn_readfirstlane(a.ucount[c]);
+        (void)stage(a.uni + (size_t)c * a.ucap, ue);
+        count  = valid ? a.nc[i] - 1u : 0u;
+        stored = min(count, a.ngmax);
+        if (a.xmOut && valid)
+        {
+            const float    hInv = 1.0f / hi, hInv2 = hInv * hInv;
+            const uint32_t nw = (stored + 1) >> 1, last = nw ? nw - 1 : 0u;
+            constexpr int  PF = kWalkPF;
+            uint32_t       nx[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u)
+                nx[u] = ll[(size_t)min((uint32_t)u, last) * kWave];
+            for (uint32_t w0 = 0; w0 < nw; w0 += PF)
+            {
+                uint32_t cw[PF];
+#pragma unroll
+                for (int u = 0; u < PF; ++u)
+                {
+                    cw[u] = nx[u];
+                    nx[u] = ll[(size_t)min(w0 + PF + u, last) * kWave];
+                }
+#pragma unroll
+                for (int u = 0; u < PF; ++u)
+                {
+                    const uint32_t w = w0 + u;
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2)
+                    {
+                        const float4 q  = s_rec[min(h2 ? cw[u] >> 16 : cw[u] & 0xffffu, (uint32_t)kSkinCap - 1u)];
+                        const float  dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
+                        const float  r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                        rho0 += keepOrZero(kernelWt(r2 * hInv2) * q.w, 2 * w + h2 < stored);
+                    }
+                }
+            }
+        }
     }
+    else
+    {
+
+    // ---- 2. stage U_s
+    const uint32_t* un   = a.uni + (size_t)c * a.ucap + a.uoff;
+    const float     pmax = stage(un, U);
 
     // ---- 3. walk the skin lists: count, mark the exact union, store the hits' U_s positions (rewritten in step 5)
-    const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
-                zr = (float)foldPbc(zi - oz, a.box, 2);
     const uint32_t  WS = nlocWords(a.ngmaxS);
     const uint32_t* sl = a.sloc + (size_t)gw * WS * kWave + lane;
-    uint32_t*       ll = a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane;
     const unsigned  ngmin     = a.ng0 / 4;
-    int             iteration = 0;
     bool            active    = valid;
-    unsigned        count     = 0, stored = 0;
     //! one pass over this lane's skin list in blocks of kWalkPF words (16 entries): begin(b) starts block b,
     //! visit(p, e, inr) takes entry e of the block (U_s position p; inr: the entry is in the list, else p is a valid
     //! position of no meaning), end(b) closes the block.  Every entry of a block is visited without a branch (a wave's
@@ -389,10 +467,10 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     //! t = |p - r|^2 - 4h^2 in float (p, r relative to the cluster origin), with the reference's double criterion
     //! where |t| may be rounding (the bound of sx_neighbors.hip's |p|^2 + |r|^2 - 2p.r form, which covers this one);
     //! r2 becomes the pair's r^2 (the fused XMass)
-    auto test = [&](uint32_t p, float4 q, bool inr, float& r2) -> bool {
+    auto test = [&](uint32_t p, float4 q, bool inr, float& r2, float& t) -> bool {
         const float dx = q.x - xr, dy = q.y - yr, dz = q.z - zr;
         r2             = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-        const float t  = r2 - r2f;
+        t              = r2 - r2f;
         bool        hit = t < 0.0f;
         // bitwise, not short-circuit: one branch per entry, around the (rare) double criterion
         if (inr & ((!safe) | (fabsf(t) <= tol)))
@@ -411,8 +489,8 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         }
         return inr & hit; // j != i: the build's skin list never holds the target itself
     };
-    const float mi   = a.m[iS];
-    float       rho0 = mi, hInv2 = 0; // fused XMass (xmassJLoop, hydro_ve/xmass_kern.hpp:50-79) of the final pass
+    float hInv2 = 0;
+    float tmin = INFINITY; // the final pass's smallest |t| over the walked entries (1b)
     while (true)
     {
         for (uint32_t u = threadIdx.x; u < U; u += kB)
@@ -443,11 +521,13 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         // vmcnt counts stores too, in order, so a store between the prefetch and its use would be waited for as well
         unsigned cnt = 0, st = 0;
         uint32_t bits = 0;
+        tmin = INFINITY;
         walk([&](uint32_t) { bits = 0; },
              [&](uint32_t p, int e, bool inr) {
                  const float4 q = s_rec[p];
-                 float        r2;
-                 const bool   hit  = test(p, q, inr, r2);
+                 float        r2, t;
+                 const bool   hit  = test(p, q, inr, r2, t);
+                 tmin = fminf(tmin, fabsf(t)); // entries past the list (repeated or clamped) only lower it
                  const bool   keep = hit & (cnt < a.ngmax); // the first ngmax hits in list order
                  // no branch: a miss marks the spare byte; rho0 + (+0) == rho0
                  s_hit[keep ? p : (uint32_t)kSkinCap] = 1;
@@ -484,6 +564,15 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         }
         if (!blockAny(again)) break;
     }
+    // the freeze reference of this pass (1b): g = min((min |t| - tol) / (R + 2h), R - 2h) bounds every entry's
+    // distance to the 2h sphere from below -- |r - 2h| = |r^2 - 4h^2| / (r + 2h) for an entry within the skin radius R
+    // (|t| is within tol of |r^2 - 4h^2|), at least R - 2h beyond it; only lanes whose test was the float one (safe)
+    // and whose h did not iterate
+    if (valid && safe && iteration == 0)
+    {
+        const float g = fminf(fmaxf(0.0f, tmin - tol) / ((Ri + 2.0f * hi) * (1.0f + 0x1p-20f)), Ri - 2.0f * hi);
+        frzK          = (g * (1.0f - 0x1p-20f) + di + A) * (1.0f - 0x1p-22f);
+    }
 
     // ---- 4b. every target kept the same hits as the pass that wrote this cluster's exact lists: the union and lists
     //          in place are this step's (the skin lists are fixed between builds, so equal bits are equal sets)
@@ -493,7 +582,6 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
         const uint32_t lo = s_bm[2 * k][threadIdx.x];
         return 2 * k + 1 < nbl ? lo | ((uint32_t)s_bm[2 * k + 1][threadIdx.x] << 16) : lo;
     };
-    bool kept = false;
     if (hm && a.keepLists && !a.fresh && a.same[c])
     {
         constexpr int MW = (kWalkBlocks + 1) / 2;
@@ -510,7 +598,7 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     }
 
     // ---- 5. exact union: ranks of the hit U_s entries (U_s order), the union at the slot's start, lists rewritten
-    uint32_t ue = kept ? __builtin_amdgcn_readfirstlane(a.ucount[c]) : 0u;
+    ue = kept ? __builtin_amdgcn_readfirstlane(a.ucount[c]) : 0u;
     if (!kept)
     {
         // every thread a run of consecutive entries
@@ -573,11 +661,15 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
             if (threadIdx.x == 0) a.same[c] = 1;
         }
     }
+    } // not frozen
 
     // ---- 6. outputs
     if (valid)
     {
-        a.nc[i] = count + 1;
+        if (!frozen)
+        {
+            a.nc[i] = count + 1; // (a frozen cluster's count is the one in place)
+        }
         if (a.iterateH) a.h[i] = hi;
         if (a.rxOut) a.rxOut[i] = RecX{xi, yi, zi, hi, a.m[i]};
         if (a.fresh) a.hb[i] = h0;
@@ -602,19 +694,30 @@ __global__ __launch_bounds__(kB) void skinFilterKernel(SkinArgs a, uint32_t numC
     const unsigned           maxCnt = waveMax(valid ? count : 0u);
     const unsigned long long nst    = waveSum((unsigned long long)(valid ? stored : 0u));
     const unsigned long long walked = waveSum((unsigned long long)scount);
+    // the freeze reference of a walked pass (1b): the cluster's minima of K_i +- 2h_i
+    const float kp = waveMin(valid ? frzK + 2.0f * hi : INFINITY), km = waveMin(valid ? frzK - 2.0f * hi : INFINITY);
     if (lane == 0)
     {
         if (nfail) atomicAdd(&a.stats[1], nfail);
-        s_cst[wave] = make_uint4(maxCnt, (uint32_t)nst, (uint32_t)walked, 0u);
+        // (LDS: 40960 B is exactly a quarter of the CU's, four workgroups; no byte more)
+        s_cst[wave]  = make_uint4(maxCnt, (uint32_t)nst, (uint32_t)walked, __float_as_uint(kp));
+        s_wsum[wave] = __float_as_uint(km);
     }
     __syncthreads();
     if (threadIdx.x == 0)
     {
+        if (a.frz && !frozen)
+        {
+            float2 f = make_float2(__uint_as_float(s_cst[0].w), __uint_as_float(s_wsum[0]));
+            for (int w = 1; w < kClusterWaves; ++w)
+                f.x = fminf(f.x, __uint_as_float(s_cst[w].w)), f.y = fminf(f.y, __uint_as_float(s_wsum[w]));
+            a.frz[c] = f;
+        }
         uint4 t = s_cst[0];
         for (int w = 1; w < kClusterWaves; ++w)
             t.x = max(t.x, s_cst[w].x), t.y += s_cst[w].y, t.z += s_cst[w].z;
-        t.y |= kept ? 0x80000000u : 0u; // (stored entries < 2^31)
-        t.w          = ue;
+        t.y |= (kept ? 0x80000000u : 0u) | (frozen ? 0x40000000u : 0u); // (stored entries < 2^30)
+        t.w          = ue; // (replaces the freeze minimum)
         a.clStats[c] = t;
     }
 }

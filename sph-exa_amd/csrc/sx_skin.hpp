@@ -86,6 +86,11 @@ struct SkinArgs
     uint32_t*       hitMask;
     uint8_t*        same;
     int             keepLists;
+    // nullable: per cluster the freeze reference of the last pass that walked its skin lists, the minima over its
+    // targets of K_i + 2 h_i and K_i - 2 h_i with K_i = g_i + d_i + A_C, g_i bounding every skin entry's distance to
+    // the target's 2h sphere then (-inf: never frozen).  A cluster whose targets have all moved, and whose h have
+    // changed, less than that since (keepLists, same) is FROZEN: its exact lists stand, the skin lists are not walked
+    float2*         frz;
     DevBox          box;
     const float*    powTab;
     // nullable: the fused XMass (xmassJLoop on the final lists, as sx_hydro_cluster.hip's xmassKernel): xm of every

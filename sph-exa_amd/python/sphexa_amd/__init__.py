@@ -657,13 +657,14 @@ class Sim:
         self.ctx.check(self.L.sx_sim_rebuild_lists(self.h), "rebuild_lists")
 
     def skin_stats(self):
-        out = (C.c_uint64 * 12)()
+        out = (C.c_uint64 * 13)()
         self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
         d = dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
                       "capacity", "plain_steps"], list(out)[:8]))
         d["factor"], d["next_factor"] = out[8] * 1e-6, out[9] * 1e-6
         d["resyncs"] = out[10]
         d["kept_clusters"] = out[11]
+        d["frozen_clusters"] = out[12]
         return d
 
     def neighbor_sets(self):

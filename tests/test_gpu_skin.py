@@ -113,6 +113,41 @@ def test_skin_quiescent_lattice_reuses(ctx):
         sim.close()
 
 
+def test_skin_frozen_steps_equal_fresh_search(ctx):
+    """a lattice at rest: its h follows nc from shell to shell, so the hit sets change together on some steps and stand
+    still on others; on those the filter proves from the last walk's margins that no entry can have crossed its 2h
+    sphere and keeps the exact lists without walking the skin lists (frozen clusters, sx_skin.hpp SkinArgs::frz).
+    Every step's nc, h and neighbor sets equal a fresh sync + search of the same state, and xm (the frozen path's
+    XMass over the exact lists) agrees with the fresh step's to float rounding"""
+    st, obox = po.sedov_state(20)
+    st.temp[:] = st.temp.min()
+    box = gutil.box_to_sx(obox)
+    a = sx.Sim(ctx, st.n, box)
+    a.set_skin(0.05, 24)
+    b = sx.Sim(ctx, st.n, box)
+    b.set_skin(0.0, 1)
+    a.set_state(st.arrays, st.minDt, st.minDt_m1)
+    try:
+        for s in range(12):
+            g = a.get(STATE)
+            sc = a.scalars()
+            b.set_state(g, sc["minDt"], sc["minDt_m1"])
+            a.step()
+            b.step()
+            ga, gb = a.get(["id", "nc", "h", "xm"]), b.get(["id", "nc", "h", "xm"])
+            oa, ob = np.argsort(ga["id"]), np.argsort(gb["id"])
+            assert np.array_equal(ga["nc"][oa], gb["nc"][ob]) and np.array_equal(ga["h"][oa], gb["h"][ob]), s
+            np.testing.assert_allclose(ga["xm"][oa], gb["xm"][ob], rtol=2e-6, err_msg=str(s))
+            na, nb = a.neighbor_sets(), b.neighbor_sets()
+            assert all(np.array_equal(na[k], nb[k]) for k in na), s
+        ks = a.skin_stats()
+        print(ks)
+        assert ks["frozen_clusters"] > 0 and ks["kept_clusters"] >= ks["frozen_clusters"], ks
+    finally:
+        a.close()
+        b.close()
+
+
 def test_skin_with_gravity_matches_fresh_tree(ctx):
     """self-gravity on filter-served steps (sx_sim.cpp: the last sync's tree, multipoles from the current positions,
     MAC boxes refreshed to hold each node's cell and its particles): each step's accelerations and potential energy
