@@ -12,6 +12,19 @@ namespace sx
 {
 
 //! arguments shared by the neighbor-list pair kernels (one wavefront per 64-particle block of [first,last))
+//! computeEOS_Impl (hydro_ve/eos.hpp:52-77) fused into the producer of kx and gradh (cluster VeDefGradh): the same
+//! arithmetic as eosKernel per computed target, its records included; temp == nullptr: not fused
+struct EosFuse
+{
+    const double* temp;
+    double        cv;    // (double)idealGasCv(mui, gamma)
+    double        gamma;
+    float *       prho, *c;
+    const float * vx, *vy, *vz, *alpha;
+    RecV*         rvOut;
+    RecT*         rtOut;
+};
+
 struct PairArgs
 {
     uint32_t first, last, numGroups, ngmax;
@@ -72,6 +85,8 @@ struct PairArgs
     // cluster kernels, 0 = unknown: an upper bound of every cluster's union size (the search's statistics, read by
     // the host once the search has finished); AV switches skips its large-union launch when no union needs it
     uint32_t unionMax;
+    // cluster VeDefGradh only (full views): EOS of every computed target in its epilogue
+    EosFuse eos;
 };
 
 //! IAD tail shared by the VE and std IAD kernels (iad_kern.hpp:84-108, hydro_std/iad_kern.hpp:54-76): exponent

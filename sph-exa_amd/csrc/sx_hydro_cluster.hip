@@ -386,8 +386,22 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
                            ((double)kxi - K * (double)xmassi * (double)h3Inv) * (double)wrho0i);
         const float rhoi   = kxi * ri.m / xmassi;
         const float dhdrho = -ri.h / (rhoi * 3.0f);
+        const float gradhi = 1.0f - dhdrho * whomegai;
         a.kx[cu.i]         = kxi;
-        a.gradh[cu.i]      = 1.0f - dhdrho * whomegai;
+        a.gradh[cu.i]      = gradhi;
+        if (a.eos.temp)
+        {
+            // eosKernel's arithmetic (sx_hydro.hip: computeEOS_Impl, idealGasEOS) on the values just computed
+            const EosFuse& e    = a.eos;
+            const double   tmp  = e.cv * e.temp[cu.i] * (e.gamma - 1.0);
+            const double   pi   = (double)rhoi * tmp;
+            const double   ci   = sqrt(tmp);
+            const float    prho = (float)(pi / (double)(kxi * ri.m * ri.m * gradhi));
+            e.prho[cu.i]        = prho;
+            e.c[cu.i]           = (float)ci;
+            e.rvOut[cu.i]       = RecV{e.vx[cu.i], e.vy[cu.i], e.vz[cu.i], (float)ci};
+            e.rtOut[cu.i]       = RecT{xmassi, kxi, prho, e.alpha[cu.i]};
+        }
     }
 }
 

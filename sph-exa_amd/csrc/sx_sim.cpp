@@ -2540,6 +2540,11 @@ extern "C"
             // ---- [xm] halos, VeDefGradh (overlapped: interior clusters while the halos are in flight)
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             SIM_HIP(hipEventRecord(s->kev[4], st));
+            // the cluster VeDefGradh also runs the EOS of its targets (PairArgs::eos): kx and gradh stay in registers
+            PairArgs va = pa;
+            if (fused)
+                va.eos = EosFuse{s->temp,  (double)idealGasCv(s->p.muiConst, s->p.gamma), s->p.gamma, s->prho, s->c,
+                                 s->vx,    s->vy, s->vz, s->alpha, s->rv, s->rt};
             if (int e = exchangeThen(
                     s, H, {{s->xm, 4}},
                     [&](size_t a, size_t b)
@@ -2547,19 +2552,17 @@ extern "C"
                         halo(a, b, [&](size_t u, size_t v)
                              { packT(v - u, s->xm + u, nullptr, nullptr, nullptr, s->rt + u, st); });
                     },
-                    [&](const PairArgs& p) { H.veDefGradh(p, st); }, pa, st))
+                    [&](const PairArgs& p) { H.veDefGradh(p, st); }, va, st))
                 return e;
             SIM_HIP(hipEventRecord(s->kev[5], st));
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
-            // ---- EOS, then the v/prho/c/kx halo exchange
-            EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx, s->xm,
-                       s->gradh, s->prho, s->c, nullptr, nullptr};
-            if (fused)
+            // ---- EOS (unless fused above), then the v/prho/c/kx halo exchange
+            if (!fused)
             {
-                ea.vx = s->vx, ea.vy = s->vy, ea.vz = s->vz, ea.alpha = s->alpha;
-                ea.rvOut = s->rv, ea.rtOut = s->rt; // the locals' {v, c} and {xm, kx, prho, alpha} records
+                EosArgs ea{(uint32_t)s->first, (uint32_t)s->last, s->p.muiConst, s->p.gamma, s->temp, s->m, s->kx,
+                           s->xm, s->gradh, s->prho, s->c, nullptr, nullptr};
+                H.eos(ea, st);
             }
-            H.eos(ea, st);
             SIM_HIP(hipEventRecord(s->ev[ev++], st));
             // ---- [v, prho, c, kx] halos, IAD + divv/curlv, rho time-step
             auto packVT = [&](size_t a, size_t b)
