@@ -373,7 +373,7 @@ def main():
     ctx.sync()
     barrier()
     skin0 = sim.skin_stats()
-    stage_sum, kern_sum = {}, {}
+    stage_sum, kern_sum, kern_steps = {}, {}, {}
     step_s = []  # host time of every timed step (sx_sim_step returns after its stream synchronisation)
     search_ms, kept_steps = [], []  # per step: the search slot's kernel time, clusters whose exact lists were kept
     # (of them frozen)
@@ -388,6 +388,8 @@ def main():
         kt = sim.kernel_times()
         for k, v in kt.items():
             kern_sum[k] = kern_sum.get(k, 0.0) + v
+            if v > 0.0:
+                kern_steps.setdefault(k, []).append(round(v, 2))
         search_ms.append(round(kt.get("findNeighbors", 0.0), 3))
         if args.skin > 0:
             ks = sim.skin_stats()
@@ -546,6 +548,9 @@ def main():
         "kernels_ms": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_ms.items()
                        if not std_prop or k in STD_KERNEL_NAMES},
         "stages_ms": {k: v / args.steps for k, v in stage_sum.items()},
+        # per timed step (the lattice's h moves across a shell every other step: 92- and 122-neighbor steps differ)
+        "kernels_ms_per_step": {(STD_KERNEL_NAMES.get(k) if std_prop else k): v for k, v in kern_steps.items()
+                                if not std_prop or k in STD_KERNEL_NAMES},
         "neighbors_per_particle": ng,
         "candidates_per_particle": stats["sumCandidates"] / max(1, n_local),
         "union_per_particle": union_pp,

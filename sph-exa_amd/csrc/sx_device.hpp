@@ -27,6 +27,19 @@ __host__ __device__ constexpr uint32_t nlocWords(uint32_t ngmax) { return (ngmax
 //! union capacity per cluster: every union entry is a stored neighbor of at least one of its targets
 __host__ __device__ constexpr uint32_t unionCap(uint32_t ngmax) { return kCluster * ngmax; }
 
+//! the skin filter's second set of exact lists (sx_skin.hpp, round 6): per cluster c, bit kListsBSel of sel[c]
+//! selects this set's nloc / uni[c*ucap + uoff] / ucount[c] instead of the primary ones (the filter keeps the last two
+//! different hit sets of every cluster: a lattice's h moves between two shells).  sel == nullptr: the primary set
+struct ListsB
+{
+    const uint8_t*  sel;
+    const uint32_t* nloc;
+    const uint32_t* ucount;
+    uint32_t        uoff;
+};
+constexpr uint8_t kListsBSel = 4; //!< sel bit: the second set is current (bits 0 / 1: set A / B valid, the filter's)
+__host__ __device__ inline bool listsB(const ListsB& b, uint32_t c) { return b.sel && (b.sel[c] & kListsBSel); }
+
 //! box data as the kernels need it (cstone::Box<double>, sfc/box.hpp:111-191)
 struct DevBox
 {

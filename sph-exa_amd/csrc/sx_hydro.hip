@@ -41,9 +41,11 @@ constexpr bool kFastClusters = SX_STR(SX_VARIANT)[0] == 'f';
         unsigned c1 = a.nc[i] - 1;                                                                                     \
         cnt         = c1 < a.ngmax ? c1 : a.ngmax;                                                                     \
     }                                                                                                                  \
-    const uint32_t* nb = a.localLists ? a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane                       \
+    const bool      lB = a.localLists && gw < a.numGroups && listsB(a.lb, gw / kClusterWaves);                       \
+    const uint32_t* nb = a.localLists ? (lB ? a.lb.nloc : a.nloc) + (size_t)gw * nlocWords(a.ngmax) * kWave + lane    \
                                       : a.nidx + (size_t)gw * a.ngmax * kWave + lane;                                 \
-    const uint32_t* un = a.localLists ? a.uni + (size_t)(gw / kClusterWaves) * a.ucap : nullptr;                       \
+    const uint32_t* un = a.localLists ? a.uni + (size_t)(gw / kClusterWaves) * a.ucap + (lB ? a.lb.uoff : 0u)        \
+                                      : nullptr;                                                                       \
     auto nbj = [&](unsigned k) -> uint32_t {                                                                           \
         if (!a.localLists) return nb[(size_t)k * kWave];                                                               \
         uint32_t w = nb[(size_t)(k >> 1) * kWave];                                                                     \

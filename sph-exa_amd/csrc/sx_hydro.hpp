@@ -36,6 +36,7 @@ struct PairArgs
     const uint32_t* uni;
     const uint32_t* ucount;
     uint32_t        ucap;
+    ListsB          lb;   // the second set of cluster lists (sx_device.hpp); lb.sel == nullptr: none
     const uint32_t* nc;   // includes self
     const RecX*     rx;
     const RecV*     rv;

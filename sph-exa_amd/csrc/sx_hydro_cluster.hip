@@ -98,9 +98,10 @@ __device__ __forceinline__ Clu setup(const PairArgs& a, float* s_red)
     const uint32_t nw = (cu.cnt + 1) >> 1;
     cu.wBeg           = nw * cu.part / SPLIT;
     cu.wEnd           = nw * (cu.part + 1) / SPLIT;
-    cu.U              = a.ucount[cu.c];
-    cu.un             = a.uni + (size_t)cu.c * a.ucap;
-    cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
+    const bool lB     = listsB(a.lb, cu.c); // the cluster's current set of lists
+    cu.U              = lB ? a.lb.ucount[cu.c] : a.ucount[cu.c];
+    cu.un             = a.uni + (size_t)cu.c * a.ucap + (lB ? a.lb.uoff : 0u);
+    cu.nl             = (lB ? a.lb.nloc : a.nloc) + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
     const RecX o      = a.rx[c0];
     cu.ox = o.x, cu.oy = o.y, cu.oz = o.z;
 
@@ -645,7 +646,8 @@ __global__ __launch_bounds__(kB * SPLIT) void avSwitchesKernel(PairArgs a)
     {
         // one of the two capacity launches (avSwitches): this workgroup's cluster belongs to the other one
         const uint32_t blk = xcdBlock(blockIdx.x, gridDim.x);
-        const uint32_t U   = a.ucount[a.clusterList ? a.clusterList[blk] : blk];
+        const uint32_t cc  = a.clusterList ? a.clusterList[blk] : blk;
+        const uint32_t U   = listsB(a.lb, cc) ? a.lb.ucount[cc] : a.ucount[cc];
         if (U < (uint32_t)UMIN || (UMAX > 0 && U > (uint32_t)UMAX)) return;
     }
     const Clu   cu  = setup<SPLIT>(a, s_red);
@@ -775,6 +777,7 @@ struct MePre
     static constexpr int NT = kB * SPLIT, S = (CH + NT - 1) / NT;
     static constexpr int SP = S < 2 ? S : 2; // slots whose records are prefetched (registers); the rest load at staging
     uint32_t c, U;
+    bool     lB; // the cluster's second set of lists is current (sx_device.hpp ListsB)
     uint32_t nc;
     uint8_t  act;
     RecX     o; // the cluster origin (its first particle)
@@ -845,7 +848,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
     auto prefetch = [&](uint32_t c) {
         Pre p;
         p.c = c;
-        p.U = 0, p.nc = 1, p.act = 1;
+        p.U = 0, p.nc = 1, p.act = 1, p.lB = false;
 #pragma unroll
         for (int s = 0; s < S; ++s)
             p.js[s] = 0u;
@@ -853,7 +856,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         const uint32_t c0 = __builtin_amdgcn_readfirstlane(a.first + c * kCluster), i = c0 + tid;
         const bool     in = c * kClusterWaves + sub < a.numGroups && i < a.last;
         const uint32_t iL = in ? i : c0;
-        p.U               = a.ucount[c];
+        p.lB              = listsB(a.lb, c);
+        p.U               = p.lB ? a.lb.ucount[c] : a.ucount[c];
         p.o               = a.rx[c0];
         p.nc              = in ? a.nc[i] : 1u;
         p.act             = (in && a.active) ? a.active[i] : (uint8_t)1;
@@ -863,7 +867,7 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
             p.gi[0] = a.dV11[iL], p.gi[1] = a.dV12[iL], p.gi[2] = a.dV13[iL];
             p.gi[3] = a.dV22[iL], p.gi[4] = a.dV23[iL], p.gi[5] = a.dV33[iL];
         }
-        const uint32_t* un = a.uni + (size_t)c * a.ucap;
+        const uint32_t* un = a.uni + (size_t)c * a.ucap + (p.lB ? a.lb.uoff : 0u);
 #pragma unroll
         for (int s = 0; s < S; ++s)
         {
@@ -912,8 +916,8 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumEnergyKernel(PairArgs a, u
         cu.wBeg           = nw * cu.part / SPLIT;
         cu.wEnd           = nw * (cu.part + 1) / SPLIT;
         cu.U              = cur.U;
-        cu.un             = a.uni + (size_t)cu.c * a.ucap;
-        cu.nl             = a.nloc + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
+        cu.un             = a.uni + (size_t)cu.c * a.ucap + (cur.lB ? a.lb.uoff : 0u);
+        cu.nl             = (cur.lB ? a.lb.nloc : a.nloc) + (size_t)cu.gw * nlocWords(a.ngmax) * kWave + lane;
         const RecX o      = cur.o;
         cu.ox = o.x, cu.oy = o.y, cu.oz = o.z;
         // lanes outside the view read the cluster's first particle, as setup<SPLIT> does
@@ -1226,6 +1230,9 @@ __global__ __launch_bounds__(kB * SPLIT) void momentumStdKernel(PairArgs a)
 #ifndef SX_SPLIT_IAD
 #define SX_SPLIT_IAD 2
 #endif
+#ifndef SX_SPLIT_AV_LARGE
+#define SX_SPLIT_AV_LARGE 3 // the 2048-record launch runs two workgroups per CU: three shares keep six waves per SIMD
+#endif
 #ifndef SX_SPLIT_AV
 #define SX_SPLIT_AV 2
 #endif
@@ -1270,7 +1277,7 @@ void avSwitches(const PairArgs& a, hipStream_t s)
     if (!a.numGroups || !clusters(a)) return;
     avSwitchesKernel<kChAv, SX_SPLIT_AV, 0, kChAv><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
     if (a.unionMax == 0 || a.unionMax > (uint32_t)kChAv) // else every workgroup of it would exit after one load
-        avSwitchesKernel<kChAvLarge, SX_SPLIT_AV, kChAv + 1, 0><<<clusters(a), kB * SX_SPLIT_AV, 0, s>>>(a);
+        avSwitchesKernel<kChAvLarge, SX_SPLIT_AV_LARGE, kChAv + 1, 0><<<clusters(a), kB * SX_SPLIT_AV_LARGE, 0, s>>>(a);
 }
 //! min over the per-workgroup Courant time-steps of one launch -> *minDt (one atomic)
 __global__ __launch_bounds__(1024) void reduceBlockDtKernel(const float* v, uint32_t n, float* minDt)

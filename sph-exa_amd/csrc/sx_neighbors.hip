@@ -1098,8 +1098,9 @@ __global__ void exportKernel(NsArgs a, uint32_t* out)
         {
             if (a.localLists)
             {
-                uint32_t w = a.nloc[((size_t)g * W + k / 2) * kWave + lane];
-                j          = a.uni[(size_t)c * a.ucap + ((k & 1) ? (w >> 16) : (w & 0xffffu))];
+                const bool lB = listsB(a.lb, c);
+                uint32_t   w  = (lB ? a.lb.nloc : a.nloc)[((size_t)g * W + k / 2) * kWave + lane];
+                j = a.uni[(size_t)c * a.ucap + (lB ? a.lb.uoff : 0u) + ((k & 1) ? (w >> 16) : (w & 0xffffu))];
             }
             else { j = a.nidx[((size_t)g * a.ngmax + k) * kWave + lane]; }
         }

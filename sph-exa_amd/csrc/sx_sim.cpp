@@ -630,6 +630,7 @@ void allocFields(sx_sim* s, size_t cap)
 PairArgs simPairArgs(sx_sim* s)
 {
     PairArgs a{};
+    a.lb             = s->skin.lb; // the step's second set of lists (skin filter), or none
     a.first          = (uint32_t)s->first;
     a.last           = (uint32_t)s->last;
     a.numGroups      = (uint32_t)((s->last - s->first + kGroupSize - 1) / kGroupSize);
@@ -817,17 +818,20 @@ int sortLocals(sx_sim* s, size_t nl, hipStream_t st)
 //! interior / boundary clusters: a cluster is interior when no entry of its neighbor union is a halo (outside
 //! [first, last)).  One wave per cluster; the lists are compacted with one atomic per cluster (order is free: every
 //! cluster is computed independently)
-__global__ void classifyClustersKernel(const uint32_t* uni, const uint32_t* ucount, uint32_t ucap, uint32_t first,
-                                       uint32_t last, uint32_t numClusters, uint32_t* lists, uint32_t* counts)
+__global__ void classifyClustersKernel(const uint32_t* uni, const uint32_t* ucount, uint32_t ucap, ListsB lb,
+                                       uint32_t first, uint32_t last, uint32_t numClusters, uint32_t* lists,
+                                       uint32_t* counts)
 {
     const uint32_t c    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     if (c >= numClusters) return;
     // an overflowed union (ucount > ucap, stats bit 8, reported as an error after the step) is only partly stored:
     // read what is there and treat the cluster as boundary
-    const uint32_t  U = min(ucount[c], ucap);
-    const uint32_t* u = uni + (size_t)c * ucap;
-    bool            halo = ucount[c] > ucap;
+    const bool      lB = listsB(lb, c);
+    const uint32_t  uc = lB ? lb.ucount[c] : ucount[c];
+    const uint32_t  U  = min(uc, ucap);
+    const uint32_t* u  = uni + (size_t)c * ucap + (lB ? lb.uoff : 0u);
+    bool            halo = uc > ucap;
     for (uint32_t k = lane; k < U; k += 64)
     {
         const uint32_t j = u[k];
@@ -1691,8 +1695,15 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint32_t*   hmask = s->mem.get<uint32_t>("skin.hitmask", na.numGroups * (size_t)kSkinMaskWords * kWave);
     uint8_t*    same  = s->mem.get<uint8_t>("skin.same", ncl);
     float2*     frz   = s->mem.get<float2>("skin.frz", ncl);
+    // the second set of exact lists (SkinArgs::nlocB): its union in the slot's second quarter, below the skin union
+    const bool  twoSets = na.ucap / 4 >= (uint32_t)kSkinCap && !getenv("SX_SKIN_ONESET");
+    uint32_t*   nlocB = twoSets ? s->mem.get<uint32_t>("skin.nlocB", na.numGroups * (size_t)nlocWords(na.ngmax) * kWave)
+                                : nullptr;
+    uint32_t*   ucB   = twoSets ? s->mem.get<uint32_t>("skin.ucountB", ncl) : nullptr;
+    uint32_t*   hmB   = twoSets ? s->mem.get<uint32_t>("skin.hitmaskB", na.numGroups * (size_t)kSkinMaskWords * kWave)
+                                : nullptr;
     if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk ||
-        !hmask || !same || !frz)
+        !hmask || !same || !frz || (twoSets && (!nlocB || !ucB || !hmB)))
         return SX_ERR_NOMEM;
 
     const SkinGrid g = skinGrid(s->dbox);
@@ -1714,9 +1725,10 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     // this simulation left (no other search or allocation since)
     fa.hitMask   = hmask;
     fa.same      = same;
+    fa.nlocB = nlocB, fa.ucountB = ucB, fa.hitMaskB = hmB, fa.uoffB = na.ucap / 4;
     fa.frz       = getenv("SX_SKIN_NOFREEZE") ? nullptr : frz; // (A/B: every reuse step walks its skin lists)
     fa.keepLists = reuse && K.listsKept && K.keptNloc == na.nloc && K.keptUni == na.uni && K.keptMask == hmask &&
-                   K.keptSame == same && K.keptFrz == frz;
+                   K.keptSame == same && K.keptFrz == frz && K.keptNlocB == nlocB;
     K.listsKept  = false; // until this search completes
 
     // the skin build: the search with radii 2 h (1 + s), no h iteration, skin lists and counts as its outputs
@@ -1804,6 +1816,9 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     }
     SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
     K.listsKept = true, K.keptNloc = na.nloc, K.keptUni = na.uni, K.keptMask = hmask, K.keptSame = same, K.keptFrz = frz;
+    K.keptNlocB = nlocB;
+    // the pair kernels read each cluster's current set
+    K.lb = twoSets ? ListsB{same, nlocB, ucB, na.ucap / 4} : ListsB{};
     if (getenv("SX_SKIN_DEBUG"))
     {
         uint32_t f = 0;
@@ -2036,6 +2051,7 @@ extern "C"
         NsArgs a{};
         a.first = (uint32_t)s->first, a.last = (uint32_t)s->last, a.ngmax = s->p.ngmax, a.nc = s->nc;
         a.setLists(s->nb);
+        a.lb = s->skin.lb; // the lists the last step's pair kernels read
         hipStream_t st = (hipStream_t)sx_ctx_stream_internal(s->ctx);
         SIM_HIP(exportNeighbors(a, out, st));
         SIM_HIP(hipStreamSynchronize(st));
@@ -2333,6 +2349,7 @@ extern "C"
                 x.policy = &pol;
                 const int R  = std::max(1, atoi(reps));
                 s->skin.listsKept = false; // this search rewrites the exact lists
+                s->skin.lb        = ListsB{};
                 SIM_HIP(hipEventRecord(s->kev[0], st));
                 for (int r = 0; r < R; ++r)
                 {
@@ -2378,6 +2395,7 @@ extern "C"
             {
                 s->skin.xmFused   = false;
                 s->skin.listsKept = false;
+                s->skin.lb        = ListsB{}; // the plain search writes the primary set
                 SIM_HIP(findNeighbors(na, st));
             }
             SIM_HIP(hipEventRecord(s->kev[1], st));
@@ -2427,8 +2445,9 @@ extern "C"
                 SIM_HIP(hipMemsetAsync(s->clsCount, 0, 8, st));
                 if (ncl)
                     classifyClustersKernel<<<(ncl + 3) / 4, 256, 0, st>>>(s->nb.uni, s->nb.ucount, s->nb.ucap,
-                                                                         (uint32_t)s->first, (uint32_t)s->last, ncl,
-                                                                         s->clsList, s->clsCount);
+                                                                         s->skin.lb, (uint32_t)s->first,
+                                                                         (uint32_t)s->last, ncl, s->clsList,
+                                                                         s->clsCount);
                 SIM_HIP(hipMemcpyAsync(s->clsHost, s->clsCount, 8, hipMemcpyDeviceToHost, st));
             }
             if (int e = syncErrEnqueue(s, st)) return e;

@@ -94,8 +94,11 @@ struct SkinState
     // the exact lists, hit masks and per-cluster flags the last skin search left (SkinArgs::keepLists), and the
     // clusters whose lists a reuse step kept (statistics)
     bool      listsKept{false};
-    const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr}, *keptFrz{nullptr};
+    const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr}, *keptFrz{nullptr},
+        *keptNlocB{nullptr};
     uint64_t  keptClusters{0}, frozenClusters{0};
+    // the step's second set of exact lists (sel == nullptr unless the step's search was the skin filter)
+    sx::ListsB lb{};
 };
 
 } // namespace sx::sim

@@ -28,7 +28,6 @@ namespace sx
 namespace
 {
 
-constexpr int kSkinCap = 1920; //!< U_s entries staged (16 B each; a larger skin union takes the exact search)
 constexpr int kWalkPF  = 8;    //!< skin-list words per walk block (16 entries: one u16 of hit bits per lane)
 //! walk blocks per lane at the largest skin-list capacity (256 entries)
 constexpr int kWalkBlocks = (nlocWords(256) + kWalkPF - 1) / kWalkPF;
@@ -168,7 +167,7 @@ __device__ __forceinline__ void pushStale(const SkinArgs& a, uint32_t c)
     uint32_t* L = (a.direct && a.streak && a.streak[c]) ? a.direct : a.stale;
     L[1 + atomicAdd(&L[0], 1u)] = c;
     if (a.streak) a.streak[c] = 1;
-    if (a.same) a.same[c] = 0; // its lists are rewritten by a rebuild or the exact search
+    if (a.same) a.same[c] = 0; // its lists are rewritten by a rebuild or the exact search (into set A)
 }
 static_assert((kWalkBlocks + 1) / 2 <= (int)kSkinMaskWords, "hit-mask words per target");
 
@@ -212,7 +211,11 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
     const uint32_t U      = __builtin_amdgcn_readfirstlane(a.ucountS[c]);
     const float    kEps   = 0x1p-16f;
     // the freeze reference (1b), loaded with the target's state: its latency off the vote's chain
-    const bool     mayFreeze = a.frz && a.keepLists && !a.fresh && a.same[c];
+    // the cluster's list sets (SkinArgs::same): the current one (B with a second set and its bit), which hold lists
+    const uint32_t lstate    = (a.same && a.keepLists && !a.fresh) ? (uint32_t)a.same[c] : 0u;
+    const uint32_t lcur      = (a.nlocB && (lstate & kListsBSel)) ? 1u : 0u;
+    const bool     curValid  = ((lstate >> lcur) & 1u) != 0;
+    const bool     mayFreeze = a.frz && curValid;
     const float2   fref      = mayFreeze ? a.frz[c] : make_float2(-INFINITY, -INFINITY);
     //! per bit k of v: whether any thread of the workgroup set it (one vote round for several decisions)
     auto           blockBits = [&](uint32_t v) -> uint32_t {
@@ -331,7 +334,15 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
     float    frzK    = -INFINITY; // this pass's freeze reference (1b)
     const float xr = (float)foldPbc(xi - ox, a.box, 0), yr = (float)foldPbc(yi - oy, a.box, 1),
                 zr = (float)foldPbc(zi - oz, a.box, 2);
-    uint32_t* const ll = a.nloc + (size_t)gw * nlocWords(a.ngmax) * kWave + lane;
+    //! set k's lists of this lane, union of this cluster, union count
+    auto setLists = [&](uint32_t k) { return (k ? a.nlocB : a.nloc) + (size_t)gw * nlocWords(a.ngmax) * kWave + lane; };
+    auto setUnion = [&](uint32_t k) { return a.uni + (size_t)c * a.ucap + (k ? a.uoffB : 0u); };
+    auto setCount = [&](uint32_t k) { return k ? a.ucountB + c : a.ucount + c; };
+    auto setMask  = [&](uint32_t k) {
+        uint32_t* m = k ? a.hitMaskB : a.hitMask;
+        return m ? m + (size_t)gw * kSkinMaskWords * kWave + lane : nullptr;
+    };
+    const uint32_t* const ll = setLists(lcur); // the current set's lists (the frozen path's XMass)
     //! stages n union entries (global indices list[0 .. n)) as float positions relative to the cluster origin and
     //! masses; returns the largest |p|_1 over them (all loads of a thread in flight together)
     auto stage = [&](const uint32_t* list, uint32_t n) -> float {
@@ -374,8 +385,8 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
     if (frozen)
     {
         // ---- 2'/3'. the exact union staged, the fused XMass over the exact lists (count, h, lists unchanged)
-        ue = __builtin_amdgcn_readfirstlane(a.ucount[c]);
-        (void)stage(a.uni + (size_t)c * a.ucap, ue);
+        ue = __builtin_amdgcn_readfirstlane(*setCount(lcur));
+        (void)stage(setUnion(lcur), ue);
         count  = valid ? a.nc[i] - 1u : 0u;
         stored = min(count, a.ngmax);
         if (a.xmOut && valid)
@@ -574,16 +585,15 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
         frzK          = (g * (1.0f - 0x1p-20f) + di + A) * (1.0f - 0x1p-22f);
     }
 
-    // ---- 4b. every target kept the same hits as the pass that wrote this cluster's exact lists: the union and lists
-    //          in place are this step's (the skin lists are fixed between builds, so equal bits are equal sets)
-    const uint32_t   nbl = valid ? (((scount + 1) >> 1) + kWalkPF - 1) / kWalkPF : 0u; // walk blocks of this lane
-    uint32_t* const  hm  = a.hitMask ? a.hitMask + (size_t)gw * kSkinMaskWords * kWave + lane : nullptr;
-    auto             maskWord = [&](uint32_t k) {
+    // ---- 4b. every target kept the same hits as the pass that wrote one of this cluster's list sets: that set is
+    //          this step's (the skin lists are fixed between builds, so equal bits are equal sets) -- the current one
+    //          (kept), or the other (the set becomes current: a lattice's h moving back to the last shell)
+    const uint32_t nbl = valid ? (((scount + 1) >> 1) + kWalkPF - 1) / kWalkPF : 0u; // walk blocks of this lane
+    auto           maskWord = [&](uint32_t k) {
         const uint32_t lo = s_bm[2 * k][threadIdx.x];
         return 2 * k + 1 < nbl ? lo | ((uint32_t)s_bm[2 * k + 1][threadIdx.x] << 16) : lo;
     };
-    if (hm && a.keepLists && !a.fresh && a.same[c])
-    {
+    auto sameBits = [&](const uint32_t* hm) -> bool {
         constexpr int MW = (kWalkBlocks + 1) / 2;
         const uint32_t nmw = (nbl + 1) >> 1;
         uint32_t       prev[MW];
@@ -594,11 +604,28 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
 #pragma unroll
         for (int k = 0; k < MW; ++k)
             if ((uint32_t)k < nmw) diff |= prev[k] != maskWord(k);
-        kept = !blockAny(diff);
+        return !blockAny(diff);
+    };
+    uint32_t lnew = lstate; // the cluster's list sets after this pass
+    uint32_t ltgt = lcur;   // the set this pass's lists are in
+    // the other set first: a walked (not frozen) step of a cluster that holds two sets mostly moves back to the other
+    // (a lattice's h crossing a shell: two such steps, then frozen ones); each comparison reads 32 B per target
+    const bool otherValid = a.nlocB && a.hitMask && ((lstate >> (1u - lcur)) & 1u);
+    if (otherValid && sameBits(setMask(1u - lcur)))
+    {
+        kept = true, ltgt = 1u - lcur;
+        lnew = (lstate & 3u) | (ltgt ? kListsBSel : 0u);
+    }
+    if (!kept && a.hitMask && curValid) kept = sameBits(setMask(lcur));
+    if (!kept)
+    {
+        // written into the other set (with a second one: the current set stays valid), or set A
+        ltgt = a.nlocB ? 1u - lcur : 0u;
+        lnew = (curValid && ltgt != lcur ? 1u << lcur : 0u) | (1u << ltgt) | (ltgt ? kListsBSel : 0u);
     }
 
-    // ---- 5. exact union: ranks of the hit U_s entries (U_s order), the union at the slot's start, lists rewritten
-    ue = kept ? __builtin_amdgcn_readfirstlane(a.ucount[c]) : 0u;
+    // ---- 5. exact union: ranks of the hit U_s entries (U_s order), the union at the set's start, lists rewritten
+    ue = kept ? __builtin_amdgcn_readfirstlane(*setCount(ltgt)) : 0u;
     if (!kept)
     {
         // every thread a run of consecutive entries
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
             run += s_wsum[w];
         for (int w = 0; w < kClusterWaves; ++w)
             ue += s_wsum[w];
-        uint32_t* ux = a.uni + (size_t)c * a.ucap;
+        uint32_t* ux = setUnion(ltgt);
         for (uint32_t u0 = b0; u0 < b1; u0 += 8)
         {
             uint32_t jj[8];
@@ -641,6 +668,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
     // pass B: the same walk, the first ngmax hits written as exact-union ranks (two per word); the hit bits recorded
     if (!kept)
     {
+        uint32_t* const lw = setLists(ltgt);
         unsigned st = 0;
         uint32_t pend = 0, bits = 0;
         walk([&](uint32_t b) { bits = s_bm[b][threadIdx.x]; },
@@ -648,19 +676,18 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
                  const bool     keep = ((bits >> e) & 1u) != 0;
                  const uint32_t r    = s_rank[p];
                  const bool     odd  = (st & 1u) != 0;
-                 if (keep && odd) ll[(size_t)(st >> 1) * kWave] = pend | (r << 16);
+                 if (keep && odd) lw[(size_t)(st >> 1) * kWave] = pend | (r << 16);
                  pend = (keep && !odd) ? r : pend;
                  st += keep ? 1u : 0u;
              },
              [](uint32_t) {});
-        if (st & 1u) ll[(size_t)(st >> 1) * kWave] = pend;
-        if (hm)
-        {
+        if (st & 1u) lw[(size_t)(st >> 1) * kWave] = pend;
+        if (uint32_t* const hm = setMask(ltgt))
             for (uint32_t k = 0; 2 * k < nbl; ++k)
                 hm[(size_t)k * kWave] = maskWord(k);
-            if (threadIdx.x == 0) a.same[c] = 1;
-        }
+        if (threadIdx.x == 0) *setCount(ltgt) = ue;
     }
+    if (threadIdx.x == 0 && a.same && lnew != lstate) a.same[c] = (uint8_t)lnew;
     } // not frozen
 
     // ---- 6. outputs
@@ -686,7 +713,6 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
     if (threadIdx.x == 0)
     {
         a.acc[c]    = a.fresh ? 0.0f : A;
-        a.ucount[c] = ue;
         if (a.streak && !a.fresh) a.streak[c] = 0; // served by its skin: a later stale step rebuilds it again
     }
     const unsigned           failed = (valid && a.iterateH && iteration >= 10) ? 1u : 0u;

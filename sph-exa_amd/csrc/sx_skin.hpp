@@ -38,6 +38,7 @@ namespace sx
 using SkinGrid = DispGrid; //!< per-step displacement maxima by cell (sx_device.hpp)
 
 constexpr int kSkinGridN = 64;
+constexpr int kSkinCap   = 1920; //!< U_s entries the filter stages (16 B each; a larger skin union takes the exact search)
 //! u32 words of kept-hit bits per target (SkinArgs::hitMask): one u16 per 16-entry walk block, up to 256 entries
 constexpr uint32_t kSkinMaskWords = 8;
 
@@ -86,6 +87,13 @@ struct SkinArgs
     uint32_t*       hitMask;
     uint8_t*        same;
     int             keepLists;
+    // nullable: the second set of exact lists (ListsB, sx_device.hpp; same[c] bits 0 / 1: set A / B holds the lists
+    // of its hit masks, bit kListsBSel: B is current).  A pass whose hits match the other set's makes that set current;
+    // one that matches neither writes its lists into the other set, so the last two different hit sets stay
+    uint32_t*       nlocB;
+    uint32_t*       ucountB;
+    uint32_t*       hitMaskB;
+    uint32_t        uoffB;
     // nullable: per cluster the freeze reference of the last pass that walked its skin lists, the minima over its
     // targets of K_i + 2 h_i and K_i - 2 h_i with K_i = g_i + d_i + A_C, g_i bounding every skin entry's distance to
     // the target's 2h sphere then (-inf: never frozen).  A cluster whose targets have all moved, and whose h have

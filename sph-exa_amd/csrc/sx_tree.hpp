@@ -204,6 +204,7 @@ struct NsArgs
     // uni[c*ucap + u] (global indices, stream order), ucount[c] = U, and per target the u16 positions into that
     // union, two per word: nloc[(group*nlocWords + k/2)*64 + lane]
     int             localLists;
+    ListsB          lb; // exportNeighbors only: the second set of cluster lists (sx_device.hpp)
     uint32_t*       nloc;
     uint32_t*       uni;
     uint32_t*       ucount;
