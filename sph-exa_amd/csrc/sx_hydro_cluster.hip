@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kB * SPLIT) void veDefGradhKernel(PairArgs a)
     __shared__ float  s_red[kClusterWaves * SPLIT];
     const Clu   cu     = setup<SPLIT>(a, s_red);
     const RecX  ri     = a.rx[cu.iSafe];
-    const float xmassi = a.rt[cu.iSafe].xm;
+    const float xmassi = a.xm[cu.iSafe]; // the dense field (its RecT is rewritten by this kernel's EOS)
     const float xi = relc(ri.x, cu.ox, a.box, 0), yi = relc(ri.y, cu.oy, a.box, 1), zi = relc(ri.z, cu.oz, a.box, 2);
     const float hInv = 1.0f / ri.h, hInv2 = hInv * hInv, h2 = 2.0f * ri.h;
     const bool  own = cu.part == 0; // the self terms go to share 0

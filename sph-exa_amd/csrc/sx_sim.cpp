@@ -2371,7 +2371,8 @@ extern "C"
                 // the fast variant's XMass (or the std density's xmass pass) rides on the filter's final pass
                 const bool fastXm = !sx_ctx_exact_internal(s->ctx);
                 float*     xmOut  = fastXm ? (s->p.propagator == 1 ? s->rho : s->xm) : nullptr;
-                RecT*      rtXm   = (fastXm && s->p.propagator != 1 && H.clusterLists) ? s->rt : nullptr;
+                // no RecT {xm} for the locals: VeDefGradh reads xm from the dense field and writes the records
+                RecT*      rtXm   = nullptr;
                 const int e = skinSearch(s, na, reuse, st, xmOut, rtXm, skc);
                 resync      = e == kSkinResync;
                 if (e && !resync) return e;
