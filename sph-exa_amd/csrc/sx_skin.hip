@@ -15,7 +15,9 @@
  *   4. lanes with nc outside [ng0/4, ngmax+1] update h and walk again (at most 10 updates, the CPU loop's bound); an
  *      updated h must stay within the skin, else the cluster is stale;
  *   5. h, nc, the targets' RecX and the exact lists (ascending positions into U_s, first ngmax in stream order) are
- *      written only by a cluster that completes.
+ *      written only by a cluster that completes;
+ *   4b. (round 6) a walk whose hit bits equal one of the cluster's two recorded list sets keeps that set (no 5), and a
+ *      cluster whose freeze reference proves its hits unchanged is not walked (1b: the XMass over its exact lists).
  * This file is compiled with -ffp-contract=off (the double criterion must round like the reference).
  */
 #include "sx_kernel_poly.hpp"
@@ -697,7 +699,7 @@ __global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(4))) void sk
         {
             a.nc[i] = count + 1; // (a frozen cluster's count is the one in place)
         }
-        if (a.iterateH) a.h[i] = hi;
+        if (a.iterateH && iteration > 0) a.h[i] = hi; // (h changes only by the iteration)
         if (a.rxOut) a.rxOut[i] = RecX{xi, yi, zi, hi, a.m[i]};
         if (a.fresh) a.hb[i] = h0;
         a.rel[i] = di; // 0 for a fresh cluster

@@ -27,6 +27,15 @@
  * Between builds the particle order and the tree are kept (no SFC re-sort: that would renumber the union entries);
  * sx_sim does a full sync + build of every cluster when the stale share or the steps since the last full build pass
  * their limits (SkinState).
+ *
+ * Round 6, what a reuse step may skip (sets, nc and h stay exactly those of the search):
+ *  - KEPT: a cluster's exact lists are a function of its targets' kept-hit bits (the skin lists are fixed), so a walk
+ *    whose bits equal those recorded with a set of lists (hitMask / hitMaskB) keeps that set: no rank pass, no second
+ *    walk, no list writes.  Two sets per cluster (nloc / nlocB): a lattice's h moves between two shells, and the step
+ *    after a crossing usually returns to the other set;
+ *  - FROZEN: a walk also leaves a lower bound g_i of every skin entry's distance to its target's 2h sphere; while the
+ *    growth of d_i + A_C since that walk plus 2|h_i - h_i,ref| stays below it for every target, no hit can have
+ *    changed (the same drift bound), and the cluster is not walked at all -- the fused XMass runs over the exact lists.
  */
 #pragma once
 
