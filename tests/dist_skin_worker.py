@@ -71,7 +71,8 @@ def main():
             out[f"s{s}_{tag}_dt"] = np.array([sim.scalars()["minDt"]])
             out[f"s{s}_{tag}_egrav"] = np.array([sim.conserved()["egrav"]])
         ks = a.skin_stats()
-        out[f"s{s}_skin"] = np.array([ks[k] for k in SKIN] + [ks["factor"], ks["next_factor"]], np.float64)
+        out[f"s{s}_skin"] = np.array([ks[k] for k in SKIN] + [ks["factor"], ks["next_factor"], ks["kept_clusters"],
+                                                             ks["frozen_clusters"]], np.float64)
         out[f"s{s}_layout"] = np.array(list(a.layout().values()), np.int64)
     np.savez(os.path.join(args.out, f"rank{rank}.npz"), **out)
     a.close()

@@ -66,8 +66,13 @@ def test_distributed_skin_equals_fresh_search(tmp_path, nproc, port, ic, side, s
         for col in (0, 1, 4, 5, 6, 7):  # builds, reuse steps, plain steps, resyncs, skin factor, next factor
             assert np.all(sk[:, col] == sk[0, col]), (s, col, sk[:, col])
     last = np.array([d[f"s{steps - 1}_skin"] for d in ranks])
-    print(ic, nproc, side, skin, dict(zip(SKIN, last[0][:6])), "stale per rank", last[:, 2])
+    kept, frozen = int(last[:, 8].sum()), int(last[:, 9].sum())  # clusters whose lists were kept (of them frozen)
+    print(ic, nproc, side, skin, dict(zip(SKIN, last[0][:6])), "stale per rank", last[:, 2], "kept", kept,
+          "frozen", frozen)
     assert last[0][SKIN.index("reuse_steps")] > 0, last[0]
+    if ic == "sedov":
+        # the lattice outside the blast: steps whose hits match a recorded list set keep it on every rank's clusters
+        assert kept > 0, last
 
 
 @pytest.mark.parametrize("nproc,port,side", [(2, 29656, 20), (3, 29657, 22)])
