@@ -163,6 +163,16 @@ def sedov_state(side):
     return st, make_box(-r, r, True)
 
 
+def pbc_wave_state(side, eps=0.3):
+    """periodic self-gravity test IC: the Sedov lattice (periodic box [-0.5, 0.5]^3, total mass 1) at its ambient
+    temperature, the particle masses modulated by 1 + eps sin(2 pi x): a density wave whose periodic field is
+    g_x = (4 pi G eps / k) cos(k x), k = 2 pi (Poisson's equation with the mean density removed, as the Ewald sum does)"""
+    st, box = sedov_state(side)
+    st.temp[:] = np.float64(st.temp.min())
+    st.m[:] = (st.m.astype(np.float64) * (1.0 + eps * np.sin(2.0 * math.pi * st.x))).astype(np.float32)
+    return st, box
+
+
 def noh_state(side):
     """Noh substitute: side^3 lattice in [-0.5,0.5]^3 cut to r<=0.5, open box,
     v = -r_hat, x_m1 = v dt0, T = 1e-20/cv, dt0 = 1e-4 (noh_init.hpp:46-100 field values)."""

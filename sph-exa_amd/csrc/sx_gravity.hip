@@ -827,24 +827,35 @@ __global__ void cellMomentsKernel(const double* x, const double* y, const double
 }
 
 //! one wave per remote cell: near[k] = 1 if the cell violates the vector MAC for any target box (c, s: center and
-//! half-size, stride 8 doubles) -- such a cell's particles are needed as gravity halos
-__global__ void cellNearKernel(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near)
+//! half-size, stride 8 doubles) -- such a cell's particles are needed as gravity halos.  PBC: the smallest distance
+//! over the images shifted by -1, 0, +1 box lengths is taken per axis (the squared distance is a sum of per-axis
+//! terms, so this is the minimum over all 27 images), and the MAC radius is widened by a relative 1e-9: a cell at
+//! the acceptance boundary becomes near, never a far leaf that the image walk's own test (other rounding) opens
+__global__ void cellNearKernel(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near,
+                               double L0, double L1, double L2, int pbc)
 {
     const int k    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (k >= nCells) return;
     const GCell& g   = cells[k];
     bool         hit = false;
+    const double mac2 = pbc ? g.mac2 * (1.0 + 1e-9) : g.mac2;
     if (g.mac2 != 0.0)
         for (int b = lane; b < nBoxes && !hit; b += 64)
         {
             const double* B  = boxes + 8 * (size_t)b;
-            double        d0 = fabs(B[0] - g.com[0]) - B[3], d1 = fabs(B[1] - g.com[1]) - B[4],
-                   d2 = fabs(B[2] - g.com[2]) - B[5];
+            double        a0 = fabs(B[0] - g.com[0]), a1 = fabs(B[1] - g.com[1]), a2 = fabs(B[2] - g.com[2]);
+            if (pbc)
+            {
+                a0 = fmin(a0, fabs(L0 - a0));
+                a1 = fmin(a1, fabs(L1 - a1));
+                a2 = fmin(a2, fabs(L2 - a2));
+            }
+            double d0 = a0 - B[3], d1 = a1 - B[4], d2 = a2 - B[5];
             d0 = d0 > 0 ? d0 : 0;
             d1 = d1 > 0 ? d1 : 0;
             d2 = d2 > 0 ? d2 : 0;
-            hit = d0 * d0 + (d1 * d1 + d2 * d2) < g.mac2;
+            hit = d0 * d0 + (d1 * d1 + d2 * d2) < mac2;
         }
     const bool any = __ballot(hit) != 0;
     if (lane == 0) near[k] = any ? 1u : 0u;
@@ -929,10 +940,46 @@ hipError_t farRefreshBoxes(const GravArgs& a, const GCell* cells, const uint32_t
     return hipGetLastError();
 }
 
-hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near, hipStream_t s)
+hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near, hipStream_t s,
+                         const double* boxL)
 {
-    if (nCells > 0) cellNearKernel<<<grid((size_t)nCells * 64), 256, 0, s>>>(cells, nCells, boxes, nBoxes, near);
+    if (nCells > 0)
+        cellNearKernel<<<grid((size_t)nCells * 64), 256, 0, s>>>(cells, nCells, boxes, nBoxes, near,
+                                                                 boxL ? boxL[0] : 0.0, boxL ? boxL[1] : 0.0,
+                                                                 boxL ? boxL[2] : 0.0, boxL ? 1 : 0);
     return hipGetLastError();
+}
+
+void combineRoots(const double cN[4], const float mN[8], const double cF[4], const float mF[8], double c[4], float m[8])
+{
+    // CombineSourceCenter over the two roots (weights: their masses), then the M2M of upsweepMultipolesKernel
+    const double  wN = (double)mN[0], wF = (double)mF[0], W = wN + wF;
+    const double  inv = W != 0.0 ? 1.0 / W : 0.0;
+    for (int d = 0; d < 3; ++d)
+        c[d] = (wN * cN[d] + wF * cF[d]) * inv;
+    c[3] = W;
+    float         comp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const double* Xi[2]   = {cN, cF};
+    const float*  add[2]  = {mN, mF};
+    for (int k = 0; k < 2; ++k)
+    {
+        if (add[k][0] == 0.0f) continue; // an empty tree (all cells near, or no locals): its center is meaningless
+        const float* q  = add[k];
+        double       rx = c[0] - Xi[k][0], ry = c[1] - Xi[k][1], rz = c[2] - Xi[k][2];
+        double       rx_2 = rx * rx, ry_2 = ry * ry, rz_2 = rz * rz;
+        double       r_2  = (rx_2 + ry_2 + rz_2) * (1.0 / 3.0);
+        double       ml   = (double)(q[0] * 3);
+        comp[7]           = (float)((double)(comp[7] + q[7]) + ml * r_2);
+        comp[0] += q[0];
+        comp[1] = (float)((double)comp[1] + ((double)q[1] + ml * (rx_2 - r_2)));
+        comp[2] = (float)((double)comp[2] + ((double)q[2] + ml * rx * ry));
+        comp[3] = (float)((double)comp[3] + ((double)q[3] + ml * rx * rz));
+        comp[4] = (float)((double)comp[4] + ((double)q[4] + ml * (ry_2 - r_2)));
+        comp[5] = (float)((double)comp[5] + ((double)q[5] + ml * ry * rz));
+        comp[6] = (float)((double)comp[6] + ((double)q[6] + ml * (rz_2 - r_2)));
+    }
+    for (int k = 0; k < 8; ++k)
+        m[k] = comp[k];
 }
 
 hipError_t farTreeLeafMap(const GravArgs& a, hipStream_t s)

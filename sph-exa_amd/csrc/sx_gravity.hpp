@@ -61,9 +61,15 @@ static_assert(sizeof(GCell) == 96, "GCell layout");
 hipError_t cellMoments(const double* x, const double* y, const double* z, const float* m, const uint32_t* cellBeg,
                        const uint32_t* cellIds, int nCells, const int32_t* farLeafToNode, const double* geoC,
                        const double* geoS, float invTheta, GCell* out, hipStream_t s, bool drift = false);
-//! near[k] = 1 if cell k violates the vector MAC for any of the target boxes (center[3], half-size[3], stride 8)
+//! near[k] = 1 if cell k violates the vector MAC for any of the target boxes (center[3], half-size[3], stride 8).
+//! boxL (nullable): a periodic box's lengths -- the test covers the cell's images shifted by -1, 0, +1 box lengths
+//! per axis (the image walk's numShells = 1), with a relative margin on the near side
 hipError_t cellNearFlags(const GCell* cells, int nCells, const double* boxes, int nBoxes, uint32_t* near,
-                         hipStream_t s);
+                         hipStream_t s, const double* boxL = nullptr);
+//! the global root expansion of the two source trees of a rank (near: locals + gravity halos, far: far cells), each
+//! source counted once: mass center and M2M of the two roots as upsweepMultipoles combines children, on the host
+void combineRoots(const double cN[4], const float mN[8], const double cF[4], const float mF[8], double c[4],
+                  float m[8]);
 //! a.leafToNode of a tree (leaf index -> node index)
 hipError_t farTreeLeafMap(const GravArgs& a, hipStream_t s);
 //! far tree (uniform level-6 octree): leaves of the cells with far[k] set carry their moments, all others are

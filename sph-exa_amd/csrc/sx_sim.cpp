@@ -1268,6 +1268,29 @@ bool syncErrFailed(sx_sim* s)
     return h && *h != 0;
 }
 
+/*! the Ewald correction of periodic self-gravity (gravity_wrapper.hpp:135-157) for the locals [first, last), from the
+ *  global root expansion (c4: mass center, m8: quadrupole) with the reference's EwaldSettings defaults (ewald.h:17-21)
+ *  and the walk's one image shell; the box is a cube (checked by sx_sim_create) */
+int ewaldStep(sx_sim* s, const double c4[4], const float m8[8], const uint8_t* active, hipStream_t st)
+{
+    EwaldArgs           ea{};
+    std::vector<double> hs;
+    const double        L = s->box.lim[1] - s->box.lim[0];
+    if (ewaldInit(ea.p, hs, c4, m8, L, 1, 2.6, 2.8, 2.0, 3.0e-3)) return SX_ERR_ARG;
+    double* hd = s->work.get<double>("ewald.hsum", std::max<size_t>(hs.size(), 5));
+    if (!hd) return SX_ERR_NOMEM;
+    SIM_HIP(hipMemcpyAsync(hd, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    ea.first = (uint32_t)s->first, ea.last = (uint32_t)s->last;
+    ea.x = s->x, ea.y = s->y, ea.z = s->z, ea.m = s->m;
+    ea.ax = s->ax, ea.ay = s->ay, ea.az = s->az;
+    ea.active = active;
+    ea.G = (float)s->p.g, ea.hsum = hd, ea.usum = &s->sc->egrav, ea.uscale = 0.5 * (double)ea.G;
+    SIM_HIP(ewaldCorrection(ea, st));
+    // the host table must outlive the copy
+    SIM_HIP(hipStreamSynchronize(st));
+    return SX_OK;
+}
+
 /*! Self-gravity with several ranks (replaces syncGrav + MultipoleHolder::upsweep/traverse of the reference,
  *  domain.hpp:246-372, multipole_holder.cuh:40-66, and the global multipole exchange of
  *  ryoanji/interface/global_multipole.hpp).  Sources are split by level-6 SFC cells, each owned by one rank (the
@@ -1289,6 +1312,9 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool dr
     const size_t   nl = s->last - s->first;
     const float    invTheta = 1.0f / s->p.theta;
     const size_t   nCellsAll = size_t(1) << kHistBits;
+    // periodic self-gravity: both walks over the one image shell of the single-rank path (gravity_wrapper.hpp:135-157)
+    const bool     pbc = periodicGravity(s);
+    const double   boxL[3] = {s->box.lim[1] - s->box.lim[0], s->box.lim[3] - s->box.lim[2], s->box.lim[5] - s->box.lim[4]};
 
     // --- far tree: uniform level-6 octree (one synthetic key per cell, bucket 1), built once
     if (s->farTree.numLeaves != (int)nCellsAll)
@@ -1368,7 +1394,8 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool dr
     uint32_t*     farF    = W.get<uint32_t>("g.far", nAll + 1);
     uint32_t*     reqF    = W.get<uint32_t>("g.reqFlag", nAll + 1);
     uint32_t*     reqS    = W.get<uint32_t>("g.reqScan", nAll + 1);
-    SIM_HIP(cellNearFlags(all, (int)nAll, reinterpret_cast<const double*>(boxes), (int)nChunks, nearF, st));
+    SIM_HIP(cellNearFlags(all, (int)nAll, reinterpret_cast<const double*>(boxes), (int)nChunks, nearF, st,
+                          pbc ? boxL : nullptr));
     nearToFarKernel<<<grid(nAll + 1), 256, 0, st>>>(nearF, nAll, farF, reqF);
     tmpB = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpB, reqF, reqS, (int)nAll + 1, st);
@@ -1487,7 +1514,13 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool dr
     ga.egrav = &s->sc->egrav;
     ga.err   = &s->sc->gravErr;
     ga.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
-    ga.interactions = s->gravCount ? s->work.get<unsigned long long>("grav.inter", 2) : nullptr;
+    ga.interactions = s->gravCount && !pbc ? s->work.get<unsigned long long>("grav.inter", 2) : nullptr;
+    if (pbc)
+    {
+        ga.numShells = 1;
+        for (int d = 0; d < 3; ++d)
+            ga.boxL[d] = boxL[d];
+    }
     SIM_HIP(gravityUpsweep(ga, s->nearTree.levelRangeHost.data(), st));
     ga.waveE = s->work.get<double>("grav.waveE", (ga.last - ga.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(ga, st));
@@ -1515,6 +1548,9 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool dr
     fa.err   = &s->sc->gravErr;
     fa.fast  = sx_ctx_exact_internal(s->ctx) ? 0 : 1;
     fa.interactions = ga.interactions;
+    fa.numShells    = ga.numShells;
+    for (int d = 0; d < 3; ++d)
+        fa.boxL[d] = ga.boxL[d];
     if (drift)
     {
         double* c3 = s->farMem.get<double>("far.geoC", 3 * (size_t)s->farTree.numNodes);
@@ -1527,6 +1563,20 @@ int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool dr
     SIM_HIP(farUpsweep(fa, all, farF, (int)nAll, s->farTree.levelRangeHost.data(), st));
     fa.waveE = s->work.get<double>("grav.waveE", (fa.last - fa.first + kWave - 1) / kWave + 1);
     SIM_HIP(gravityTraverse(fa, st));
+    if (pbc)
+    {
+        // the Ewald correction from the global root: the near tree (locals + near cells) and the far tree (far cells)
+        // together hold every source once
+        double cN[4], cF[4], c4[4];
+        float  mN[8], mF[8], m8[8];
+        SIM_HIP(hipMemcpyAsync(cN, ga.centers4, sizeof(cN), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipMemcpyAsync(mN, ga.multipoles, sizeof(mN), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipMemcpyAsync(cF, fa.centers4, sizeof(cF), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipMemcpyAsync(mF, fa.multipoles, sizeof(mF), hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipStreamSynchronize(st));
+        combineRoots(cN, mN, cF, mF, c4, m8);
+        if (int e = ewaldStep(s, c4, m8, active, st)) return e;
+    }
     s->gravHalos       = nLow + nHigh;
     s->gravRemoteCells = nAll;
     s->gravFarCells    = nAll - (reqOff.empty() ? 0 : hwReq);
@@ -1980,8 +2030,6 @@ extern "C"
     int sx_sim_set_comm(sx_sim* s, sx_comm* c)
     {
         sx::Transport* T = sx_comm_transport_internal(c);
-        // periodic self-gravity runs on one rank only (the multi-rank far field has no image walk)
-        if (periodicGravity(s) && T && T->size() > 1) return SX_ERR_ARG;
         if (T && T->size() > 1)
         {
             // the sync's small per-rank buffers, allocated here so that no rank fails alone between two collectives
@@ -2711,24 +2759,12 @@ extern "C"
             SIM_HIP(gravityTraverse(ga, st));
             if (pbc)
             {
-                double c4[4]; // (cubic box: checked by sx_sim_create)
+                double c4[4];
                 float  m8[8];
                 SIM_HIP(hipMemcpyAsync(c4, ga.centers4, sizeof(c4), hipMemcpyDeviceToHost, st));
                 SIM_HIP(hipMemcpyAsync(m8, ga.multipoles, sizeof(m8), hipMemcpyDeviceToHost, st));
                 SIM_HIP(hipStreamSynchronize(st));
-                EwaldArgs ea{};
-                std::vector<double> hs;
-                if (ewaldInit(ea.p, hs, c4, m8, ga.boxL[0], 1, 2.6, 2.8, 2.0, 3.0e-3)) return SX_ERR_ARG;
-                double* hd = s->work.get<double>("ewald.hsum", std::max<size_t>(hs.size(), 5));
-                if (!hd) return SX_ERR_NOMEM;
-                SIM_HIP(hipMemcpyAsync(hd, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, st));
-                ea.first = ga.first, ea.last = ga.last;
-                ea.x = s->x, ea.y = s->y, ea.z = s->z, ea.m = s->m;
-                ea.ax = s->ax, ea.ay = s->ay, ea.az = s->az;
-                ea.G = ga.G, ea.hsum = hd, ea.usum = &s->sc->egrav, ea.uscale = 0.5 * (double)ga.G;
-                SIM_HIP(ewaldCorrection(ea, st));
-                // the host table must outlive the copy
-                SIM_HIP(hipStreamSynchronize(st));
+                if (int e = ewaldStep(s, c4, m8, nullptr, st)) return e;
             }
             }
             maxAccSq(s, st);

@@ -222,7 +222,13 @@ int halosOutgrown(sx_sim* s, hipStream_t st, unsigned& flag);
 //! targets
 //! drift: a skin-list reuse step (particles may have left the cells and request boxes of the last sync): the near/far
 //! split takes request boxes of the current positions and every MAC box holds its cell and its particles
+//! In a periodic box the near tree and the far tree are both walked over the one image shell, the near/far split
+//! takes the cells' images into account, and the Ewald correction uses the two trees' combined root.
 int distributedGravity(sx_sim* s, hipStream_t st, const uint8_t* active, bool drift = false);
+//! self-gravity with periodic images: the box is periodic (all axes, checked by sx_sim_create) and G != 0
+bool periodicGravity(const sx_sim* s);
+//! the Ewald correction onto ax, ay, az of the locals from the global root expansion (center c4, quadrupole m8)
+int ewaldStep(sx_sim* s, const double c4[4], const float m8[8], const uint8_t* active, hipStream_t st);
 //! max |a|^2 of the locals into the device scalars (accelerationTimestep)
 void maxAccSq(sx_sim* s, hipStream_t st);
 

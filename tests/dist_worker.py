@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--backend", default="host")
     ap.add_argument("--side", type=int, default=16)
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--ic", default="sedov", help="sedov | sedov_dev | noh | evrard (self-gravity, G = 1)")
+    ap.add_argument("--ic", default="sedov",
+                    help="sedov | sedov_dev | noh | evrard (self-gravity, G = 1) | pbc_wave (periodic self-gravity, G = 1)")
     ap.add_argument("--std", action="store_true", help="std propagator (HydroProp)")
     ap.add_argument("--no-overlap", action="store_true", help="serial halo exchanges (no interior/boundary split)")
     ap.add_argument("--av-clean", action="store_true", help="avClean momentum (dV halos)")
@@ -44,12 +45,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ctx = sx.Context(0 if args.backend == "host" else local)
     comm = sx.Comm(args.backend)
-    ic = {"evrard": po.evrard_state, "noh": po.noh_state}.get(args.ic, po.sedov_state)
+    ic = {"evrard": po.evrard_state, "noh": po.noh_state, "pbc_wave": po.pbc_wave_state}.get(args.ic, po.sedov_state)
     st, obox = ic(args.side)
     if args.ic in ("evrard", "noh"):
         po.converge_h(po.load_oracle(), st, obox)  # these ICs' h would iterate (and may not converge) in the first search
     box = sx.make_box(list(obox.lim), list(obox.bnd))
-    g = args.g if args.g is not None else (1.0 if args.ic == "evrard" else 0.0)
+    g = args.g if args.g is not None else (1.0 if args.ic in ("evrard", "pbc_wave") else 0.0)
     params = sx.default_params(g=g, std=args.std, av_clean=args.av_clean,
                                bdt=args.bdt)
     sim = sx.Sim(ctx, 2 * st.n // size + 4096, box, params=params)
