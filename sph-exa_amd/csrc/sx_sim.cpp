@@ -1874,8 +1874,8 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         uint32_t f = 0;
         SIM_HIP(hipMemcpyAsync(&f, na.stats, 4, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
-        fprintf(stderr, "skin: reuse %d s %.3f clusters %u stale %u exact %u flags 0x%x mode %d\n", (int)reuse,
-                K.built, ncl, n1 + nd, n2, f, s->nsPolicy.mode);
+        fprintf(stderr, "skin: reuse %d s %.3f clusters %u stale %u exact %u (direct %u) flags 0x%x mode %d\n",
+                (int)reuse, K.built, ncl, n1 + nd, n2, nd, f, s->nsPolicy.mode);
     }
     return SX_OK;
 }
