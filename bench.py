@@ -406,7 +406,7 @@ def main():
         el = float(t.item())
     stats = sim.stats()
     skin = {k: (v - skin0[k] if k in ("builds", "reuse_steps", "stale_clusters", "exact_clusters", "plain_steps",
-                                      "kept_clusters", "frozen_clusters") else v)
+                                      "kept_clusters", "frozen_clusters", "early_exact") else v)
             for k, v in sim.skin_stats().items()}  # the timed steps'
     if args.skin > 0:
         skin["search_ms_per_step"] = search_ms

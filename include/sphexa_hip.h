@@ -517,9 +517,10 @@ int    sx_sim_rebuild_lists(sx_sim* sim);
  *  backing off, the current skin's s and the next build's s (both in millionths), reuse steps redone from a full sync
  *  (clusters stale again after their rebuild), clusters of reuse steps whose targets all kept the hits of the last
  *  step, so the filter kept their exact lists in place, of them frozen: no skin entry could have crossed its target's
- *  2h sphere, so their skin lists were not walked}.  A skin that does not outlast
+ *  2h sphere, so their skin lists were not walked, clusters whose exact search ran concurrently with the rebuild of
+ *  the other stale clusters}.  A skin that does not outlast
  *  two steps makes the next build's twice as wide (up to 0.16), then the steps back off to a plain search. */
-int    sx_sim_skin_stats(sx_sim* sim, uint64_t out[13]);
+int    sx_sim_skin_stats(sx_sim* sim, uint64_t out[14]);
 /*! the last step's neighbor lists of the local particles as global indices into the state of sx_sim_fields, row-major
  *  out[(i - first) * ngmax + k] for k < min(nc - 1, ngmax) (device buffer of (last - first) * ngmax words; the lists
  *  the step's pair kernels used, cstone::findNeighbors' layout) */

@@ -1740,7 +1740,8 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint32_t*   ucS   = s->mem.get<uint32_t>("skin.ucount", ncl);
     uint32_t*   l1    = s->mem.get<uint32_t>("skin.l1", ncl + 1);
     uint32_t*   l2    = s->mem.get<uint32_t>("skin.l2", ncl + 1);
-    uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 3);
+    uint32_t*   l3    = s->mem.get<uint32_t>("skin.l3", ncl + 1);
+    uint32_t*   hl    = s->mem.pinned<uint32_t>("skin.host", 4);
     uint8_t*    strk  = s->mem.get<uint8_t>("skin.streak", ncl);
     uint32_t*   hmask = s->mem.get<uint32_t>("skin.hitmask", na.numGroups * (size_t)kSkinMaskWords * kWave);
     uint8_t*    same  = s->mem.get<uint8_t>("skin.same", ncl);
@@ -1752,7 +1753,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
     uint32_t*   ucB   = twoSets ? s->mem.get<uint32_t>("skin.ucountB", ncl) : nullptr;
     uint32_t*   hmB   = twoSets ? s->mem.get<uint32_t>("skin.hitmaskB", na.numGroups * (size_t)kSkinMaskWords * kWave)
                                 : nullptr;
-    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !hl || !strk ||
+    if (!rel || !dx || !dy || !dz || !sloc || !scnt || !hb || !acc || !cells || !ucS || !l1 || !l2 || !l3 || !hl || !strk ||
         !hmask || !same || !frz || (twoSets && (!nlocB || !ucB || !hmB)))
         return SX_ERR_NOMEM;
 
@@ -1829,26 +1830,64 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         b.centers = x.centers = c3;
         b.sizes = x.sizes = s3;
     }
+    // the directly stale clusters' exact search does not depend on the rebuild of the others (disjoint clusters: their
+    // lists, unions, h, nc and records; only the statistics words are shared, reduced again below): with both, it runs
+    // on the auxiliary stream with its own search scratch while the rebuild and its filter run here
+    const bool early = n1 && nd && reuse && s->auxStream && s->evAuxIn && s->evAuxOut && !getenv("SX_SKIN_SERIAL_EXACT");
+    if (early)
+    {
+        NsArgs xd   = x;
+        xd.subset   = l2;
+        xd.work     = s->mem.get<uint32_t>("skin.aux.work", 16);
+        xd.hSave    = s->mem.get<float>("skin.aux.over", ncl + 1);
+        xd.hitMasks = s->mem.get<uint64_t>("skin.aux.masks", searchScratchBytes() / sizeof(uint64_t));
+        if (!xd.work || !xd.hSave || !xd.hitMasks) return SX_ERR_NOMEM;
+        SIM_HIP(hipEventRecord(s->evAuxIn, st));
+        SIM_HIP(hipStreamWaitEvent(s->auxStream, s->evAuxIn, 0));
+        SIM_HIP(findNeighbors(xd, s->auxStream));
+        SIM_HIP(hipEventRecord(s->evAuxOut, s->auxStream));
+    }
+    uint32_t* lx = l2; // the exact search's list below: l2 (the direct clusters, then those stale after the rebuild)
     if (n1)
     {
         b.subset  = l1;
         SIM_HIP(findNeighbors(b, st));
         fa.fresh  = 1;
         fa.list   = l1;
-        fa.stale  = l2; // appended after the direct ones
+        // appended after the direct ones, or (their search already running) a list of their own
+        if (early) SIM_HIP(hipMemsetAsync(l3, 0, 4, st));
+        fa.stale  = early ? l3 : l2;
         fa.streak = nullptr;
         fa.direct = nullptr;
         SIM_HIP(skinFilter(fa, ncl, st));
-        SIM_HIP(hipMemcpyAsync(hl + 2, l2, 4, hipMemcpyDeviceToHost, st));
+        SIM_HIP(hipMemcpyAsync(hl + 2, fa.stale, 4, hipMemcpyDeviceToHost, st));
         SIM_HIP(hipStreamSynchronize(st));
         n2 = hl[2];
     }
+    uint32_t n3 = 0; // early: the clusters stale after the rebuild (l3), searched below
+    if (early)
+    {
+        n3 = n2, n2 = nd + n3, lx = l3;
+        K.earlyExact += nd;
+        SIM_HIP(hipStreamWaitEvent(st, s->evAuxOut, 0));
+    }
     out.exact = n2;
     {
+        if (early ? n3 : n2)
+        {
+            x.subset = lx;
+            SIM_HIP(findNeighbors(x, st));
+        }
+        if (early)
+        {
+            // one list of every exact-search cluster (XMass, skinMarkStale): l3's entries after the direct ones
+            if (n3) SIM_HIP(hipMemcpyAsync(l2 + 1 + nd, l3 + 1, 4 * (size_t)n3, hipMemcpyDeviceToDevice, st));
+            hl[3] = n2;
+            SIM_HIP(hipMemcpyAsync(l2, hl + 3, 4, hipMemcpyHostToDevice, st));
+            SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
+        }
         if (n2)
         {
-            x.subset = l2;
-            SIM_HIP(findNeighbors(x, st));
             if (reuse)
             {
                 // on a reuse step the walk takes the drifted tree's refreshed boxes, which overlap: should the exact
@@ -2006,6 +2045,9 @@ extern "C"
         (void)hipEventCreateWithFlags(&s->evProd, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evComm, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evStats, hipEventDisableTiming);
+        if (hipStreamCreateWithFlags(&s->auxStream, hipStreamNonBlocking) != hipSuccess) s->auxStream = nullptr;
+        (void)hipEventCreateWithFlags(&s->evAuxIn, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&s->evAuxOut, hipEventDisableTiming);
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};
         (void)hipMemcpy(s->sc, &init, sizeof(Scalars), hipMemcpyHostToDevice);
         *out = s;
@@ -2024,6 +2066,9 @@ extern "C"
         if (s->evComm) (void)hipEventDestroy(s->evComm);
         if (s->evStats) (void)hipEventDestroy(s->evStats);
         if (s->commStream) (void)hipStreamDestroy(s->commStream);
+        if (s->evAuxIn) (void)hipEventDestroy(s->evAuxIn);
+        if (s->evAuxOut) (void)hipEventDestroy(s->evAuxOut);
+        if (s->auxStream) (void)hipStreamDestroy(s->auxStream);
         delete s;
     }
 
@@ -2081,14 +2126,14 @@ extern "C"
         return SX_OK;
     }
 
-    int sx_sim_skin_stats(sx_sim* s, uint64_t out[13])
+    int sx_sim_skin_stats(sx_sim* s, uint64_t out[14])
     {
         if (!s) return SX_ERR_ARG;
         const auto& K = s->skin;
         out[0] = K.builds, out[1] = K.reuseSteps, out[2] = K.staleClusters, out[3] = K.exactClusters;
         out[4] = K.lastStale, out[5] = K.lastExact, out[6] = K.ngmaxS, out[7] = K.plainSteps;
         out[8] = (uint64_t)std::lround(1e6 * K.built), out[9] = (uint64_t)std::lround(1e6 * K.cur);
-        out[10] = K.resyncs, out[11] = K.keptClusters, out[12] = K.frozenClusters;
+        out[10] = K.resyncs, out[11] = K.keptClusters, out[12] = K.frozenClusters, out[13] = K.earlyExact;
         return SX_OK;
     }
 

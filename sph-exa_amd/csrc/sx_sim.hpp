@@ -97,6 +97,7 @@ struct SkinState
     const void *keptNloc{nullptr}, *keptUni{nullptr}, *keptMask{nullptr}, *keptSame{nullptr}, *keptFrz{nullptr},
         *keptNlocB{nullptr};
     uint64_t  keptClusters{0}, frozenClusters{0};
+    uint64_t  earlyExact{0}; // exact-search clusters searched concurrently with the rebuild of the others
     // the step's second set of exact lists (sel == nullptr unless the step's search was the skin filter)
     sx::ListsB lb{};
 };
@@ -180,6 +181,9 @@ struct sx_sim
     hipStream_t commStream{nullptr};
     hipEvent_t  evProd{nullptr}, evComm{nullptr};
     hipEvent_t  evStats{nullptr}; // the search's statistics have reached statsHost
+    // the skin search's exact search of the directly stale clusters, concurrent with the rebuild of the others
+    hipStream_t auxStream{nullptr};
+    hipEvent_t  evAuxIn{nullptr}, evAuxOut{nullptr};
     uint32_t*   clsList{nullptr}; // [interior | boundary] cluster indices (2 x numClusters)
     uint32_t*   clsCount{nullptr};
     uint32_t*   clsHost{nullptr}; // pinned copy of clsCount

@@ -657,7 +657,7 @@ class Sim:
         self.ctx.check(self.L.sx_sim_rebuild_lists(self.h), "rebuild_lists")
 
     def skin_stats(self):
-        out = (C.c_uint64 * 13)()
+        out = (C.c_uint64 * 14)()
         self.ctx.check(self.L.sx_sim_skin_stats(self.h, out), "skin_stats")
         d = dict(zip(["builds", "reuse_steps", "stale_clusters", "exact_clusters", "last_stale", "last_exact",
                       "capacity", "plain_steps"], list(out)[:8]))
@@ -665,6 +665,7 @@ class Sim:
         d["resyncs"] = out[10]
         d["kept_clusters"] = out[11]
         d["frozen_clusters"] = out[12]
+        d["early_exact"] = out[13]
         return d
 
     def neighbor_sets(self):

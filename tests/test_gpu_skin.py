@@ -113,6 +113,61 @@ def test_skin_quiescent_lattice_reuses(ctx):
         sim.close()
 
 
+def _sorted_rows(sim):
+    """the last step's neighbor lists as one array: a row per particle in id order, its neighbor ids sorted and padded
+    with 2^32 - 1 (the vectorized form of Sim.neighbor_sets, for runs of a few 100k particles)"""
+    n, ngmax = sim.size(), int(sim.params.ngmax)
+    buf = sim.ctx.alloc(n * ngmax, np.uint32)
+    try:
+        sim.ctx.check(sim.L.sx_sim_export_neighbors(sim.h, buf.ptr), "export_neighbors")
+        rows = buf.get()[: n * ngmax].reshape(n, ngmax)
+    finally:
+        sim.ctx.free(buf)
+    g = sim.get(["id", "nc"])
+    ids = g["id"].astype(np.uint32)
+    cnt = np.minimum(g["nc"].astype(np.int64) - 1, ngmax)
+    out = np.where(np.arange(ngmax)[None, :] < cnt[:, None], ids[rows], np.uint32(0xFFFFFFFF))
+    out.sort(axis=1)
+    return out[np.argsort(ids)]
+
+
+def test_skin_early_exact_search_equals_fresh_search(ctx):
+    """Noh's infall at 80^3 (268k particles): from step 6 on some clusters are stale on the step after their rebuild
+    and take the exact search on the auxiliary stream, concurrently with the rebuild + filter of the other stale
+    clusters (sx_sim.cpp skinSearch).  Every step's nc and h equal a fresh sync + search's; on each step with such
+    clusters the neighbor sets of all particles do too"""
+    st, obox = po.noh_state(80)
+    box = gutil.box_to_sx(obox)
+    a = sx.Sim(ctx, st.n, box)
+    a.set_skin(0.05, 24)
+    b = sx.Sim(ctx, st.n, box)
+    b.set_skin(0.0, 1)
+    a.set_state(st.arrays, st.minDt, st.minDt_m1)
+    checked = 0
+    try:
+        early0 = 0
+        for s in range(16):
+            g = a.get(STATE)
+            sc = a.scalars()
+            b.set_state(g, sc["minDt"], sc["minDt_m1"])
+            a.step()
+            b.step()
+            ga, gb = a.get(["id", "nc", "h"]), b.get(["id", "nc", "h"])
+            oa, ob = np.argsort(ga["id"]), np.argsort(gb["id"])
+            assert np.array_equal(ga["nc"][oa], gb["nc"][ob]), s
+            assert np.array_equal(ga["h"][oa], gb["h"][ob]), s
+            ks = a.skin_stats()
+            if ks["early_exact"] > early0:
+                assert np.array_equal(_sorted_rows(a), _sorted_rows(b)), s
+                checked += 1
+            early0 = ks["early_exact"]
+        print("noh 80", checked, "steps with early exact searches", a.skin_stats())
+        assert checked >= 2, a.skin_stats()
+    finally:
+        a.close()
+        b.close()
+
+
 def test_skin_frozen_steps_equal_fresh_search(ctx):
     """a lattice at rest: its h follows nc from shell to shell, so the hit sets change together on some steps and stand
     still on others; on those the filter proves from the last walk's margins that no entry can have crossed its 2h
