@@ -1142,7 +1142,9 @@ hipError_t findNeighborsOnce(const NsArgs& a, hipStream_t s)
 {
     if (a.numGroups == 0) return hipSuccess;
     const unsigned clusters = (a.numGroups + kClusterWaves - 1) / kClusterWaves;
-    findNeighborsKernel<<<std::min(searchGrid(), clusters), kCluster, 0, s>>>(a); // a redo list holds <= clusters
+    unsigned       grid     = std::min(searchGrid(), clusters); // a redo list holds <= clusters
+    if (a.maxGrid) grid = std::min(grid, a.maxGrid);
+    findNeighborsKernel<<<grid, kCluster, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -1841,6 +1841,15 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
         xd.work     = s->mem.get<uint32_t>("skin.aux.work", 16);
         xd.hSave    = s->mem.get<float>("skin.aux.over", ncl + 1);
         xd.hitMasks = s->mem.get<uint64_t>("skin.aux.masks", searchScratchBytes() / sizeof(uint64_t));
+        // one workgroup per cluster here, the rest of the resident grid for the rebuild: a persistent rebuild grid
+        // holding every slot would leave this search waiting for it (SX_SKIN_AUX_SHARE=0: both take the whole grid)
+        const char* sh = getenv("SX_SKIN_AUX_SHARE");
+        if (!sh || atoi(sh) != 0)
+        {
+            const unsigned G = searchGrid();
+            xd.maxGrid       = std::min(nd, G / 2);
+            b.maxGrid        = G - xd.maxGrid;
+        }
         if (!xd.work || !xd.hSave || !xd.hitMasks) return SX_ERR_NOMEM;
         SIM_HIP(hipEventRecord(s->evAuxIn, st));
         SIM_HIP(hipStreamWaitEvent(s->auxStream, s->evAuxIn, 0));
@@ -2045,7 +2054,15 @@ extern "C"
         (void)hipEventCreateWithFlags(&s->evProd, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evComm, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evStats, hipEventDisableTiming);
-        if (hipStreamCreateWithFlags(&s->auxStream, hipStreamNonBlocking) != hipSuccess) s->auxStream = nullptr;
+        {
+            // the highest priority: its few workgroups (one per directly stale cluster) are dispatched ahead of the
+            // rebuild's persistent grid instead of sharing the CUs with it (SX_SKIN_AUX_PRIO=0: default priority)
+            int least = 0, greatest = 0;
+            (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+            const char* ap = getenv("SX_SKIN_AUX_PRIO");
+            const int   pr = ap && atoi(ap) == 0 ? least : greatest;
+            if (hipStreamCreateWithPriority(&s->auxStream, hipStreamNonBlocking, pr) != hipSuccess) s->auxStream = nullptr;
+        }
         (void)hipEventCreateWithFlags(&s->evAuxIn, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&s->evAuxOut, hipEventDisableTiming);
         Scalars init{1e-6, 1e-6, 0.0, INFINITY, INFINITY, 0.0, 1e10f, 0, 0.0, 0ull, 0u};

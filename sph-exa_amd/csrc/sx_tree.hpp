@@ -242,6 +242,9 @@ struct NsArgs
     // per-workgroup hit-mask scratch, searchScratchBytes() bytes
     uint32_t*       work;
     uint64_t*       hitMasks;
+    // > 0: at most this many workgroups in the large build's persistent grid (two searches sharing the GPU, sx_sim.cpp
+    // skinSearch); 0: the whole resident grid
+    uint32_t        maxGrid;
     // optional: the targets' final neighbor records {x, y, z, h, m} (the pair kernels' RecX), written by the search
     // for every target it completes, so no separate packing pass is needed for [first, last)
     RecX*           rxOut;
@@ -321,6 +324,8 @@ hipError_t spatialGroups(Arena& arena, uint32_t first, uint32_t last, const doub
 hipError_t findNeighbors(const NsArgs& a, hipStream_t s);
 //! bytes of NsArgs::hitMasks the search needs (both builds' persistent grids)
 size_t     searchScratchBytes();
+//! workgroups of the large build resident on the whole chip (its persistent grid)
+unsigned   searchGrid();
 //! a's list fields (nidx or nloc/uni/ucap), first, last, ngmax and nc select the lists to export
 hipError_t exportNeighbors(const NsArgs& a, uint32_t* out, hipStream_t s);
 hipError_t importNeighbors(uint32_t* nidx, uint32_t first, uint32_t last, uint32_t ngmax, const uint32_t* in,
