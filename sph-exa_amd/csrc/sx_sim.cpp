@@ -1892,8 +1892,7 @@ int skinSearch(sx_sim* s, const NsArgs& na, bool reuse, hipStream_t st, float* x
             // one list of every exact-search cluster (XMass, skinMarkStale): l3's entries after the direct ones
             if (n3) SIM_HIP(hipMemcpyAsync(l2 + 1 + nd, l3 + 1, 4 * (size_t)n3, hipMemcpyDeviceToDevice, st));
             hl[3] = n2;
-            SIM_HIP(hipMemcpyAsync(l2, hl + 3, 4, hipMemcpyHostToDevice, st));
-            SIM_HIP(reduceClusterStats(na.clStats, ncl, na.stats, st));
+            SIM_HIP(hipMemcpyAsync(l2, hl + 3, 4, hipMemcpyHostToDevice, st)); // read by the synchronisation below
         }
         if (n2)
         {
