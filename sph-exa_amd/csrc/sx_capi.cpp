@@ -1132,6 +1132,7 @@ extern "C"
         a.centers4   = centers;
         a.multipoles = multipoles;
         a.invTheta   = 1.0f / theta;
+        a.fast       = c->exact ? 0 : 1; // exact: the reference's sequential leaf sums (bit-identical); fast: per wave
         int32_t lr[kMaxLevel + 2];
         SX_HIP(c, hipMemcpyAsync(lr, tree->levelRange, sizeof(lr), hipMemcpyDeviceToHost, c->stream));
         SX_HIP(c, hipStreamSynchronize(c->stream));

@@ -132,6 +132,82 @@ __global__ void leafP2MKernel(GravArgs a)
         o[k] = gv[k];
 }
 
+//! fast variant of leafCentersKernel + leafP2MKernel in one launch: one wave per leaf, its particles across the lanes
+//! (a leaf holds at most a bucket, 64 here, so usually one pass), the sums in double reduced over the wave; the
+//! quadrupole's sums are rounded to float once instead of after every particle.  A thread per leaf walked its
+//! particles with every lane on another leaf, so the loads never coalesced (Evrard 14.1M: 0.75 + 0.76 ms per step;
+//! two wave kernels: 0.32 + 0.56).  The leaves' multipoles need only their own centers, so they are formed before
+//! the inner nodes' centers and MAC radii.  Same moments to double / float rounding; the exact variant keeps the
+//! reference's sequential order (bit-identical upsweep).
+__device__ __forceinline__ double waveSumD(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void leafMomentsWaveKernel(GravArgs a)
+{
+    const int L    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (L >= a.numLeaves) return; // whole wave
+    const uint32_t b = a.layout[L], e = a.layout[L + 1];
+    const int      node = a.leafToNode[L];
+    // mass center (massCenter<double>): the sums reach every lane (xor reduction)
+    double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    for (uint32_t i = b + lane; i < e; i += 64)
+    {
+        const double w = (double)a.m[i];
+        c0 += w * a.x[i];
+        c1 += w * a.y[i];
+        c2 += w * a.z[i];
+        c3 += w;
+    }
+    c0 = waveSumD(c0), c1 = waveSumD(c1), c2 = waveSumD(c2), c3 = waveSumD(c3);
+    const double invM = (c3 != 0.0) ? 1.0 / c3 : 0.0;
+    const double cx = c0 * invM, cy = c1 * invM, cz = c2 * invM;
+    // quadrupole about it (P2M; the leaf's particles are read again, from cache)
+    double s[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = b + lane; i < e; i += 64)
+    {
+        const double m_i = (double)a.m[i];
+        const double rx = a.x[i] - cx, ry = a.y[i] - cy, rz = a.z[i] - cz;
+        s[0] += m_i;
+        s[1] += rx * rx * m_i;
+        s[2] += rx * ry * m_i;
+        s[3] += rx * rz * m_i;
+        s[4] += ry * ry * m_i;
+        s[5] += ry * rz * m_i;
+        s[6] += rz * rz * m_i;
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        s[k] = waveSumD(s[k]);
+    if (lane == 0)
+    {
+        double* c = a.centers4 + 4 * (size_t)node;
+        c[0] = cx, c[1] = cy, c[2] = cz, c[3] = c3;
+        float gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (b != e)
+        {
+            for (int k = 0; k < 7; ++k)
+                gv[k] = (float)s[k];
+            const float traceQ = gv[1] + gv[4] + gv[6];
+            gv[7]              = traceQ;
+            gv[1]              = 3 * gv[1] - traceQ;
+            gv[4]              = 3 * gv[4] - traceQ;
+            gv[6]              = 3 * gv[6] - traceQ;
+            gv[2] *= 3;
+            gv[3] *= 3;
+            gv[5] *= 3;
+        }
+        float* o = a.multipoles + 8 * (size_t)node;
+        for (int k = 0; k < 8; ++k)
+            o[k] = gv[k];
+    }
+}
+
 //! M2M with addQuadrupole<float, double> over the nodes of one level (upsweepMultipoles, upsweep_cpu.hpp:71-86)
 __global__ void upsweepMultipolesKernel(GravArgs a, int start, int end)
 {
@@ -1013,14 +1089,15 @@ hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipS
 {
     if (a.numNodes <= 0) return hipSuccess;
     leafToNodeKernel<<<grid(a.numNodes), 256, 0, s>>>(a.childOffsets, a.internalToLeaf, a.numNodes, a.leafToNode);
-    leafCentersKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
+    if (a.fast) leafMomentsWaveKernel<<<grid((size_t)a.numLeaves * 64), 256, 0, s>>>(a); // centers + P2M
+    else leafCentersKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
     for (int level = kMaxLevel; level >= 0; --level)
     {
         const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
         if (e > b) upsweepCentersKernel<<<grid(e - b), 256, 0, s>>>(a, b, e);
     }
     setMacKernel<<<grid(a.numNodes), 256, 0, s>>>(a);
-    leafP2MKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
+    if (!a.fast) leafP2MKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
     for (int level = kMaxLevel; level >= 0; --level)
     {
         const int b = levelRangeHost[level], e = levelRangeHost[level + 1];
