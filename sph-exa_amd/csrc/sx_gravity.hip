@@ -132,31 +132,34 @@ __global__ void leafP2MKernel(GravArgs a)
         o[k] = gv[k];
 }
 
-//! fast variant of leafCentersKernel + leafP2MKernel in one launch: one wave per leaf, its particles across the lanes
-//! (a leaf holds at most a bucket, 64 here, so usually one pass), the sums in double reduced over the wave; the
-//! quadrupole's sums are rounded to float once instead of after every particle.  A thread per leaf walked its
-//! particles with every lane on another leaf, so the loads never coalesced (Evrard 14.1M: 0.75 + 0.76 ms per step;
-//! two wave kernels: 0.32 + 0.56).  The leaves' multipoles need only their own centers, so they are formed before
-//! the inner nodes' centers and MAC radii.  Same moments to double / float rounding; the exact variant keeps the
-//! reference's sequential order (bit-identical upsweep).
-__device__ __forceinline__ double waveSumD(double v)
+//! sum over each 16-lane group, in every lane of it
+__device__ __forceinline__ double groupSumD(double v)
 {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o, 64);
+    for (int o = 8; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 16);
     return v;
 }
 
+//! fast variant of leafCentersKernel + leafP2MKernel in one launch: 16 lanes per leaf, its particles across them, the
+//! sums in double reduced over the group; the quadrupole's sums are rounded to float once instead of after every
+//! particle.  A thread per leaf walked its
+//! particles with every lane on another leaf, so the loads never coalesced (Evrard 14.1M: 0.75 + 0.76 ms per step;
+//! 16 lanes per leaf in one launch: 0.16).  The leaves' multipoles need only their own centers, so they are formed before
+//! the inner nodes' centers and MAC radii.  Same moments to double / float rounding; the exact variant keeps the
+//! reference's sequential order (bit-identical upsweep).
+
 __global__ __launch_bounds__(256) void leafMomentsWaveKernel(GravArgs a)
 {
-    const int L    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (L >= a.numLeaves) return; // whole wave
-    const uint32_t b = a.layout[L], e = a.layout[L + 1];
-    const int      node = a.leafToNode[L];
-    // mass center (massCenter<double>): the sums reach every lane (xor reduction)
+    // four leaves per wave, 16 lanes each: a leaf averages a few dozen particles, and the waves' dependent load chains
+    // (leaf range -> particles -> reduction -> their second pass), not the arithmetic, set the time
+    const int L    = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+    const int t    = threadIdx.x & 15;
+    const bool ok  = L < a.numLeaves;
+    const uint32_t b = ok ? a.layout[L] : 0u, e = ok ? a.layout[L + 1] : 0u;
+    // mass center (massCenter<double>): the sums reach every lane of the group (xor reduction)
     double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    for (uint32_t i = b + lane; i < e; i += 64)
+    for (uint32_t i = b + t; i < e; i += 16)
     {
         const double w = (double)a.m[i];
         c0 += w * a.x[i];
@@ -164,12 +167,12 @@ __global__ __launch_bounds__(256) void leafMomentsWaveKernel(GravArgs a)
         c2 += w * a.z[i];
         c3 += w;
     }
-    c0 = waveSumD(c0), c1 = waveSumD(c1), c2 = waveSumD(c2), c3 = waveSumD(c3);
+    c0 = groupSumD(c0), c1 = groupSumD(c1), c2 = groupSumD(c2), c3 = groupSumD(c3);
     const double invM = (c3 != 0.0) ? 1.0 / c3 : 0.0;
     const double cx = c0 * invM, cy = c1 * invM, cz = c2 * invM;
     // quadrupole about it (P2M; the leaf's particles are read again, from cache)
     double s[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = b + lane; i < e; i += 64)
+    for (uint32_t i = b + t; i < e; i += 16)
     {
         const double m_i = (double)a.m[i];
         const double rx = a.x[i] - cx, ry = a.y[i] - cy, rz = a.z[i] - cz;
@@ -183,10 +186,11 @@ __global__ __launch_bounds__(256) void leafMomentsWaveKernel(GravArgs a)
     }
 #pragma unroll
     for (int k = 0; k < 7; ++k)
-        s[k] = waveSumD(s[k]);
-    if (lane == 0)
+        s[k] = groupSumD(s[k]);
+    if (ok && t == 0)
     {
-        double* c = a.centers4 + 4 * (size_t)node;
+        const int node = a.leafToNode[L];
+        double*   c    = a.centers4 + 4 * (size_t)node;
         c[0] = cx, c[1] = cy, c[2] = cz, c[3] = c3;
         float gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (b != e)
@@ -1089,7 +1093,7 @@ hipError_t gravityUpsweep(const GravArgs& a, const int32_t* levelRangeHost, hipS
 {
     if (a.numNodes <= 0) return hipSuccess;
     leafToNodeKernel<<<grid(a.numNodes), 256, 0, s>>>(a.childOffsets, a.internalToLeaf, a.numNodes, a.leafToNode);
-    if (a.fast) leafMomentsWaveKernel<<<grid((size_t)a.numLeaves * 64), 256, 0, s>>>(a); // centers + P2M
+    if (a.fast) leafMomentsWaveKernel<<<grid((size_t)a.numLeaves * 16), 256, 0, s>>>(a); // centers + P2M
     else leafCentersKernel<<<grid(a.numLeaves), 256, 0, s>>>(a);
     for (int level = kMaxLevel; level >= 0; --level)
     {
